@@ -1,0 +1,193 @@
+"""TEST INFRASTRUCTURE ONLY -- ctypes binding of the CPU restatement (the oracle).
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may
+import this module.  The product (orb-slam-system_amd/liborbx.so) never
+touches it.  Parity status: "parity unpinned" vs the reference binary (see
+oracle/orb_oracle.h and DESIGN.md §Oracle).
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "build", "liborb_oracle.so")
+
+KEYPOINT_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"),
+                           ("response", "<f4"), ("octave", "<i4"), ("class_id", "<i4")])
+assert KEYPOINT_DTYPE.itemsize == 28
+
+OO_OK, OO_ERR_ARG, OO_ERR_CELL_ROI, OO_ERR_LEVEL_SIZE, OO_ERR_QUADTREE, OO_ERR_CAPACITY, \
+    OO_ERR_UNSUPPORTED = 0, -1, -2, -3, -4, -5, -6
+
+_lib = None
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", HERE])
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = ctypes.CDLL(LIB_PATH)
+        P = ctypes.c_void_p
+        i, f = ctypes.c_int, ctypes.c_float
+        L.oo_create.restype = P
+        L.oo_create.argtypes = [i, f, i, i, i, i]
+        L.oo_destroy.argtypes = [P]
+        L.oo_get_tables.argtypes = [P, P, P, P, P, P, P]
+        L.oo_extract.argtypes = [P, P, i, i, i, P, i, P, P]
+        L.oo_level_size.argtypes = [P, i, P, P]
+        L.oo_level_pixels.restype = P
+        L.oo_level_pixels.argtypes = [P, i]
+        L.oo_level_candidates.argtypes = [P, i, P, i]
+        L.oo_level_keys.argtypes = [P, i, P, i]
+        L.oo_fast_atan2.restype = f
+        L.oo_fast_atan2.argtypes = [f, f]
+        L.oo_fast_detect.argtypes = [P, i, i, i, i, i, P, i]
+        L.oo_resize_linear.argtypes = [P, i, i, i, P, i, i, i]
+        L.oo_gaussian_blur7.argtypes = [P, i, i, i, P, i]
+        L.oo_gaussian_kernel7.argtypes = [P]
+        L.oo_brief_descriptor.argtypes = [P, i, i, i, f, P]
+        L.oo_descriptor_distance.argtypes = [P, P]
+        L.oo_search_by_bow.argtypes = [i, P, P, P, i, P, P, P, i, P, P, P, i, P, P, P, f, i, P]
+        _lib = L
+    return _lib
+
+
+def _p(a):
+    return None if a is None else a.ctypes.data_as(ctypes.c_void_p)
+
+
+class OracleError(RuntimeError):
+    def __init__(self, code):
+        super().__init__("oracle error %d" % code)
+        self.code = code
+
+
+class Extractor:
+    """CPU restatement of ORB_SLAM2::ORBextractor (ORBextractor.cc:116-515)."""
+
+    def __init__(self, nfeatures, scale_factor, nlevels, ini_th, min_th, cell_guard="strict"):
+        self.nfeatures, self.nlevels = nfeatures, nlevels
+        self._h = lib().oo_create(nfeatures, scale_factor, nlevels, ini_th, min_th,
+                                  1 if cell_guard == "empty" else 0)
+        if not self._h:
+            raise ValueError("bad extractor parameters")
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            lib().oo_destroy(self._h)
+            self._h = None
+
+    def tables(self):
+        L = self.nlevels
+        s, inv, s2, inv2 = (np.zeros(L, np.float32) for _ in range(4))
+        fpl = np.zeros(L, np.int32)
+        umax = np.zeros(16, np.int32)
+        lib().oo_get_tables(self._h, _p(s), _p(inv), _p(s2), _p(inv2), _p(fpl), _p(umax))
+        return dict(scale=s, inv_scale=inv, sigma2=s2, inv_sigma2=inv2, features_per_level=fpl,
+                    umax=umax)
+
+    def extract(self, img):
+        img = np.ascontiguousarray(img, dtype=np.uint8)
+        h, w = img.shape
+        cap = 4 * self.nfeatures + 64 * self.nlevels + 64
+        kps = np.zeros(cap, KEYPOINT_DTYPE)
+        desc = np.zeros((cap, 32), np.uint8)
+        n = ctypes.c_int(0)
+        rc = lib().oo_extract(self._h, _p(img), w, h, w, _p(kps), cap, _p(desc), ctypes.byref(n))
+        if rc != OO_OK:
+            raise OracleError(rc)
+        return kps[:n.value].copy(), desc[:n.value].copy()
+
+    def level(self, l):
+        w, h = ctypes.c_int(), ctypes.c_int()
+        lib().oo_level_size(self._h, l, ctypes.byref(w), ctypes.byref(h))
+        ptr = lib().oo_level_pixels(self._h, l)
+        buf = (ctypes.c_uint8 * (w.value * h.value)).from_address(ptr)
+        return np.frombuffer(buf, np.uint8).reshape(h.value, w.value).copy()
+
+    def candidates(self, l):
+        n = lib().oo_level_candidates(self._h, l, None, 0)
+        out = np.zeros(n, KEYPOINT_DTYPE)
+        lib().oo_level_candidates(self._h, l, _p(out), n)
+        return out
+
+    def level_keys(self, l):
+        n = lib().oo_level_keys(self._h, l, None, 0)
+        out = np.zeros(n, KEYPOINT_DTYPE)
+        lib().oo_level_keys(self._h, l, _p(out), n)
+        return out
+
+
+def fast_atan2(y, x):
+    return lib().oo_fast_atan2(float(y), float(x))
+
+
+def fast_detect(img, threshold, nonmax=True):
+    img = np.ascontiguousarray(img, dtype=np.uint8)
+    h, w = img.shape
+    cap = w * h + 1
+    out = np.zeros(cap, KEYPOINT_DTYPE)
+    n = lib().oo_fast_detect(_p(img), w, h, w, threshold, 1 if nonmax else 0, _p(out), cap)
+    return out[:n].copy()
+
+
+def resize_linear(src, dw, dh):
+    src = np.ascontiguousarray(src, dtype=np.uint8)
+    sh, sw = src.shape
+    dst = np.zeros((dh, dw), np.uint8)
+    lib().oo_resize_linear(_p(src), sw, sh, sw, _p(dst), dw, dh, dw)
+    return dst
+
+
+def gaussian_blur7(src):
+    src = np.ascontiguousarray(src, dtype=np.uint8)
+    h, w = src.shape
+    dst = np.zeros_like(src)
+    lib().oo_gaussian_blur7(_p(src), w, h, w, _p(dst), w)
+    return dst
+
+
+def gaussian_kernel7():
+    k = np.zeros(7, np.int32)
+    lib().oo_gaussian_kernel7(_p(k))
+    return k
+
+
+def brief_descriptor(blurred, cx, cy, angle_deg):
+    blurred = np.ascontiguousarray(blurred, dtype=np.uint8)
+    d = np.zeros(32, np.uint8)
+    lib().oo_brief_descriptor(_p(blurred), blurred.shape[1], cx, cy, float(angle_deg), _p(d))
+    return d
+
+
+def descriptor_distance(a, b):
+    a = np.ascontiguousarray(a, np.uint8)
+    b = np.ascontiguousarray(b, np.uint8)
+    return lib().oo_descriptor_distance(_p(a), _p(b))
+
+
+def search_by_bow(kf1, kf2, nnratio=0.6, check_ori=True):
+    """kf = dict(desc (N,32) u8, angle (N,) f32, valid (N,) u8 or None,
+    node_id (M,) u32 ascending, off (M+1,) u32, feat u32)."""
+    def unpack(k):
+        d = np.ascontiguousarray(k["desc"], np.uint8)
+        a = np.ascontiguousarray(k["angle"], np.float32)
+        v = None if k.get("valid") is None else np.ascontiguousarray(k["valid"], np.uint8)
+        nid = np.ascontiguousarray(k["node_id"], np.uint32)
+        off = np.ascontiguousarray(k["off"], np.uint32)
+        feat = np.ascontiguousarray(k["feat"], np.uint32)
+        return d, a, v, nid, off, feat
+    d1, a1, v1, n1, o1, f1 = unpack(kf1)
+    d2, a2, v2, n2, o2, f2 = unpack(kf2)
+    m = np.full(len(d1), -1, np.int32)
+    nm = lib().oo_search_by_bow(len(d1), _p(d1), _p(a1), _p(v1), len(n1), _p(n1), _p(o1), _p(f1),
+                                len(d2), _p(d2), _p(a2), _p(v2), len(n2), _p(n2), _p(o2), _p(f2),
+                                float(nnratio), 1 if check_ori else 0, _p(m))
+    return m, nm

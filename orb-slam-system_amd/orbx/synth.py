@@ -1,0 +1,62 @@
+"""Deterministic synthetic grayscale frames.
+
+splitmix64 stream, element i of the stream seeded with s is
+``mix(s + (i+1) * 0x9E3779B97F4A7C15)`` (counter form of the sequential
+generator), with ``seed = 0x5EED0000 + frame_idx``.
+
+kinds:
+  rects  horizontal gradient 64->192, then 96 axis-aligned rectangles
+         (stream elements 5r..5r+4: x0, x1, y0, y1 mod W/H, value mod 256; later
+         rectangles overwrite earlier ones; corners inclusive), then additive
+         noise U{-6..6} (element 480 + y*W + x, mod 13, minus 6), clamped.
+  noise  iid U{0..255} (element y*W + x, mod 256).
+  flat   constant 128.
+
+The device generator (`orbx_synth_frames`, csrc/kernels_synth.hip) produces
+the identical bytes; tests/test_gpu_parity.py checks that.
+"""
+import numpy as np
+
+GOLDEN = np.uint64(0x9E3779B97F4A7C15)
+M1 = np.uint64(0xBF58476D1CE4E5B9)
+M2 = np.uint64(0x94D049BB133111EB)
+SEED_BASE = 0x5EED0000
+KINDS = {"rects": 0, "noise": 1, "flat": 2}
+
+
+def _mix(z):
+    z = z.astype(np.uint64, copy=False)
+    with np.errstate(over="ignore"):
+        z = (z ^ (z >> np.uint64(30))) * M1
+        z = (z ^ (z >> np.uint64(27))) * M2
+    return z ^ (z >> np.uint64(31))
+
+
+def stream(seed, start, count):
+    i = np.arange(start + 1, start + count + 1, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        return _mix(np.uint64(seed) + i * GOLDEN)
+
+
+def frame(w, h, frame_idx, kind="rects"):
+    seed = SEED_BASE + frame_idx
+    if kind == "flat":
+        return np.full((h, w), 128, np.uint8)
+    if kind == "noise":
+        return (stream(seed, 0, w * h) % np.uint64(256)).astype(np.uint8).reshape(h, w)
+    if kind != "rects":
+        raise ValueError(kind)
+    x = np.arange(w, dtype=np.int64)
+    bg = 64 + (128 * x) // max(w - 1, 1)
+    img = np.broadcast_to(bg, (h, w)).astype(np.int32).copy()
+    r = stream(seed, 0, 5 * 96).reshape(96, 5)
+    for x0, x1, y0, y1, v in r:
+        x0, x1 = int(x0 % np.uint64(w)), int(x1 % np.uint64(w))
+        y0, y1 = int(y0 % np.uint64(h)), int(y1 % np.uint64(h))
+        img[min(y0, y1):max(y0, y1) + 1, min(x0, x1):max(x0, x1) + 1] = int(v % np.uint64(256))
+    noise = (stream(seed, 480, w * h) % np.uint64(13)).astype(np.int32).reshape(h, w) - 6
+    return np.clip(img + noise, 0, 255).astype(np.uint8)
+
+
+def frames(w, h, first_idx, count, kind="rects"):
+    return np.stack([frame(w, h, first_idx + i, kind) for i in range(count)])
