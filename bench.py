@@ -1,0 +1,227 @@
+#!/usr/bin/env python3
+"""ORB extract+match throughput on MI355X (BASELINE.json metric).
+
+One step = one pass of the hot path over one resident batch of synthetic
+1920x1080 frames per GPU:
+  * ORBextractor on every frame (8-level pyramid, FAST cells, quadtree,
+    orientation, rotated BRIEF) -- orbx_plan_extract;
+  * ORBmatcher::SearchByBoW brute force (one vocabulary node, top-2000
+    keypoints by response) of every frame against its predecessor --
+    orbm_plan_match_frames.  Frames are sharded in contiguous blocks per
+    rank; the first frame of a rank is matched against the last frame of the
+    previous rank (ring), whose keypoints + descriptors arrive through an
+    RCCL all-gather over xGMI (the one real exchange step).
+value = frames processed by all ranks / max-over-ranks wall time.
+
+python bench.py [--gpus N --steps K --warmup W --batch B]
+multi-GPU: python -m torch.distributed.run --nproc-per-node N bench.py --gpus N
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "orb-slam-system_amd"))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=128, help="frames per GPU per step")
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--nfeatures", type=int, default=2000)
+    ap.add_argument("--nlevels", type=int, default=8)
+    ap.add_argument("--topn", type=int, default=2000)
+    ap.add_argument("--kind", default="rects")
+    ap.add_argument("--nnratio", type=float, default=0.75)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"))
+    return ap.parse_args()
+
+
+def stage_bytes(geo, nframes, kps_total, npairs, topn):
+    """Algorithmic bytes per step of each stage."""
+    L = geo.nlevels
+    w, h, alias = geo.level("width"), geo.level("height"), geo.level("alias")
+    P = [w[l] * h[l] for l in range(L)]
+    uniq = [l for l in range(L) if alias[l] == l]
+    resize = sum(P[l] + P[alias[l - 1]] for l in uniq if l > 0)
+    fast = sum(P[l] for l in uniq)
+    blur = 2 * sum(P[l] for l in uniq)
+    brief = 1321 * kps_total  # 749 disk + 512 samples + 60 output bytes per keypoint
+    match = npairs * (2 * topn * 32 + topn * 8)
+    return {"resize": resize * nframes, "fast_cells": fast * nframes, "blur": blur * nframes,
+            "orient_brief": brief, "match_candidates": match}
+
+
+def cpu_baseline(args):
+    """Bounded sample of the same workload on the oracle (1 host core)."""
+    from oracle import oracle as O
+    from orbx import synth
+    O.build()
+    ex = O.Extractor(args.nfeatures, 1.2, args.nlevels, 20, 7, cell_guard="empty")
+    t0 = time.perf_counter()
+    prev = None
+    n = 0
+    while True:
+        img = synth.frame(args.width, args.height, n, args.kind)
+        ts = time.perf_counter()
+        k, d = ex.extract(img)
+        order = sorted(range(len(k)), key=lambda i: (-float(k["response"][i]), i))[:args.topn]
+        sel = np.sort(np.array(order, np.uint32))
+        cur = dict(desc=d, angle=k["angle"], valid=None, node_id=np.array([0], np.uint32),
+                   off=np.array([0, len(sel)], np.uint32), feat=sel)
+        if prev is not None:
+            O.search_by_bow(cur, prev, args.nnratio, True)
+        prev = cur
+        n += 1
+        if time.perf_counter() - t0 >= args.cpu_seconds and n >= 3:
+            break
+        del ts
+    el = time.perf_counter() - t0
+    return {"value": n / el, "unit": "frames/s", "cores": 1, "kind": "port",
+            "sample": "%d synthetic %s %dx%d frames, oracle ORBextractor + top-%d single-node "
+                      "SearchByBoW vs previous frame, single thread (scalar restatement)" %
+                      (n, args.kind, args.width, args.height, args.topn)}
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+    import orbx
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    B, W, H = args.batch, args.width, args.height
+    prm = orbx.params(args.nfeatures, 1.2, args.nlevels, 20, 7, "empty")
+    plan = orbx.Plan(prm, W, H, B, device=local)
+    kcap = plan.kcap
+    mp = orbx.MatchPlan(B, kcap, args.topn, device=local)
+    frames = torch.empty((B, H, W), dtype=torch.uint8, device=dev)
+    orbx.synth_frames(frames, rank * B, args.kind)
+    # exchange buffer: last frame's keypoints (28 B) + descriptors (32 B) + count
+    xbytes = kcap * 60 + 16
+    mine = torch.zeros(xbytes, dtype=torch.uint8, device=dev)
+    gathered = torch.zeros((world, xbytes), dtype=torch.uint8, device=dev)
+    prev_rank = (rank - 1) % world
+
+    def step():
+        plan.extract(frames)
+        if B > 1:
+            mp.match(B - 1, plan.kps[1:], plan.desc[1:], plan.counts[1:], plan.kps, plan.desc,
+                     plan.counts, args.nnratio, True)
+        if world > 1:
+            mine[:kcap * 28].copy_(plan.kps[B - 1].reshape(-1))
+            mine[kcap * 28:kcap * 60].copy_(plan.desc[B - 1].reshape(-1))
+            mine[kcap * 60:kcap * 60 + 4].copy_(plan.counts[B - 1:B].view(torch.uint8))
+            dist.all_gather_into_tensor(gathered.view(-1), mine)
+            src = gathered[prev_rank]
+            kb = src[:kcap * 28].view(1, kcap, 28)
+            db = src[kcap * 28:kcap * 60].view(1, kcap, 32)
+            cb = src[kcap * 60:kcap * 60 + 4].view(torch.int32)
+        else:
+            kb, db, cb = plan.kps[B - 1:], plan.desc[B - 1:], plan.counts[B - 1:]
+        mp.match(1, plan.kps, plan.desc, plan.counts, kb, db, cb, args.nnratio, True,
+                 out_offset=B - 1)
+
+    for _ in range(args.warmup):
+        step()
+    plan.check()
+    torch.cuda.synchronize()
+    plan.set_timing(True)
+    mp.set_timing(True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    plan.check()
+    st = plan.stage_times()
+    mst = mp.stage_times()
+    for k, v in mst.items():
+        if v[1]:
+            st[k] = v
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    kps_total = int(plan.counts[:B].sum().item())
+    nmatch = int(mp.nmatches[:B].sum().item())
+    if rank != 0:
+        if world > 1:
+            dist.destroy_process_group()
+        return
+    frames_total = world * B * args.steps
+    geo = plan.geo
+    by = stage_bytes(geo, B, kps_total, B, args.topn)
+    per_step = {k: st[k][0] / args.steps for k in st if st[k][1]}
+    dom = max(per_step, key=per_step.get)
+    dom_launches = st[dom][1] / args.steps
+    roof = None
+    if dom in by:
+        ach = by[dom] / (per_step[dom] * 1e-3) / 1e9
+        traffic = None
+        if os.path.exists(args.traffic):
+            try:
+                traffic = json.load(open(args.traffic)).get(dom)
+            except Exception:
+                traffic = None
+        roof = {"bound": "hbm", "kernel": dom, "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
+                "bytes_per_step": by[dom], "launches_per_step": dom_launches,
+                "ms_per_step": round(per_step[dom], 4)}
+    out = {
+        "metric": "ORB extract+match frames/sec at %dx%d, %d pyramid levels" % (W, H, args.nlevels),
+        "value": round(frames_total / el, 2),
+        "unit": "frames/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(el / args.steps * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic (orbx/synth.py '%s' frames, seeds 0x5EED0000+idx), resident in HBM" % args.kind,
+        "config": {"workload": "BASELINE config 4: %dx%d %d-level ORBextractor (%d features, "
+                               "cell_guard=empty) + brute-force SearchByBoW top-%d vs previous "
+                               "frame" % (W, H, args.nlevels, args.nfeatures, args.topn),
+                   "frames_per_gpu_per_step": B, "parallelism": "frame-sharded dp%d" % world,
+                   "keypoints_last_batch": kps_total, "matches_last_batch": nmatch},
+        "stages_ms_per_step": {k: round(v, 4) for k, v in per_step.items()},
+        "roofline": roof,
+    }
+    if world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(args)
+    print(json.dumps(out))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,210 @@
+/* orbx.h -- C ABI of the MI355X-native ORB front end (liborbx.so).
+ *
+ * Drop-in boundary for the reference's hot path:
+ *   ORB_SLAM2::ORBextractor   /root/reference/include/ORBextractor.h:25-91
+ *   ORB_SLAM2::ORBmatcher     /root/reference/include/ORBmatcher.h:16-81
+ * Plain C: POD structs, raw pointers, explicit sizes, int status codes, no
+ * exceptions across the boundary, no torch types.  Every compute entry point
+ * runs hand-written HIP kernels on a gfx950 device; there is no CPU path.
+ *
+ * Threading: an orbx_extractor / orbx_plan owns its own HIP stream and
+ * scratch and may be used from one thread at a time; distinct instances may
+ * run concurrently (the reference runs left/right extractors on two threads,
+ * /root/reference/src/Frame.cc:58-61).  Matcher calls are re-entrant.
+ */
+#ifndef ORBX_H
+#define ORBX_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ORBX_ABI_VERSION 1
+
+/* status codes */
+enum {
+  ORBX_OK = 0,
+  ORBX_ERR_ARG = -1,         /* bad argument / image type                               */
+  ORBX_ERR_CELL_ROI = -2,    /* strict cell guard: a FAST cell has negative extent; the
+                                reference throws cv::Exception from cv::Mat(m, Rect) at
+                                src/ORBextractor.cc:328 (1920x1080)      */
+  ORBX_ERR_LEVEL_SIZE = -3,  /* a pyramid level has <= 32 rows (reference divides by 0 at
+                                src/ORBextractor.cc:230) or < 32 cols                     */
+  ORBX_ERR_QUADTREE = -4,    /* DistributeOctTree would never terminate */
+  ORBX_ERR_CAPACITY = -5,    /* caller buffer too small (*n holds the required count)     */
+  ORBX_ERR_UNSUPPORTED = -6, /* exact 2x level ratio (OpenCV switches to INTER_AREA) or a
+                                configuration beyond the kernels' static limits          */
+  ORBX_ERR_HIP = -7,         /* HIP runtime error                                         */
+  ORBX_ERR_NO_DEVICE = -8,   /* no gfx950 device / bad device ordinal                     */
+};
+
+/* ORBextractor constructor arguments (ORBextractor.h:31-32) + switches. */
+typedef struct {
+  int nfeatures;
+  float scale_factor;
+  int nlevels;
+  int ini_th_fast;
+  int min_th_fast;
+  int cell_guard; /* 0 = strict (reference: throw on negative-extent FAST cells),
+                     1 = empty (such cells yield no corners; == upstream ORB-SLAM2 guards) */
+} orbx_params;
+
+/* Layout-identical to cv::KeyPoint (28 bytes): pt.x, pt.y, size, angle,
+ * response, octave, class_id. */
+typedef struct {
+  float x, y, size, angle, response;
+  int32_t octave, class_id;
+} orbx_keypoint;
+
+int orbx_abi_version(void);
+const char* orbx_status_string(int status);
+/* number of visible gfx950 devices (0 on a host without GPU) */
+int orbx_device_count(void);
+
+/* ---------------------------------------------------------------------------
+ * Level geometry and constant tables (host-only, no device needed).
+ * Mirrors ORBextractor::ORBextractor (src/ORBextractor.cc:116-170),
+ * GetScaleFactors() & co. (ORBextractor.h:43-63) and ComputePyramid sizes
+ * (src/ORBextractor.cc:501-502).
+ * ------------------------------------------------------------------------- */
+int orbx_tables(const orbx_params* p, float* scale, float* inv_scale, float* sigma2,
+                float* inv_sigma2, int* features_per_level, int* umax16);
+
+typedef struct {
+  int nlevels;
+  int width[32], height[32];
+  int alias[32];          /* level whose pixels this level shares (level 1 == level 0:
+                             mvScaleFactor[1] == 1)                    */
+  int ncols[32], nrows[32], wcell[32], hcell[32]; /* FAST cell grid (:308-314)        */
+  int ncells_bad[32];     /* cells with negative extent (strict guard -> error)       */
+  int features[32];       /* mnFeaturesPerLevel                                        */
+  int nini[32];           /* DistributeOctTree initial nodes (:230)                    */
+  int kcap_level[32];     /* max keypoints a level can emit                            */
+  int kcap;               /* max keypoints per frame (sum of kcap_level)               */
+  long long pixels;       /* sum of level pixel counts                                 */
+  long long bytes_pyr_fast; /* algorithmic bytes of pyramid + FAST per frame */
+} orbx_geometry;
+
+int orbx_geometry_compute(const orbx_params* p, int width, int height, orbx_geometry* g);
+
+/* Resize coefficient tables for level l (l >= 1, non-alias): xofs[w_l],
+ * alpha[2*w_l], yofs[h_l], beta[2*h_l] (INTER_RESIZE_COEF_BITS = 11). */
+int orbx_resize_tables(const orbx_params* p, int width, int height, int level, int32_t* xofs,
+                       int16_t* alpha, int32_t* yofs, int16_t* beta);
+
+/* ---------------------------------------------------------------------------
+ * ORBextractor drop-in: host image in, host keypoints/descriptors out.
+ * Replaces ORBextractor::operator() (src/ORBextractor.cc:442-495).
+ * ------------------------------------------------------------------------- */
+typedef struct orbx_extractor orbx_extractor;
+
+int orbx_extractor_create(const orbx_params* p, int device, orbx_extractor** out);
+int orbx_extractor_destroy(orbx_extractor* e);
+
+/* Capacity needed for a w x h image (upper bound of the keypoint count). */
+int orbx_extractor_capacity(orbx_extractor* e, int width, int height, int* kcap);
+
+/* operator()(image, mask, keypoints, descriptors): img is CV_8UC1 rows of
+ * `stride` bytes.  On success *n = K; kps[0..K) and desc[0..K*32) hold the
+ * level-major keypoints (level coordinates * mvScaleFactor) and descriptors.
+ * K == 0 leaves kps/desc untouched (reference :460-463).  cap < K returns
+ * ORBX_ERR_CAPACITY with *n = K.  Synchronous. */
+int orbx_extract(orbx_extractor* e, const uint8_t* img, int width, int height, size_t stride,
+                 orbx_keypoint* kps, int cap, uint8_t* desc, int* n);
+
+/* mvImagePyramid[level] of the last orbx_extract (copied D2H on demand). */
+int orbx_extractor_level(orbx_extractor* e, int level, uint8_t* dst, size_t dst_stride,
+                         int* width, int* height);
+
+/* ---------------------------------------------------------------------------
+ * Batched device-resident extraction (the throughput path; bench.py).
+ * ------------------------------------------------------------------------- */
+typedef struct orbx_plan orbx_plan;
+
+int orbx_plan_create(const orbx_params* p, int width, int height, int max_batch, int device,
+                     orbx_plan** out);
+int orbx_plan_destroy(orbx_plan* plan);
+int orbx_plan_geometry(const orbx_plan* plan, orbx_geometry* g);
+
+/* d_frames: nframes images, frame i at d_frames + i*frame_stride, rows of
+ * row_stride bytes (device memory).  Outputs (device memory):
+ *   d_kps  [nframes][kcap], d_desc [nframes][kcap][32], d_counts [nframes].
+ * Asynchronous on `stream` (a hipStream_t; NULL = the plan's own stream).
+ * Device-side failures (quadtree stuck) are latched; read them with
+ * orbx_plan_check(). */
+int orbx_plan_extract(orbx_plan* plan, const uint8_t* d_frames, int nframes, size_t frame_stride,
+                      size_t row_stride, orbx_keypoint* d_kps, uint8_t* d_desc, int* d_counts,
+                      void* stream);
+/* synchronises `stream`, returns and clears the latched device error */
+int orbx_plan_check(orbx_plan* plan, void* stream);
+
+/* Per-stage device timing (HIP events around every launch of a stage). */
+int orbx_stage_count(void);
+const char* orbx_stage_name(int stage);
+int orbx_plan_set_timing(orbx_plan* plan, int enable); /* also resets the accumulators   */
+/* after the stream is synchronised: total ms and launch count per stage */
+int orbx_plan_stage_times(orbx_plan* plan, double* ms, int* launches, int nstages);
+
+/* Device synthetic frames (same bytes as orbx/synth.py): kind 0 rects,
+ * 1 noise, 2 flat; frame i gets seed 0x5EED0000 + first_idx + i. */
+int orbx_synth_frames(uint8_t* d_frames, int width, int height, size_t frame_stride, int nframes,
+                      int first_idx, int kind, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * ORBmatcher drop-in.
+ * ------------------------------------------------------------------------- */
+/* One KeyFrame's matcher inputs.  DBoW2::FeatureVector
+ * (Thirdparty/DBoW2/DBoW2/FeatureVector.h:21-22) flattened: node_id[nnodes]
+ * ascending & unique, node j holds feat[node_off[j] .. node_off[j+1]).
+ * valid[i] != 0 <=> GetMapPointMatches()[i] && !isBad() (NULL = all valid).
+ * angle[i] = mvKeysUn[i].angle. */
+typedef struct {
+  int n;
+  const uint8_t* desc; /* n x 32 */
+  const float* angle;  /* n */
+  const uint8_t* valid;
+  int nnodes;
+  const uint32_t* node_id;
+  const uint32_t* node_off; /* nnodes + 1 */
+  const uint32_t* feat;
+} orbx_bow_frame;
+
+/* ORBmatcher::SearchByBoW(KeyFrame*, KeyFrame*, vector<MapPoint*>&)
+ * (src/ORBmatcher.cc:278-366).  Host inputs; match12[n1] = matched index in
+ * kf2 (vpMatches12[i] = vpMapPoints2[match12[i]]) or -1.  Synchronous. */
+int orbm_search_by_bow(const orbx_bow_frame* kf1, const orbx_bow_frame* kf2, float nnratio,
+                       int check_ori, int device, int32_t* match12, int* nmatches);
+
+/* ORBmatcher::DescriptorDistance (src/ORBmatcher.cc:896-908), batched on the
+ * device: dist[i] = Hamming(a + 32*ia[i], b + 32*ib[i]); host pointers. */
+int orbm_descriptor_distance_batch(const uint8_t* a, int na, const uint8_t* b, int nb,
+                                   const int32_t* ia, const int32_t* ib, int npairs, int device,
+                                   int32_t* dist);
+
+/* Batched device matcher over extractor outputs (bench "extract+match",
+ * BASELINE config 4): pair p matches frame A_p against frame B_p, each
+ * reduced to its top `topn` keypoints by (response desc, index asc) and
+ * placed in ONE vocabulary node in ascending index order (brute force).
+ * match12 rows are indexed by keypoint index of frame A (cap kcap), value =
+ * keypoint index in frame B or -1.  Frame p of side A is d_kps_a + p*kcap,
+ * d_desc_a + p*kcap*32, d_count_a[p] (side B likewise), i.e. the layout of
+ * orbx_plan_extract outputs; d_match12 is [npairs][kcap], d_nmatches
+ * [npairs].  Asynchronous on `stream`. */
+typedef struct orbm_plan orbm_plan;
+int orbm_plan_create(int max_pairs, int kcap, int topn, int device, orbm_plan** out);
+int orbm_plan_destroy(orbm_plan* mp);
+int orbm_plan_match_frames(orbm_plan* mp, int npairs, const orbx_keypoint* d_kps_a,
+                           const uint8_t* d_desc_a, const int* d_count_a,
+                           const orbx_keypoint* d_kps_b, const uint8_t* d_desc_b,
+                           const int* d_count_b, float nnratio, int check_ori,
+                           int32_t* d_match12, int* d_nmatches, void* stream);
+int orbm_plan_set_timing(orbm_plan* mp, int enable);
+int orbm_plan_stage_times(orbm_plan* mp, double* ms, int* launches, int nstages);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ORBX_H */

@@ -1,0 +1,98 @@
+// api_common.h -- host helpers shared by the C-ABI translation units.
+#ifndef ORBX_API_COMMON_H
+#define ORBX_API_COMMON_H
+
+#include <hip/hip_runtime.h>
+
+#include <vector>
+
+#include "../../include/orbx.h"
+
+#define ORBX_TRY(expr)                              \
+  do {                                              \
+    if ((expr) != hipSuccess) return ORBX_ERR_HIP;  \
+  } while (0)
+
+enum {
+  ORBX_STAGE_RESIZE = 0,
+  ORBX_STAGE_FAST,
+  ORBX_STAGE_QUADTREE,
+  ORBX_STAGE_BLUR,
+  ORBX_STAGE_BRIEF,
+  ORBX_STAGE_MSELECT,
+  ORBX_STAGE_MCAND,
+  ORBX_STAGE_MRESOLVE,
+  ORBX_STAGE_MFINAL,
+  ORBX_NSTAGES
+};
+
+namespace orbx {
+
+// HIP events recorded around every launch group of a stage, on the stream
+// the kernels run on.  collect() must be called after that stream is idle.
+struct StageTimer {
+  bool enabled = false;
+  struct Rec {
+    int stage;
+    hipEvent_t a, b;
+  };
+  std::vector<Rec> recs;
+  std::vector<hipEvent_t> pool;
+  hipEvent_t pending[ORBX_NSTAGES] = {};
+
+  hipEvent_t get() {
+    if (!pool.empty()) {
+      hipEvent_t e = pool.back();
+      pool.pop_back();
+      return e;
+    }
+    hipEvent_t e = nullptr;
+    hipEventCreate(&e);
+    return e;
+  }
+  void begin(int stage, hipStream_t s) {
+    if (!enabled) return;
+    pending[stage] = get();
+    hipEventRecord(pending[stage], s);
+  }
+  void end(int stage, hipStream_t s) {
+    if (!enabled || !pending[stage]) return;
+    hipEvent_t b = get();
+    hipEventRecord(b, s);
+    recs.push_back({stage, pending[stage], b});
+    pending[stage] = nullptr;
+  }
+  void reset(bool en) {
+    for (auto& r : recs) {
+      pool.push_back(r.a);
+      pool.push_back(r.b);
+    }
+    recs.clear();
+    enabled = en;
+  }
+  int collect(double* ms, int* launches, int n) {
+    for (int i = 0; i < n; ++i) {
+      if (ms) ms[i] = 0;
+      if (launches) launches[i] = 0;
+    }
+    for (auto& r : recs) {
+      float t = 0;
+      if (hipEventElapsedTime(&t, r.a, r.b) != hipSuccess) return ORBX_ERR_HIP;
+      if (r.stage < n) {
+        if (ms) ms[r.stage] += t;
+        if (launches) launches[r.stage] += 1;
+      }
+    }
+    reset(enabled);
+    return ORBX_OK;
+  }
+  void release() {
+    reset(false);
+    for (auto e : pool) hipEventDestroy(e);
+    pool.clear();
+  }
+};
+
+}  // namespace orbx
+
+#endif

@@ -1,0 +1,455 @@
+// api_extract.hip -- C ABI of the extractor (include/orbx.h): plan
+// creation, batched launches, the ORBextractor::operator() drop-in, stage
+// timing and synthetic frames.
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <mutex>
+#include <vector>
+
+#include "../../include/orbx.h"
+#include "api_common.h"
+#include "geometry.h"
+
+namespace orbx {
+__global__ void k_resize(const uint8_t*, size_t, size_t, uint8_t*, size_t, const LevelInfo*, int,
+                         const int32_t*, const int32_t*, const int16_t*, const int32_t*,
+                         const int16_t*);
+__global__ void k_fast_cells(const uint8_t*, size_t, size_t, const uint8_t*, size_t,
+                             const LevelInfo*, const CellInfo*, uint32_t*, size_t, uint32_t*, int,
+                             int, int);
+__global__ void k_quadtree(const LevelInfo*, const CellInfo*, const uint32_t*, size_t,
+                           const uint32_t*, int, uint32_t*, int32_t*, size_t, uint32_t*, size_t,
+                           int*, int, int, int, int*);
+__global__ void k_blur(const uint8_t*, size_t, size_t, const uint8_t*, size_t, uint8_t*, size_t,
+                       const LevelInfo*, int);
+__global__ void k_orient_brief(const uint8_t*, size_t, size_t, const uint8_t*, size_t,
+                               const uint8_t*, size_t, const LevelInfo*, int, const uint32_t*,
+                               size_t, const int*, const int16_t*, int, orbx_keypoint*, uint8_t*,
+                               int*, int);
+__global__ void k_synth(uint8_t*, int, int, size_t, int, int);
+}  // namespace orbx
+
+using namespace orbx;
+
+static const char* kStageNames[ORBX_NSTAGES] = {
+    "resize", "fast_cells", "quadtree", "blur", "orient_brief",
+    "match_select", "match_candidates", "match_resolve", "match_finalize"};
+
+extern "C" int orbx_abi_version(void) { return ORBX_ABI_VERSION; }
+
+extern "C" const char* orbx_status_string(int s) {
+  switch (s) {
+    case ORBX_OK: return "ok";
+    case ORBX_ERR_ARG: return "invalid argument";
+    case ORBX_ERR_CELL_ROI: return "negative-extent FAST cell (reference throws cv::Exception)";
+    case ORBX_ERR_LEVEL_SIZE: return "pyramid level too small";
+    case ORBX_ERR_QUADTREE: return "DistributeOctTree does not terminate";
+    case ORBX_ERR_CAPACITY: return "output capacity too small";
+    case ORBX_ERR_UNSUPPORTED: return "unsupported configuration";
+    case ORBX_ERR_HIP: return "HIP runtime error";
+    case ORBX_ERR_NO_DEVICE: return "no gfx950 device";
+    default: return "unknown status";
+  }
+}
+
+extern "C" int orbx_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+extern "C" int orbx_stage_count(void) { return ORBX_NSTAGES; }
+extern "C" const char* orbx_stage_name(int s) {
+  return (s >= 0 && s < ORBX_NSTAGES) ? kStageNames[s] : "";
+}
+
+extern "C" int orbx_tables(const orbx_params* p, float* scale, float* inv_scale, float* sigma2,
+                           float* inv_sigma2, int* fpl, int* umax16) {
+  if (!p) return ORBX_ERR_ARG;
+  Tables t;
+  int rc = compute_tables(*p, t);
+  if (rc) return rc;
+  for (int l = 0; l < t.nlevels; ++l) {
+    if (scale) scale[l] = t.scale[l];
+    if (inv_scale) inv_scale[l] = t.inv_scale[l];
+    if (sigma2) sigma2[l] = t.sigma2[l];
+    if (inv_sigma2) inv_sigma2[l] = t.inv_sigma2[l];
+    if (fpl) fpl[l] = t.features[l];
+  }
+  if (umax16) memcpy(umax16, t.umax, sizeof(t.umax));
+  return ORBX_OK;
+}
+
+extern "C" int orbx_geometry_compute(const orbx_params* p, int width, int height,
+                                     orbx_geometry* g) {
+  if (!p || !g) return ORBX_ERR_ARG;
+  Plan P;
+  int rc = plan_geometry(*p, width, height, P);
+  if (rc) return rc;
+  *g = P.geo;
+  return ORBX_OK;
+}
+
+extern "C" int orbx_resize_tables(const orbx_params* p, int width, int height, int level,
+                                  int32_t* xofs, int16_t* alpha, int32_t* yofs, int16_t* beta) {
+  if (!p) return ORBX_ERR_ARG;
+  Plan P;
+  int rc = plan_geometry(*p, width, height, P);
+  if (rc) return rc;
+  if (level < 1 || level >= p->nlevels || P.levels[level].unique != level) return ORBX_ERR_ARG;
+  const LevelInfo& L = P.levels[level];
+  for (int x = 0; x < L.w; ++x) {
+    if (xofs) xofs[x] = P.xofs[L.lut_x + x];
+    if (alpha) { alpha[2 * x] = P.alpha[2 * (L.lut_x + x)]; alpha[2 * x + 1] = P.alpha[2 * (L.lut_x + x) + 1]; }
+  }
+  for (int y = 0; y < L.h; ++y) {
+    if (yofs) yofs[y] = P.yofs[L.lut_y + y];
+    if (beta) { beta[2 * y] = P.beta[2 * (L.lut_y + y)]; beta[2 * y + 1] = P.beta[2 * (L.lut_y + y) + 1]; }
+  }
+  return ORBX_OK;
+}
+
+// ---------------------------------------------------------------------------
+// orbx_plan
+// ---------------------------------------------------------------------------
+struct orbx_plan {
+  Plan P;
+  int device = 0, max_batch = 0;
+  hipStream_t stream = nullptr;
+  LevelInfo* d_lv = nullptr;
+  CellInfo* d_cells = nullptr;
+  int32_t *d_xofs = nullptr, *d_xofs1 = nullptr, *d_yofs = nullptr;
+  int16_t *d_alpha = nullptr, *d_beta = nullptr, *d_disk = nullptr;
+  int ndisk = 0;
+  uint8_t *d_pyr = nullptr, *d_blur = nullptr;
+  uint32_t *d_slots = nullptr, *d_ccount = nullptr, *d_qkeys = nullptr, *d_qout = nullptr;
+  int32_t* d_qnode = nullptr;
+  int *d_lcount = nullptr, *d_err = nullptr;
+  size_t pyr_stride = 0, blur_stride = 0, slot_stride = 0, qk_stride = 0, qout_stride = 0;
+  size_t qt_lds = 0;
+  StageTimer timer;
+};
+
+static size_t round_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
+
+static void plan_free(orbx_plan* p) {
+  if (!p) return;
+  hipSetDevice(p->device);
+  void* bufs[] = {p->d_lv, p->d_cells, p->d_xofs, p->d_xofs1, p->d_yofs, p->d_alpha, p->d_beta,
+                  p->d_disk, p->d_pyr, p->d_blur, p->d_slots, p->d_ccount, p->d_qkeys, p->d_qout,
+                  p->d_qnode, p->d_lcount, p->d_err};
+  for (void* b : bufs)
+    if (b) hipFree(b);
+  p->timer.release();
+  if (p->stream) hipStreamDestroy(p->stream);
+  delete p;
+}
+
+template <typename T>
+static int upload(T** dst, const std::vector<T>& v) {
+  size_t n = v.size() ? v.size() : 1;
+  if (hipMalloc((void**)dst, n * sizeof(T)) != hipSuccess) return ORBX_ERR_HIP;
+  if (v.size() && hipMemcpy(*dst, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice) != hipSuccess)
+    return ORBX_ERR_HIP;
+  return ORBX_OK;
+}
+
+static int dev_alloc(void** p, size_t bytes) {
+  if (hipMalloc(p, bytes ? bytes : 16) != hipSuccess) return ORBX_ERR_HIP;
+  return ORBX_OK;
+}
+
+extern "C" int orbx_plan_create(const orbx_params* prm, int width, int height, int max_batch,
+                                int device, orbx_plan** out) {
+  if (!prm || !out || max_batch < 1) return ORBX_ERR_ARG;
+  *out = nullptr;
+  int ndev = orbx_device_count();
+  if (device < 0 || device >= ndev) return ORBX_ERR_NO_DEVICE;
+  orbx_plan* p = new orbx_plan();
+  int rc = plan_geometry(*prm, width, height, p->P);
+  if (rc) { delete p; return rc; }
+  const Plan& P = p->P;
+  p->device = device;
+  p->max_batch = max_batch;
+  ORBX_TRY(hipSetDevice(device));
+  // quadtree LDS: cell offsets + 12 int arrays of qt_smax (see k_quadtree)
+  p->qt_lds = sizeof(int) * ((size_t)P.qt_max_cells + 1 + 12 * (size_t)P.qt_smax);
+  if (p->qt_lds > 150 * 1024) { plan_free(p); return ORBX_ERR_UNSUPPORTED; }
+  if (hipFuncSetAttribute((const void*)k_quadtree, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          (int)p->qt_lds) != hipSuccess) { plan_free(p); return ORBX_ERR_HIP; }
+  if (hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking) != hipSuccess) { plan_free(p); return ORBX_ERR_HIP; }
+  // disk offsets of IC_Angle (ORBextractor.cc:28-45), umax from the tables
+  std::vector<int16_t> disk;
+  for (int v = -15; v <= 15; ++v) {
+    const int um = (v == 0) ? 15 : P.tables.umax[v < 0 ? -v : v];
+    for (int u = -um; u <= um; ++u) { disk.push_back((int16_t)u); disk.push_back((int16_t)v); }
+  }
+  p->ndisk = (int)disk.size() / 2;
+  if (upload(&p->d_lv, P.levels) || upload(&p->d_cells, P.cells) || upload(&p->d_xofs, P.xofs) ||
+      upload(&p->d_xofs1, P.xofs1) || upload(&p->d_yofs, P.yofs) || upload(&p->d_alpha, P.alpha) ||
+      upload(&p->d_beta, P.beta) || upload(&p->d_disk, disk)) {
+    plan_free(p);
+    return ORBX_ERR_HIP;
+  }
+  p->pyr_stride = round_up((size_t)P.pyr_bytes, 256);
+  p->blur_stride = round_up((size_t)P.blur_bytes, 256);
+  p->slot_stride = round_up((size_t)P.nslots, 64);
+  p->qk_stride = round_up((size_t)P.qk_elems, 64);
+  p->qout_stride = round_up((size_t)P.kcap, 64);
+  const size_t B = (size_t)max_batch;
+  if (dev_alloc((void**)&p->d_pyr, B * p->pyr_stride) ||
+      dev_alloc((void**)&p->d_blur, B * p->blur_stride) ||
+      dev_alloc((void**)&p->d_slots, B * p->slot_stride * 4) ||
+      dev_alloc((void**)&p->d_ccount, B * (size_t)(P.ncells ? P.ncells : 1) * 4) ||
+      dev_alloc((void**)&p->d_qkeys, B * p->qk_stride * 4) ||
+      dev_alloc((void**)&p->d_qnode, B * p->qk_stride * 4) ||
+      dev_alloc((void**)&p->d_qout, B * p->qout_stride * 4) ||
+      dev_alloc((void**)&p->d_lcount, B * (size_t)P.params.nlevels * 4) ||
+      dev_alloc((void**)&p->d_err, 16)) {
+    plan_free(p);
+    return ORBX_ERR_HIP;
+  }
+  hipMemset(p->d_err, 0, 16);
+  hipMemset(p->d_ccount, 0, B * (size_t)(P.ncells ? P.ncells : 1) * 4);
+  if (hipDeviceSynchronize() != hipSuccess) { plan_free(p); return ORBX_ERR_HIP; }
+  *out = p;
+  return ORBX_OK;
+}
+
+extern "C" int orbx_plan_destroy(orbx_plan* p) {
+  plan_free(p);
+  return ORBX_OK;
+}
+
+extern "C" int orbx_plan_geometry(const orbx_plan* p, orbx_geometry* g) {
+  if (!p || !g) return ORBX_ERR_ARG;
+  *g = p->P.geo;
+  return ORBX_OK;
+}
+
+extern "C" int orbx_plan_set_timing(orbx_plan* p, int enable) {
+  if (!p) return ORBX_ERR_ARG;
+  hipSetDevice(p->device);
+  p->timer.reset(enable != 0);
+  return ORBX_OK;
+}
+
+extern "C" int orbx_plan_stage_times(orbx_plan* p, double* ms, int* launches, int n) {
+  if (!p) return ORBX_ERR_ARG;
+  hipSetDevice(p->device);
+  return p->timer.collect(ms, launches, n);
+}
+
+extern "C" int orbx_plan_extract(orbx_plan* p, const uint8_t* frames, int nframes,
+                                 size_t fstride, size_t rstride, orbx_keypoint* kps,
+                                 uint8_t* desc, int* counts, void* stream) {
+  if (!p || !frames || !kps || !desc || !counts || nframes < 1 || nframes > p->max_batch)
+    return ORBX_ERR_ARG;
+  const Plan& P = p->P;
+  if (rstride < (size_t)P.W || fstride < rstride * (size_t)P.H) return ORBX_ERR_ARG;
+  ORBX_TRY(hipSetDevice(p->device));
+  hipStream_t s = stream ? (hipStream_t)stream : p->stream;
+  const int L = P.params.nlevels, n = nframes;
+  // K1 pyramid
+  p->timer.begin(ORBX_STAGE_RESIZE, s);
+  for (int l = 1; l < L; ++l) {
+    const LevelInfo& lv = P.levels[l];
+    if (lv.unique != l) continue;
+    dim3 grid((lv.w + 255) / 256, (lv.h + 3) / 4, n), block(64, 4);
+    hipLaunchKernelGGL(k_resize, grid, block, 0, s, frames, fstride, rstride, p->d_pyr,
+                       p->pyr_stride, p->d_lv, l, p->d_xofs, p->d_xofs1, p->d_alpha, p->d_yofs,
+                       p->d_beta);
+  }
+  p->timer.end(ORBX_STAGE_RESIZE, s);
+  // K2 FAST cells
+  p->timer.begin(ORBX_STAGE_FAST, s);
+  if (P.ncells > 0) {
+    hipLaunchKernelGGL(k_fast_cells, dim3(P.ncells, n), dim3(256), 0, s, frames, fstride, rstride,
+                       p->d_pyr, p->pyr_stride, p->d_lv, p->d_cells, p->d_slots, p->slot_stride,
+                       p->d_ccount, P.ncells, P.ini_th, P.min_th);
+  }
+  p->timer.end(ORBX_STAGE_FAST, s);
+  // K3 DistributeOctTree
+  p->timer.begin(ORBX_STAGE_QUADTREE, s);
+  hipLaunchKernelGGL(k_quadtree, dim3(L, n), dim3(256), p->qt_lds, s, p->d_lv, p->d_cells,
+                     p->d_slots, p->slot_stride, p->d_ccount, P.ncells, p->d_qkeys, p->d_qnode,
+                     p->qk_stride, p->d_qout, p->qout_stride, p->d_lcount, L, P.qt_smax,
+                     P.qt_max_cells, p->d_err);
+  p->timer.end(ORBX_STAGE_QUADTREE, s);
+  // K5 blur of every unique level
+  p->timer.begin(ORBX_STAGE_BLUR, s);
+  for (int l = 0; l < L; ++l) {
+    const LevelInfo& lv = P.levels[l];
+    if (lv.unique != l) continue;
+    dim3 grid((lv.w + 63) / 64, (lv.h + 15) / 16, n);
+    hipLaunchKernelGGL(k_blur, grid, dim3(256), 0, s, frames, fstride, rstride, p->d_pyr,
+                       p->pyr_stride, p->d_blur, p->blur_stride, p->d_lv, l);
+  }
+  p->timer.end(ORBX_STAGE_BLUR, s);
+  // K4+K6+K7 orientation, descriptors, assembly
+  p->timer.begin(ORBX_STAGE_BRIEF, s);
+  hipLaunchKernelGGL(k_orient_brief, dim3((P.kcap + 3) / 4 > 0 ? (P.kcap + 3) / 4 : 1, n),
+                     dim3(256), 0, s, frames, fstride, rstride, p->d_pyr, p->pyr_stride,
+                     p->d_blur, p->blur_stride, p->d_lv, L, p->d_qout, p->qout_stride,
+                     p->d_lcount, p->d_disk, p->ndisk, kps, desc, counts, P.kcap);
+  p->timer.end(ORBX_STAGE_BRIEF, s);
+  if (hipGetLastError() != hipSuccess) return ORBX_ERR_HIP;
+  return ORBX_OK;
+}
+
+extern "C" int orbx_plan_check(orbx_plan* p, void* stream) {
+  if (!p) return ORBX_ERR_ARG;
+  ORBX_TRY(hipSetDevice(p->device));
+  hipStream_t s = stream ? (hipStream_t)stream : p->stream;
+  ORBX_TRY(hipStreamSynchronize(s));
+  int err = 0;
+  ORBX_TRY(hipMemcpy(&err, p->d_err, sizeof(int), hipMemcpyDeviceToHost));
+  if (err) {
+    ORBX_TRY(hipMemset(p->d_err, 0, sizeof(int)));
+    if (err & ORBX_DEVERR_QUADTREE) return ORBX_ERR_QUADTREE;
+    return ORBX_ERR_CAPACITY;
+  }
+  return ORBX_OK;
+}
+
+extern "C" int orbx_synth_frames(uint8_t* d_frames, int W, int H, size_t fstride, int nframes,
+                                 int first_idx, int kind, void* stream) {
+  if (!d_frames || W <= 0 || H <= 0 || nframes < 1 || kind < 0 || kind > 2 ||
+      fstride < (size_t)W * H)
+    return ORBX_ERR_ARG;
+  const long long npx = (long long)W * H;
+  dim3 grid((unsigned)((npx + 4095) / 4096), nframes);
+  hipLaunchKernelGGL(k_synth, grid, dim3(256), 0, (hipStream_t)stream, d_frames, W, H, fstride,
+                     first_idx, kind);
+  return hipGetLastError() == hipSuccess ? ORBX_OK : ORBX_ERR_HIP;
+}
+
+// ---------------------------------------------------------------------------
+// orbx_extractor: the ORBextractor::operator() drop-in (host buffers).
+// ---------------------------------------------------------------------------
+struct orbx_extractor {
+  orbx_params params;
+  int device = 0;
+  orbx_plan* plan = nullptr;
+  int W = 0, H = 0;
+  uint8_t* d_img = nullptr;
+  orbx_keypoint* d_kps = nullptr;
+  uint8_t* d_desc = nullptr;
+  int* d_count = nullptr;
+  bool have_frame = false;
+};
+
+static void extractor_release_plan(orbx_extractor* e) {
+  hipSetDevice(e->device);
+  if (e->plan) orbx_plan_destroy(e->plan);
+  if (e->d_img) hipFree(e->d_img);
+  if (e->d_kps) hipFree(e->d_kps);
+  if (e->d_desc) hipFree(e->d_desc);
+  if (e->d_count) hipFree(e->d_count);
+  e->plan = nullptr; e->d_img = nullptr; e->d_kps = nullptr; e->d_desc = nullptr;
+  e->d_count = nullptr; e->W = e->H = 0; e->have_frame = false;
+}
+
+static int extractor_prepare(orbx_extractor* e, int W, int H) {
+  if (e->plan && e->W == W && e->H == H) return ORBX_OK;
+  extractor_release_plan(e);
+  int rc = orbx_plan_create(&e->params, W, H, 1, e->device, &e->plan);
+  if (rc) return rc;
+  const int kcap = e->plan->P.kcap;
+  if (dev_alloc((void**)&e->d_img, (size_t)W * H) ||
+      dev_alloc((void**)&e->d_kps, sizeof(orbx_keypoint) * (size_t)(kcap ? kcap : 1)) ||
+      dev_alloc((void**)&e->d_desc, 32 * (size_t)(kcap ? kcap : 1)) ||
+      dev_alloc((void**)&e->d_count, sizeof(int))) {
+    extractor_release_plan(e);
+    return ORBX_ERR_HIP;
+  }
+  e->W = W;
+  e->H = H;
+  return ORBX_OK;
+}
+
+extern "C" int orbx_extractor_create(const orbx_params* p, int device, orbx_extractor** out) {
+  if (!p || !out) return ORBX_ERR_ARG;
+  *out = nullptr;
+  Tables t;
+  int rc = compute_tables(*p, t);
+  if (rc) return rc;
+  if (device < 0 || device >= orbx_device_count()) return ORBX_ERR_NO_DEVICE;
+  orbx_extractor* e = new orbx_extractor();
+  e->params = *p;
+  e->device = device;
+  *out = e;
+  return ORBX_OK;
+}
+
+extern "C" int orbx_extractor_destroy(orbx_extractor* e) {
+  if (!e) return ORBX_OK;
+  extractor_release_plan(e);
+  delete e;
+  return ORBX_OK;
+}
+
+extern "C" int orbx_extractor_capacity(orbx_extractor* e, int W, int H, int* kcap) {
+  if (!e || !kcap) return ORBX_ERR_ARG;
+  Plan P;
+  int rc = plan_geometry(e->params, W, H, P);
+  if (rc) return rc;
+  *kcap = P.kcap;
+  return ORBX_OK;
+}
+
+extern "C" int orbx_extract(orbx_extractor* e, const uint8_t* img, int W, int H, size_t stride,
+                            orbx_keypoint* kps, int cap, uint8_t* desc, int* n) {
+  if (!e || !n) return ORBX_ERR_ARG;
+  *n = 0;
+  if (!img || W <= 0 || H <= 0) return ORBX_OK; /* _image.empty(): return (:444-445) */
+  if (stride < (size_t)W) return ORBX_ERR_ARG;
+  int rc = extractor_prepare(e, W, H);
+  if (rc) return rc;
+  ORBX_TRY(hipSetDevice(e->device));
+  hipStream_t s = e->plan->stream;
+  ORBX_TRY(hipMemcpy2DAsync(e->d_img, (size_t)W, img, stride, (size_t)W, (size_t)H,
+                            hipMemcpyHostToDevice, s));
+  rc = orbx_plan_extract(e->plan, e->d_img, 1, (size_t)W * H, (size_t)W, e->d_kps, e->d_desc,
+                         e->d_count, s);
+  if (rc) return rc;
+  int K = 0;
+  ORBX_TRY(hipMemcpyAsync(&K, e->d_count, sizeof(int), hipMemcpyDeviceToHost, s));
+  rc = orbx_plan_check(e->plan, s);
+  e->have_frame = (rc == ORBX_OK);
+  if (rc) return rc;
+  *n = K;
+  if (K == 0) return ORBX_OK; /* keypoints untouched, descriptors released (:460-463) */
+  if (K > cap || !kps || !desc) return ORBX_ERR_CAPACITY;
+  ORBX_TRY(hipMemcpyAsync(kps, e->d_kps, sizeof(orbx_keypoint) * (size_t)K,
+                          hipMemcpyDeviceToHost, s));
+  ORBX_TRY(hipMemcpyAsync(desc, e->d_desc, 32 * (size_t)K, hipMemcpyDeviceToHost, s));
+  ORBX_TRY(hipStreamSynchronize(s));
+  return ORBX_OK;
+}
+
+extern "C" int orbx_extractor_level(orbx_extractor* e, int level, uint8_t* dst, size_t dst_stride,
+                                    int* width, int* height) {
+  if (!e || !e->plan || !e->have_frame || level < 0 || level >= e->params.nlevels)
+    return ORBX_ERR_ARG;
+  const LevelInfo& L = e->plan->P.levels[level];
+  if (width) *width = L.w;
+  if (height) *height = L.h;
+  if (!dst) return ORBX_OK;
+  if (dst_stride < (size_t)L.w) return ORBX_ERR_ARG;
+  ORBX_TRY(hipSetDevice(e->device));
+  const uint8_t* src;
+  size_t pitch;
+  if (L.unique == 0) {
+    src = e->d_img;
+    pitch = (size_t)e->W;
+  } else {
+    src = e->plan->d_pyr + e->plan->P.levels[L.unique].pyr_off;
+    pitch = (size_t)L.pitch;
+  }
+  ORBX_TRY(hipMemcpy2D(dst, dst_stride, src, pitch, (size_t)L.w, (size_t)L.h,
+                       hipMemcpyDeviceToHost));
+  return ORBX_OK;
+}

@@ -1,0 +1,280 @@
+/* geometry.cpp -- host planner.  Pure host C++ (no HIP calls); compiled into
+ * liborbx.so so the CPU test-suite can check it without a GPU.
+ *
+ * Floating-point expressions are written with the same operand types and
+ * evaluation order as the reference so the float/double roundings match
+ * (build flag -ffp-contract=off). */
+#include "geometry.h"
+
+#include <math.h>
+#include <string.h>
+
+#include <algorithm>
+
+namespace orbx {
+
+static int round_f(float v) { return (int)lrintf(v); } /* cvRound(float), half-even */
+static int round_d(double v) { return (int)lrint(v); }
+static short sat_s16(int v) { return (short)std::min(32767, std::max(-32768, v)); }
+
+int compute_tables(const orbx_params& p, Tables& t) {
+  if (p.nlevels < 1 || p.nlevels > ORBX_MAX_LEVELS || p.nfeatures < 0 || !(p.scale_factor > 0.f))
+    return ORBX_ERR_ARG;
+  const int n = p.nlevels;
+  t.nlevels = n;
+  t.scaleFactor = (double)p.scale_factor; /* ORBextractor.h:78 double member */
+  t.scale.assign(n, 1.0f);
+  /* src/ORBextractor.cc:123-124: std::partial_sum(begin, end-1, begin+1, op)
+   * writes d_first[0] = first[0] first, so scale[1] = scale[0] = 1 and
+   * scale[i] = f32(scale[i-1] * (double)scaleFactor) for i >= 2. */
+  if (n >= 2) {
+    float acc = t.scale[0];
+    t.scale[1] = acc;
+    for (int i = 2; i < n; ++i) {
+      acc = (float)((double)acc * t.scaleFactor);
+      t.scale[i] = acc;
+    }
+  }
+  t.sigma2.resize(n);
+  t.inv_scale.resize(n);
+  t.inv_sigma2.resize(n);
+  for (int i = 0; i < n; ++i) {
+    t.sigma2[i] = t.scale[i] * t.scale[i];
+    t.inv_scale[i] = 1.0f / t.scale[i];
+    t.inv_sigma2[i] = 1.0f / t.sigma2[i];
+  }
+  /* :141-151 features per level */
+  t.features.assign(n, 0);
+  const float factor = (float)(1.0f / t.scaleFactor);
+  float desired = (float)((float)(p.nfeatures * (1 - factor)) / (1 - pow((double)factor, n)));
+  int sum = 0;
+  for (int l = 0; l < n - 1; ++l) {
+    int cur = round_f(desired);
+    sum += cur;
+    desired *= factor;
+    t.features[l] = cur;
+  }
+  t.features[n - 1] = std::max(p.nfeatures - sum, 0);
+  /* :155-169 umax */
+  const int half = 15;
+  int vmax = (int)floorf(half * sqrtf(2.f) / 2 + 1);
+  int vmin = (int)ceilf(half * sqrtf(2.f) / 2);
+  const double hp2 = half * half;
+  for (int v = 0; v <= vmax; ++v) t.umax[v] = round_d(sqrt(hp2 - v * v));
+  for (int v = half, v0 = 0; v >= vmin; --v) {
+    while (t.umax[v0] == t.umax[v0 + 1]) ++v0;
+    t.umax[v] = v0;
+    ++v0;
+  }
+  return ORBX_OK;
+}
+
+static int pitch_of(int w) { return (w + 15) & ~15; }
+
+/* cv::resize INTER_LINEAR coefficient tables (OpenCV 3.4 resize():
+ * scale = 1/((double)dsize/ssize); f = (float)((d+0.5)*scale-0.5); s =
+ * cvFloor(f); f -= s; coefficients saturate_cast<short>((1-f)*2048), f*2048). */
+static void resize_lut(int sw, int sh, int dw, int dh, std::vector<int32_t>& xofs,
+                       std::vector<int32_t>& xofs1, std::vector<int16_t>& alpha,
+                       std::vector<int32_t>& yofs, std::vector<int16_t>& beta) {
+  const double scale_x = 1. / ((double)dw / sw), scale_y = 1. / ((double)dh / sh);
+  int xmax = dw;
+  const size_t x0 = xofs.size();
+  for (int dx = 0; dx < dw; ++dx) {
+    float fx = (float)((dx + 0.5) * scale_x - 0.5);
+    int sx = (int)floorf(fx);
+    fx -= sx;
+    if (sx < 0) fx = 0, sx = 0;
+    if (sx + 1 >= sw) {
+      xmax = std::min(xmax, dx);
+      if (sx >= sw - 1) fx = 0, sx = sw - 1;
+    }
+    xofs.push_back(sx);
+    xofs1.push_back(std::min(sx + 1, sw - 1));
+    alpha.push_back(sat_s16(round_f((1.f - fx) * 2048)));
+    alpha.push_back(sat_s16(round_f(fx * 2048)));
+  }
+  /* columns at or beyond xmax use S[sx]*2048 (HResizeLinear tail loop) */
+  for (int dx = xmax; dx < dw; ++dx) {
+    alpha[2 * (x0 + dx)] = 2048;
+    alpha[2 * (x0 + dx) + 1] = 0;
+    xofs1[x0 + dx] = xofs[x0 + dx];
+  }
+  for (int dy = 0; dy < dh; ++dy) {
+    float fy = (float)((dy + 0.5) * scale_y - 0.5);
+    int sy = (int)floorf(fy);
+    fy -= sy;
+    yofs.push_back(sy);
+    beta.push_back(sat_s16(round_f((1.f - fy) * 2048)));
+    beta.push_back(sat_s16(round_f(fy * 2048)));
+  }
+}
+
+static bool area_fast_2x(int sw, int sh, int dw, int dh) {
+  double sx = 1. / ((double)dw / sw), sy = 1. / ((double)dh / sh);
+  int ix = round_d(sx), iy = round_d(sy);
+  return fabs(sx - ix) < 2.220446049250313e-16 && fabs(sy - iy) < 2.220446049250313e-16 &&
+         ix == 2 && iy == 2;
+}
+
+int plan_geometry(const orbx_params& p, int width, int height, Plan& P) {
+  int rc = compute_tables(p, P.tables);
+  if (rc) return rc;
+  if (width <= 0 || height <= 0) return ORBX_ERR_ARG;
+  P.params = p;
+  P.W = width;
+  P.H = height;
+  P.ini_th = std::min(std::max(p.ini_th_fast, 0), 255);
+  P.min_th = std::min(std::max(p.min_th_fast, 0), 255);
+  const int L = p.nlevels;
+  P.levels.assign(L, LevelInfo());
+  P.cells.clear();
+  P.xofs.clear(); P.xofs1.clear(); P.alpha.clear(); P.yofs.clear(); P.beta.clear();
+  memset(&P.geo, 0, sizeof(P.geo));
+  P.geo.nlevels = L;
+
+  /* ComputePyramid sizes (:501-502) and storage */
+  long long pyr = 0, blur = 0;
+  for (int l = 0; l < L; ++l) {
+    LevelInfo& lv = P.levels[l];
+    float s = P.tables.inv_scale[l];
+    lv.w = round_f((float)width * s);
+    lv.h = round_f((float)height * s);
+    if (lv.h <= 32 || lv.w < 32) return ORBX_ERR_LEVEL_SIZE;
+    if (lv.w - 32 > 4095 || lv.h - 32 > 4095) return ORBX_ERR_UNSUPPORTED; /* 12-bit packing */
+    if (l > 0 && lv.w == P.levels[l - 1].w && lv.h == P.levels[l - 1].h) {
+      lv.unique = P.levels[l - 1].unique; /* cv::resize: dsize == ssize -> copyTo */
+    } else {
+      lv.unique = l;
+      if (l > 0 && area_fast_2x(P.levels[l - 1].w, P.levels[l - 1].h, lv.w, lv.h))
+        return ORBX_ERR_UNSUPPORTED; /* OpenCV would switch to INTER_AREA */
+    }
+    if (lv.unique == l) {
+      lv.pitch = (l == 0) ? 0 /* caller's row stride */ : pitch_of(lv.w);
+      lv.pyr_off = (l == 0) ? -1 : pyr;
+      if (l > 0) pyr += (long long)pitch_of(lv.w) * lv.h;
+      lv.blur_off = blur;
+      blur += (long long)pitch_of(lv.w) * lv.h;
+    } else {
+      const LevelInfo& u = P.levels[lv.unique];
+      lv.pitch = u.pitch;
+      lv.pyr_off = u.pyr_off;
+      lv.blur_off = u.blur_off;
+    }
+    lv.scale = P.tables.scale[l];
+    lv.patch_size = (int)(31 * P.tables.scale[l]); /* :345 int scaledPatchSize = 31 * float */
+    P.geo.width[l] = lv.w;
+    P.geo.height[l] = lv.h;
+    P.geo.alias[l] = lv.unique;
+    P.geo.features[l] = P.tables.features[l];
+  }
+  P.pyr_bytes = pyr;
+  P.blur_bytes = blur;
+
+  /* resize LUTs for unique levels >= 1 */
+  for (int l = 1; l < L; ++l) {
+    LevelInfo& lv = P.levels[l];
+    if (lv.unique != l) continue;
+    const LevelInfo& src = P.levels[l - 1];
+    lv.src_level = src.unique;
+    lv.lut_x = (int)P.xofs.size();
+    lv.lut_y = (int)P.yofs.size();
+    resize_lut(src.w, src.h, lv.w, lv.h, P.xofs, P.xofs1, P.alpha, P.yofs, P.beta);
+  }
+
+  /* FAST cell grid (ComputeKeyPointsOctTree :298-340) for unique levels */
+  long long slots = 0;
+  for (int l = 0; l < L; ++l) {
+    LevelInfo& lv = P.levels[l];
+    const int minB = ORBX_MINB, maxBX = lv.w - ORBX_EDGE + 3, maxBY = lv.h - ORBX_EDGE + 3;
+    const float width_f = (float)(maxBX - minB), height_f = (float)(maxBY - minB);
+    const int nCols = (int)(width_f / 30.f), nRows = (int)(height_f / 30.f);
+    const int wCell = nCols > 0 ? (int)ceilf(width_f / nCols) : 0;
+    const int hCell = nRows > 0 ? (int)ceilf(height_f / nRows) : 0;
+    P.geo.ncols[l] = nCols; P.geo.nrows[l] = nRows;
+    P.geo.wcell[l] = wCell; P.geo.hcell[l] = hCell;
+    /* DistributeOctTree (:230-231) */
+    lv.Wr = maxBX - minB;
+    lv.Hr = maxBY - minB;
+    lv.nini = lv.Wr / lv.Hr;
+    lv.hX = (float)lv.Wr / (float)(lv.nini > 0 ? lv.nini : 1);
+    lv.N = P.tables.features[l];
+    P.geo.nini[l] = lv.nini;
+    if (lv.unique != l) {
+      const LevelInfo& u = P.levels[lv.unique];
+      lv.cell_begin = u.cell_begin; lv.ncells = u.ncells;
+      lv.slot_begin = u.slot_begin; lv.nslots = u.nslots;
+      P.geo.ncells_bad[l] = P.geo.ncells_bad[lv.unique];
+      continue;
+    }
+    lv.cell_begin = (int)P.cells.size();
+    lv.slot_begin = slots;
+    int bad = 0;
+    for (int i = 0; i < nRows; ++i) {
+      const float iniY = (float)(minB + i * hCell);
+      const float maxY = std::min(iniY + hCell + 6, (float)maxBY);
+      for (int j = 0; j < nCols; ++j) {
+        const float iniX = (float)(minB + j * wCell);
+        const float maxX = std::min(iniX + wCell + 6, (float)maxBX);
+        const int rx = (int)iniX, ry = (int)iniY, rw = (int)(maxX - iniX), rh = (int)(maxY - iniY);
+        if (rw < 0 || rh < 0) { ++bad; continue; } /* cv::Mat(m, Rect) assertion */
+        if (rw < 7 || rh < 7) continue;            /* FAST scans nothing */
+        if (rw > ORBX_CELL_MAX || rh > ORBX_CELL_MAX) return ORBX_ERR_UNSUPPORTED;
+        CellInfo c;
+        c.level = l; c.x = rx; c.y = ry; c.w = rw; c.h = rh;
+        const int bw = rw - 6, bh = rh - 6;
+        c.slot_cap = ((bw + 1) / 2) * ((bh + 1) / 2); /* strict 3x3 NMS: independent set */
+        c.slot_off = (int)slots;
+        c.pad = 0;
+        slots += c.slot_cap;
+        P.cells.push_back(c);
+      }
+    }
+    lv.ncells = (int)P.cells.size() - lv.cell_begin;
+    lv.nslots = slots - lv.slot_begin;
+    P.geo.ncells_bad[l] = bad;
+    if (bad && !p.cell_guard) return ORBX_ERR_CELL_ROI;
+  }
+  P.nslots = slots;
+  P.ncells = (int)P.cells.size();
+
+  /* quadtree capacities */
+  int kout = 0, smax = 1, maxc = 1;
+  long long qk = 0;
+  for (int l = 0; l < L; ++l) {
+    LevelInfo& lv = P.levels[l];
+    long long cap = 4LL * std::max(lv.N - 1, lv.nini);
+    cap = std::min(cap, lv.nslots);
+    lv.kcap = (int)std::max(0LL, cap);
+    lv.kout_off = kout;
+    kout += lv.kcap;
+    lv.qk_off = qk;
+    qk += lv.nslots;
+    smax = std::max(smax, std::max(lv.N - 1, lv.nini));
+    maxc = std::max(maxc, lv.ncells);
+    P.geo.kcap_level[l] = lv.kcap;
+  }
+  P.kcap = kout;
+  P.qk_elems = qk;
+  P.qt_smax = smax;
+  P.qt_max_cells = maxc;
+  P.geo.kcap = kout;
+
+  /* algorithmic bytes of pyramid + FAST per frame: every unique level is
+   * written once by the resize that reads its source level, and read once
+   * by FAST (SURVEY §8d formula restricted to unique levels). */
+  long long px = 0, bytes = 0;
+  for (int l = 0; l < L; ++l) {
+    const LevelInfo& lv = P.levels[l];
+    if (lv.unique != l) continue;
+    long long P_l = (long long)lv.w * lv.h;
+    px += P_l;
+    bytes += P_l; /* FAST read */
+    if (l > 0) bytes += P_l + (long long)P.levels[lv.src_level].w * P.levels[lv.src_level].h;
+  }
+  P.geo.pixels = px;
+  P.geo.bytes_pyr_fast = bytes;
+  return ORBX_OK;
+}
+
+}  // namespace orbx

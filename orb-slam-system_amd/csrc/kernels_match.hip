@@ -1,0 +1,409 @@
+// kernels_match.hip -- gfx950 kernels of ORBmatcher::SearchByBoW /
+// DescriptorDistance (src/ORBmatcher.cc:278-366, 469-502, 896-908).
+//
+// SearchByBoW is greedy and order dependent (vbMatched2 excludes KF2
+// features already taken by earlier KF1 features), so it is split into
+//   k_match_candidates  fully parallel: per KF1 feature ("row") the ORBM_T
+//                       best KF2 candidates by (distance, list position),
+//                       one wavefront per row, XOR + v_bcnt Hamming.
+//   k_match_resolve     the order-dependent part: one wavefront walks the
+//                       rows of a node pair in list order; each row is one
+//                       ballot over its candidates against an LDS bitmap of
+//                       taken KF2 features (exact fallback: full rescan).
+//                       Node pairs of a well-formed FeatureVector touch
+//                       disjoint KF2 features, so they run in parallel.
+//   k_match_finalize    rotation histogram + ComputeThreeMaxima + output.
+#include <hip/hip_runtime.h>
+#include <limits.h>
+#include <stdint.h>
+
+#include "../../include/orbx.h"
+#include "match_internal.h"
+
+namespace orbx {
+
+__device__ __forceinline__ int hamming32(const uint32_t* a, const uint32_t* b) {
+  const uint4 a0 = reinterpret_cast<const uint4*>(a)[0], a1 = reinterpret_cast<const uint4*>(a)[1];
+  const uint4 b0 = reinterpret_cast<const uint4*>(b)[0], b1 = reinterpret_cast<const uint4*>(b)[1];
+  return __popc(a0.x ^ b0.x) + __popc(a0.y ^ b0.y) + __popc(a0.z ^ b0.z) + __popc(a0.w ^ b0.w) +
+         __popc(a1.x ^ b1.x) + __popc(a1.y ^ b1.y) + __popc(a1.z ^ b1.z) + __popc(a1.w ^ b1.w);
+}
+
+__device__ __forceinline__ int hamming_u(const uint32_t d1[8], const uint32_t* b) {
+  const uint4 b0 = reinterpret_cast<const uint4*>(b)[0], b1 = reinterpret_cast<const uint4*>(b)[1];
+  return __popc(d1[0] ^ b0.x) + __popc(d1[1] ^ b0.y) + __popc(d1[2] ^ b0.z) +
+         __popc(d1[3] ^ b0.w) + __popc(d1[4] ^ b1.x) + __popc(d1[5] ^ b1.y) +
+         __popc(d1[6] ^ b1.z) + __popc(d1[7] ^ b1.w);
+}
+
+__device__ __forceinline__ int find_node_pair(const MNodePair* nps, int nnp, int r) {
+  int lo = 0, hi = nnp;  // last np with row_base <= r
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (nps[mid].row_base <= r) lo = mid + 1; else hi = mid;
+  }
+  return lo - 1;
+}
+
+// ---------------------------------------------------------------------------
+// k_match_candidates: one wave per row.  rowinfo[r] = {valid, nvalid2, minD}.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_match_candidates(
+    const MProblem* __restrict__ probs, const MNodePair* __restrict__ nps, int nnp, int nrows,
+    uint32_t* __restrict__ cand, int4* __restrict__ rowinfo, int2* __restrict__ ev) {
+  __shared__ int hist[4][320];
+  __shared__ uint32_t lessl[4][ORBM_T], eql[4][ORBM_T];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int r = blockIdx.x * 4 + wave;
+  if (r >= nrows) return;
+  if (lane == 0) ev[r] = make_int2(-1, 0);
+  const int j = find_node_pair(nps, nnp, r);
+  if (j < 0) { if (lane == 0) rowinfo[r] = make_int4(0, 0, 0, 0); return; }
+  const MNodePair NP = nps[j];
+  const int a = r - NP.row_base;
+  if (a >= NP.n1) { if (lane == 0) rowinfo[r] = make_int4(0, 0, 0, 0); return; }
+  const MProblem P = probs[NP.prob];
+  const int idx1 = (int)P.feat1[NP.off1 + a];
+  if (P.valid1 && !P.valid1[idx1]) { if (lane == 0) rowinfo[r] = make_int4(0, 0, 0, 0); return; }
+  uint32_t d1[8];
+  const uint32_t* q1 = reinterpret_cast<const uint32_t*>(P.desc1 + (size_t)idx1 * 32);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) d1[k] = q1[k];
+  for (int b = lane; b < 320; b += 64) hist[wave][b] = 0;
+  __builtin_amdgcn_wave_barrier();
+  int nvalid = 0;
+  const uint32_t* f2 = P.feat2 + NP.off2;
+  for (int jj = lane; jj < NP.n2; jj += 64) {
+    const int idx2 = (int)f2[jj];
+    if (P.valid2 && !P.valid2[idx2]) continue;
+    const int d = hamming_u(d1, reinterpret_cast<const uint32_t*>(P.desc2 + (size_t)idx2 * 32));
+    atomicAdd(&hist[wave][d], 1);
+    ++nvalid;
+  }
+#pragma unroll
+  for (int s = 32; s >= 1; s >>= 1) nvalid += __shfl_xor(nvalid, s, 64);
+  __builtin_amdgcn_wave_barrier();
+  // cutoff D: smallest d with #(dist <= d) >= T (5 bins per lane, wave scan)
+  int h[5], hs = 0;
+#pragma unroll
+  for (int k = 0; k < 5; ++k) { h[k] = hist[wave][5 * lane + k]; hs += h[k]; }
+  int incl = hs;
+#pragma unroll
+  for (int s = 1; s < 64; s <<= 1) {
+    const int t = __shfl_up(incl, s, 64);
+    if (lane >= s) incl += t;
+  }
+  const int excl = incl - hs;
+  const uint64_t reach = __ballot(incl >= ORBM_T);
+  int D = 1 << 20, cntLess = nvalid;  // nvalid < T: take everything
+  if (reach) {
+    const int L0 = __ffsll((unsigned long long)reach) - 1;
+    int dd = 0, cl = 0;
+    if (lane == L0) {
+      int cum = excl;
+      for (int k = 0; k < 5; ++k) {
+        if (cum + h[k] >= ORBM_T) { dd = 5 * lane + k; cl = cum; break; }
+        cum += h[k];
+      }
+    }
+    D = __shfl(dd, L0, 64);
+    cntLess = __shfl(cl, L0, 64);
+  }
+  const uint64_t nz = __ballot(hs > 0);
+  int minD = 1 << 20;
+  if (nz) {
+    const int L1 = __ffsll((unsigned long long)nz) - 1;
+    int md = 0;
+    if (lane == L1) {
+      for (int k = 4; k >= 0; --k) if (h[k] > 0) md = 5 * lane + k;
+    }
+    minD = __shfl(md, L1, 64);
+  }
+  // ordered compaction: all entries with d < D, then the first (T - cntLess) with d == D
+  const int needEq = ORBM_T - cntLess;
+  int nl = 0, ne = 0;
+  for (int base = 0; base < NP.n2; base += 64) {
+    const int jj = base + lane;
+    int d = 1 << 20;
+    if (jj < NP.n2) {
+      const int idx2 = (int)f2[jj];
+      if (!(P.valid2 && !P.valid2[idx2]))
+        d = hamming_u(d1, reinterpret_cast<const uint32_t*>(P.desc2 + (size_t)idx2 * 32));
+    }
+    const uint64_t ml = __ballot(d < D), me = __ballot(d == D);
+    const uint64_t below = (1ull << lane) - 1ull;
+    if (d < D) lessl[wave][nl + __popcll(ml & below)] = ((uint32_t)d << 16) | (uint32_t)jj;
+    if (d == D) {
+      const int rk = ne + __popcll(me & below);
+      if (rk < needEq) eql[wave][rk] = ((uint32_t)d << 16) | (uint32_t)jj;
+    }
+    nl += __popcll(ml);
+    ne += __popcll(me);
+    if (nl >= cntLess && ne >= needEq) break;
+  }
+  __builtin_amdgcn_wave_barrier();
+  const int nlt = min(nl, ORBM_T), neq = max(0, min(ne, needEq));
+  uint32_t* out = cand + (size_t)r * ORBM_T;
+  if (lane < nlt) {  // rank sort of the (< T) entries below the cutoff
+    const uint32_t k = lessl[wave][lane];
+    int rank = 0;
+    for (int t = 0; t < nlt; ++t) rank += lessl[wave][t] < k;
+    out[rank] = k;
+  }
+  if (lane < ORBM_T && lane >= nlt) {
+    const int e = lane - nlt;
+    out[lane] = (e < neq) ? eql[wave][e] : 0xFFFFFFFFu;
+  }
+  if (lane == 0) rowinfo[r] = make_int4(1, nvalid, minD, idx1);
+}
+
+// ---------------------------------------------------------------------------
+// k_match_resolve: greedy, in list order.  unit = node pair (parallel mode)
+// or problem (sequential mode: all its node pairs, one bitmap).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void best_merge(uint32_t& k1, int& d2, uint32_t ok1, int od2) {
+  // (k1, d2): smallest key (dist<<16|pos) and second-smallest distance of a multiset
+  const uint32_t lo = min(k1, ok1), hi = max(k1, ok1);
+  d2 = min(min(d2, od2), (int)(hi >> 16));
+  k1 = lo;
+}
+
+__global__ __launch_bounds__(256) void k_match_resolve(
+    const MProblem* __restrict__ probs, const MNodePair* __restrict__ nps, int nunits,
+    int sequential, const uint32_t* __restrict__ cand, const int4* __restrict__ rowinfo,
+    int2* __restrict__ ev) {
+  __shared__ uint32_t bitmap[4][ORBM_MAX_N2 / 32 / 4];  // 512 words (16384 idx2) per wave
+  extern __shared__ uint32_t bigmap[];                   // used when n2 > 16384 (1 wave/block)
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int unit = blockIdx.x * (blockDim.x >> 6) + wave;
+  if (unit >= nunits) return;
+  int np0, np1;
+  const MProblem* Pp;
+  if (sequential) {
+    Pp = &probs[unit];
+    np0 = Pp->np_begin;
+    np1 = Pp->np_end;
+  } else {
+    np0 = unit;
+    np1 = unit + 1;
+    Pp = &probs[nps[unit].prob];
+  }
+  const MProblem P = *Pp;
+  uint32_t* bm = (P.n2 > 16384) ? bigmap : bitmap[wave];
+  const int words = (P.n2 + 31) >> 5;
+  for (int w = lane; w < words; w += 64) bm[w] = 0u;
+  __builtin_amdgcn_wave_barrier();
+  const float factor = 1.0f / ORBM_HISTO;
+  for (int j = np0; j < np1; ++j) {
+    const MNodePair NP = nps[j];
+    const uint32_t* f2 = P.feat2 + NP.off2;
+    for (int a = 0; a < NP.n1; ++a) {
+      const int r = NP.row_base + a;
+      const int4 info = rowinfo[r];
+      if (!info.x || info.z >= ORBM_TH_LOW) continue;  // invalid MP1, or can never pass TH_LOW
+      const uint32_t key = lane < ORBM_T ? cand[(size_t)r * ORBM_T + lane] : 0xFFFFFFFFu;
+      const int idx2 = key != 0xFFFFFFFFu ? (int)f2[key & 0xFFFFu] : 0;
+      const bool un = key != 0xFFFFFFFFu && !((bm[idx2 >> 5] >> (idx2 & 31)) & 1u);
+      const uint64_t m = __ballot(un);
+      int best1 = INT_MAX, best2 = INT_MAX, bidx2 = -1;
+      if (__popcll(m) >= 2 || info.y <= ORBM_T) {
+        if (m) {
+          const int l1 = __ffsll((unsigned long long)m) - 1;
+          best1 = (int)(__shfl(key, l1, 64) >> 16);
+          bidx2 = __shfl(idx2, l1, 64);
+          const uint64_t m2 = m & (m - 1);
+          if (m2) best2 = (int)(__shfl(key, __ffsll((unsigned long long)m2) - 1, 64) >> 16);
+        }
+      } else {  // candidates exhausted: exact rescan of the node's list
+        const uint32_t* q1 = reinterpret_cast<const uint32_t*>(P.desc1 + (size_t)info.w * 32);
+        uint32_t d1[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) d1[k] = q1[k];
+        uint32_t k1 = 0xFFFFFFFFu;
+        int d2 = INT_MAX;
+        for (int jj = lane; jj < NP.n2; jj += 64) {
+          const int i2 = (int)f2[jj];
+          if (P.valid2 && !P.valid2[i2]) continue;
+          if ((bm[i2 >> 5] >> (i2 & 31)) & 1u) continue;
+          const int d = hamming_u(d1, reinterpret_cast<const uint32_t*>(P.desc2 + (size_t)i2 * 32));
+          best_merge(k1, d2, ((uint32_t)d << 16) | (uint32_t)jj, INT_MAX);
+        }
+#pragma unroll
+        for (int s = 32; s >= 1; s >>= 1) {
+          const uint32_t ok = __shfl_xor(k1, s, 64);
+          const int od = __shfl_xor(d2, s, 64);
+          best_merge(k1, d2, ok, od);
+        }
+        if (k1 != 0xFFFFFFFFu) {
+          best1 = (int)(k1 >> 16);
+          bidx2 = (int)f2[k1 & 0xFFFFu];
+          best2 = d2;
+        }
+      }
+      if (best1 < ORBM_TH_LOW && (float)best1 < P.nnratio * (float)best2) {
+        int bin = 0;
+        if (P.check_ori) {
+          float rot = P.ang1[(size_t)info.w * P.ang_stride] - P.ang2[(size_t)bidx2 * P.ang_stride];
+          if (rot < 0.0f) rot += 360.0f;
+          bin = (int)roundf(rot * factor);
+          if (bin == ORBM_HISTO) bin = 0;
+        }
+        if (lane == 0) {
+          bm[bidx2 >> 5] |= 1u << (bidx2 & 31);
+          ev[r] = make_int2(bidx2, bin);
+        }
+        __builtin_amdgcn_wave_barrier();
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// k_match_finalize: one workgroup per problem.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_match_finalize(const MProblem* __restrict__ probs,
+                                                        const int4* __restrict__ rowinfo,
+                                                        const int2* __restrict__ ev,
+                                                        int* __restrict__ last_scratch,
+                                                        const int* __restrict__ scratch_off) {
+  __shared__ int hist[ORBM_HISTO];
+  __shared__ int ind[3];
+  __shared__ int s_nev, s_nfilt;
+  const int p = blockIdx.x, tid = threadIdx.x;
+  const MProblem P = probs[p];
+  int* last = last_scratch + scratch_off[p];
+  for (int i = tid; i < P.n1; i += 256) {
+    P.match12[i] = -1;
+    last[i] = -1;
+  }
+  if (tid < ORBM_HISTO) hist[tid] = 0;
+  if (tid == 0) { s_nev = 0; s_nfilt = 0; }
+  __syncthreads();
+  int nev = 0;
+  for (int r = P.row_begin + tid; r < P.row_end; r += 256) {
+    const int2 e = ev[r];
+    if (e.x < 0) continue;
+    const int idx1 = rowinfo[r].w;
+    atomicMax(&last[idx1], r);
+    atomicAdd(&hist[e.y], 1);
+    ++nev;
+  }
+  atomicAdd(&s_nev, nev);
+  __syncthreads();
+  if (tid == 0) {  // ComputeThreeMaxima (ORBmatcher.cc:469-502)
+    int ti[3] = {-1, -1, -1}, tv[3] = {0, 0, 0};
+    for (int i = 0; i < ORBM_HISTO; ++i) {
+      const int v = hist[i];
+      for (int jj = 0; jj < 3; ++jj) {
+        if (v > tv[jj]) {
+          for (int k = 2; k > jj; --k) { tv[k] = tv[k - 1]; ti[k] = ti[k - 1]; }
+          tv[jj] = v;
+          ti[jj] = i;
+          break;
+        }
+      }
+    }
+    if (tv[1] < 0.1f * tv[0]) { ti[1] = -1; ti[2] = -1; }
+    else if (tv[2] < 0.1f * tv[0]) { ti[2] = -1; }
+    ind[0] = ti[0]; ind[1] = ti[1]; ind[2] = ti[2];
+  }
+  __syncthreads();
+  for (int r = P.row_begin + tid; r < P.row_end; r += 256) {
+    const int2 e = ev[r];
+    if (e.x < 0) continue;
+    const int idx1 = rowinfo[r].w;
+    if (last[idx1] == r) P.match12[idx1] = e.x;
+  }
+  __syncthreads();
+  int nf = 0;
+  if (P.check_ori) {
+    for (int r = P.row_begin + tid; r < P.row_end; r += 256) {
+      const int2 e = ev[r];
+      if (e.x < 0) continue;
+      if (e.y == ind[0] || e.y == ind[1] || e.y == ind[2]) continue;
+      P.match12[rowinfo[r].w] = -1;
+      ++nf;
+    }
+  }
+  atomicAdd(&s_nfilt, nf);
+  __syncthreads();
+  if (tid == 0) *P.nmatches = s_nev - s_nfilt;
+}
+
+// ---------------------------------------------------------------------------
+// k_match_select: top-`topn` keypoints of one frame by (response desc,
+// index asc), written in ascending index order (one vocabulary node).
+// grid (npairs, 2): y = side (0: frame A -> list1, 1: frame B -> list2).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_match_select(
+    MProblem* __restrict__ probs, MNodePair* __restrict__ nps, const orbx_keypoint* __restrict__ kps_a,
+    const int* __restrict__ count_a, const orbx_keypoint* __restrict__ kps_b,
+    const int* __restrict__ count_b, int kcap, int topn, uint32_t* __restrict__ sel) {
+  __shared__ int hist[256];
+  __shared__ int s_R, s_above, wtot[4];
+  const int p = blockIdx.x, side = blockIdx.y, tid = threadIdx.x;
+  const orbx_keypoint* kp = (side ? kps_b : kps_a) + (size_t)p * kcap;
+  const int K = side ? count_b[p] : count_a[p];
+  uint32_t* out = sel + ((size_t)p * 2 + side) * topn;
+  hist[tid] = 0;
+  __syncthreads();
+  for (int i = tid; i < K; i += 256) atomicAdd(&hist[(int)kp[i].response & 255], 1);
+  __syncthreads();
+  if (tid == 0) {
+    int R = -1, above = 0;
+    if (K > topn) {
+      int cum = 0;
+      for (int v = 255; v >= 0; --v) {
+        if (cum + hist[v] >= topn) { R = v; above = cum; break; }
+        cum += hist[v];
+      }
+    }
+    s_R = R;
+    s_above = above;
+  }
+  __syncthreads();
+  const int R = s_R, needEq = topn - s_above;
+  const int wave = tid >> 6, lane = tid & 63;
+  int nsel = 0, neq = 0;
+  for (int base = 0; base < K; base += 256) {
+    const int i = base + tid;
+    int resp = -2;
+    if (i < K) resp = (int)kp[i].response;
+    const bool eq = (i < K) && resp == R;
+    // rank among equal-response entries (ordered)
+    const uint64_t meq = __ballot(eq);
+    if (lane == 0) wtot[wave] = __popcll(meq);
+    __syncthreads();
+    int eqoff = neq;
+    for (int w = 0; w < wave; ++w) eqoff += wtot[w];
+    const int eqrank = eqoff + __popcll(meq & ((1ull << lane) - 1ull));
+    const int eqtot = wtot[0] + wtot[1] + wtot[2] + wtot[3];
+    __syncthreads();
+    const bool take = (i < K) && (resp > R || (eq && eqrank < needEq));
+    const uint64_t mt = __ballot(take);
+    if (lane == 0) wtot[wave] = __popcll(mt);
+    __syncthreads();
+    int off = nsel;
+    for (int w = 0; w < wave; ++w) off += wtot[w];
+    if (take) out[off + __popcll(mt & ((1ull << lane) - 1ull))] = (uint32_t)i;
+    nsel += wtot[0] + wtot[1] + wtot[2] + wtot[3];
+    neq += eqtot;
+    __syncthreads();
+  }
+  if (tid == 0) {
+    if (side == 0) { nps[p].n1 = nsel; probs[p].n1 = K; }
+    else { nps[p].n2 = nsel; probs[p].n2 = K; }
+  }
+}
+
+// DescriptorDistance over index pairs
+__global__ void k_hamming_pairs(const uint8_t* __restrict__ a, const uint8_t* __restrict__ b,
+                                const int32_t* __restrict__ ia, const int32_t* __restrict__ ib,
+                                int npairs, int32_t* __restrict__ dist) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= npairs) return;
+  dist[i] = hamming32(reinterpret_cast<const uint32_t*>(a + (size_t)ia[i] * 32),
+                      reinterpret_cast<const uint32_t*>(b + (size_t)ib[i] * 32));
+}
+
+}  // namespace orbx

@@ -1,0 +1,47 @@
+// match_internal.h -- device tables of the SearchByBoW pipeline.
+//
+// One "problem" = one ORBmatcher::SearchByBoW(KF1, KF2) call
+// (src/ORBmatcher.cc:278-366).  Its common vocabulary nodes become "node
+// pairs" (list1 = node's features in KF1, list2 = in KF2) in ascending NodeId
+// order.  Every list1 entry owns one "row" (row_base + position) of the
+// candidate / event arrays.
+#ifndef ORBX_MATCH_INTERNAL_H
+#define ORBX_MATCH_INTERNAL_H
+
+#include <stdint.h>
+
+#define ORBM_T 16          /* candidates kept per row                     */
+#define ORBM_TH_LOW 50     /* ORBmatcher::TH_LOW (ORBmatcher.cc:14)       */
+#define ORBM_HISTO 30      /* ORBmatcher::HISTO_LENGTH (ORBmatcher.cc:15) */
+#define ORBM_MAX_N2 65536  /* list positions / idx2 bitmap bound          */
+
+struct MProblem {
+  const uint8_t* desc1;
+  const uint8_t* desc2;
+  const float* ang1;
+  const float* ang2;
+  const uint8_t* valid1;
+  const uint8_t* valid2;
+  const uint32_t* feat1;
+  const uint32_t* feat2;
+  int32_t* match12;
+  int* nmatches;
+  int ang_stride;  /* floats between consecutive angles (1, or 7 for orbx_keypoint) */
+  int n1, n2;      /* features of KF1 / KF2 */
+  int np_begin, np_end;
+  int row_begin, row_end;
+  int check_ori;
+  float nnratio;
+  int sequential;  /* 1: one wave walks all node pairs in order (malformed FeatureVectors) */
+  int pad[2];
+};
+
+struct MNodePair {
+  int prob;
+  int off1, n1;  /* list1 = feat1[off1 .. off1+n1) */
+  int off2, n2;  /* list2 = feat2[off2 .. off2+n2) */
+  int row_base;
+  int pad;
+};
+
+#endif

@@ -1,0 +1,385 @@
+"""orbx -- Python host binding of liborbx.so (the MI355X ORB front end).
+
+Thin ctypes layer over the C ABI in include/orbx.h.  It mirrors the
+reference interfaces for tests and the benchmark:
+
+  Extractor      ORB_SLAM2::ORBextractor  (/root/reference/include/ORBextractor.h:25-91)
+  search_by_bow  ORBmatcher::SearchByBoW(KF, KF) (/root/reference/src/ORBmatcher.cc:278-366)
+  descriptor_distance_batch  ORBmatcher::DescriptorDistance (ORBmatcher.cc:896-908)
+  Plan / MatchPlan  batched device-resident throughput path (bench.py)
+
+The library is mandatory: importing this package raises if liborbx.so is
+missing, and every compute call runs the HIP kernels (there is no CPU path).
+"""
+import ctypes
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(os.path.dirname(HERE), "liborbx.so")
+
+if not os.path.exists(LIB_PATH):
+    raise ImportError("liborbx.so not built (%s): run __graft_entry__.build() or "
+                      "make -C orb-slam-system_amd" % LIB_PATH)
+
+try:
+    # Load torch (and its bundled libamdhip64.so.7) first: liborbx.so then binds to the
+    # same HIP runtime by SONAME, so one process never holds two HIP runtimes.
+    import torch as _torch  # noqa: F401
+except ImportError:  # pragma: no cover - torch is plumbing only
+    _torch = None
+
+_lib = ctypes.CDLL(LIB_PATH)
+
+KEYPOINT_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"),
+                           ("response", "<f4"), ("octave", "<i4"), ("class_id", "<i4")])
+assert KEYPOINT_DTYPE.itemsize == 28
+
+OK, ERR_ARG, ERR_CELL_ROI, ERR_LEVEL_SIZE, ERR_QUADTREE, ERR_CAPACITY, ERR_UNSUPPORTED, \
+    ERR_HIP, ERR_NO_DEVICE = 0, -1, -2, -3, -4, -5, -6, -7, -8
+
+EXPORTED = [
+    "orbx_abi_version", "orbx_status_string", "orbx_device_count", "orbx_tables",
+    "orbx_geometry_compute", "orbx_resize_tables", "orbx_extractor_create",
+    "orbx_extractor_destroy", "orbx_extractor_capacity", "orbx_extract", "orbx_extractor_level",
+    "orbx_plan_create", "orbx_plan_destroy", "orbx_plan_geometry", "orbx_plan_extract",
+    "orbx_plan_check", "orbx_stage_count", "orbx_stage_name", "orbx_plan_set_timing",
+    "orbx_plan_stage_times", "orbx_synth_frames", "orbm_search_by_bow",
+    "orbm_descriptor_distance_batch", "orbm_plan_create", "orbm_plan_destroy",
+    "orbm_plan_match_frames", "orbm_plan_set_timing", "orbm_plan_stage_times",
+]
+
+
+class Params(ctypes.Structure):
+    _fields_ = [("nfeatures", ctypes.c_int), ("scale_factor", ctypes.c_float),
+                ("nlevels", ctypes.c_int), ("ini_th_fast", ctypes.c_int),
+                ("min_th_fast", ctypes.c_int), ("cell_guard", ctypes.c_int)]
+
+
+def params(nfeatures, scale_factor, nlevels, ini_th, min_th, cell_guard="strict"):
+    return Params(nfeatures, scale_factor, nlevels, ini_th, min_th,
+                  1 if cell_guard in ("empty", 1, True) else 0)
+
+
+class Geometry(ctypes.Structure):
+    _fields_ = [("nlevels", ctypes.c_int)] + [
+        (n, ctypes.c_int * 32) for n in ("width", "height", "alias", "ncols", "nrows", "wcell",
+                                         "hcell", "ncells_bad", "features", "nini", "kcap_level")
+    ] + [("kcap", ctypes.c_int), ("pixels", ctypes.c_longlong), ("bytes_pyr_fast", ctypes.c_longlong)]
+
+    def level(self, name):
+        return list(getattr(self, name))[:self.nlevels]
+
+
+class BowFrame(ctypes.Structure):
+    _fields_ = [("n", ctypes.c_int), ("desc", ctypes.c_void_p), ("angle", ctypes.c_void_p),
+                ("valid", ctypes.c_void_p), ("nnodes", ctypes.c_int), ("node_id", ctypes.c_void_p),
+                ("node_off", ctypes.c_void_p), ("feat", ctypes.c_void_p)]
+
+
+P, I, F, SZ = ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.c_size_t
+_sig = {
+    "orbx_abi_version": (I, []),
+    "orbx_status_string": (ctypes.c_char_p, [I]),
+    "orbx_device_count": (I, []),
+    "orbx_tables": (I, [P, P, P, P, P, P, P]),
+    "orbx_geometry_compute": (I, [P, I, I, P]),
+    "orbx_resize_tables": (I, [P, I, I, I, P, P, P, P]),
+    "orbx_extractor_create": (I, [P, I, P]),
+    "orbx_extractor_destroy": (I, [P]),
+    "orbx_extractor_capacity": (I, [P, I, I, P]),
+    "orbx_extract": (I, [P, P, I, I, SZ, P, I, P, P]),
+    "orbx_extractor_level": (I, [P, I, P, SZ, P, P]),
+    "orbx_plan_create": (I, [P, I, I, I, I, P]),
+    "orbx_plan_destroy": (I, [P]),
+    "orbx_plan_geometry": (I, [P, P]),
+    "orbx_plan_extract": (I, [P, P, I, SZ, SZ, P, P, P, P]),
+    "orbx_plan_check": (I, [P, P]),
+    "orbx_stage_count": (I, []),
+    "orbx_stage_name": (ctypes.c_char_p, [I]),
+    "orbx_plan_set_timing": (I, [P, I]),
+    "orbx_plan_stage_times": (I, [P, P, P, I]),
+    "orbx_synth_frames": (I, [P, I, I, SZ, I, I, I, P]),
+    "orbm_search_by_bow": (I, [P, P, F, I, I, P, P]),
+    "orbm_descriptor_distance_batch": (I, [P, I, P, I, P, P, I, I, P]),
+    "orbm_plan_create": (I, [I, I, I, I, P]),
+    "orbm_plan_destroy": (I, [P]),
+    "orbm_plan_match_frames": (I, [P, I, P, P, P, P, P, P, F, I, P, P, P]),
+    "orbm_plan_set_timing": (I, [P, I]),
+    "orbm_plan_stage_times": (I, [P, P, P, I]),
+}
+for _n, (_r, _a) in _sig.items():
+    _f = getattr(_lib, _n)
+    _f.restype = _r
+    _f.argtypes = _a
+
+
+def lib():
+    return _lib
+
+
+class OrbxError(RuntimeError):
+    def __init__(self, code, what=""):
+        msg = _lib.orbx_status_string(code).decode()
+        super().__init__("%s: %s (%d)" % (what, msg, code) if what else "%s (%d)" % (msg, code))
+        self.code = code
+
+
+def _check(rc, what=""):
+    if rc != OK:
+        raise OrbxError(rc, what)
+    return rc
+
+
+def _p(a):
+    return None if a is None else a.ctypes.data_as(ctypes.c_void_p)
+
+
+def device_count():
+    return _lib.orbx_device_count()
+
+
+def stage_names():
+    return [_lib.orbx_stage_name(i).decode() for i in range(_lib.orbx_stage_count())]
+
+
+# --------------------------------------------------------------------------- host-only tables
+def tables(prm):
+    L = prm.nlevels
+    s, inv, s2, inv2 = (np.zeros(L, np.float32) for _ in range(4))
+    fpl = np.zeros(L, np.int32)
+    umax = np.zeros(16, np.int32)
+    _check(_lib.orbx_tables(ctypes.byref(prm), _p(s), _p(inv), _p(s2), _p(inv2), _p(fpl), _p(umax)))
+    return dict(scale=s, inv_scale=inv, sigma2=s2, inv_sigma2=inv2, features_per_level=fpl,
+                umax=umax)
+
+
+def geometry(prm, width, height):
+    g = Geometry()
+    _check(_lib.orbx_geometry_compute(ctypes.byref(prm), width, height, ctypes.byref(g)), "geometry")
+    return g
+
+
+def resize_tables(prm, width, height, level):
+    g = geometry(prm, width, height)
+    w, h = g.width[level], g.height[level]
+    xofs = np.zeros(w, np.int32)
+    alpha = np.zeros(2 * w, np.int16)
+    yofs = np.zeros(h, np.int32)
+    beta = np.zeros(2 * h, np.int16)
+    _check(_lib.orbx_resize_tables(ctypes.byref(prm), width, height, level, _p(xofs), _p(alpha),
+                                   _p(yofs), _p(beta)))
+    return xofs, alpha.reshape(w, 2), yofs, beta.reshape(h, 2)
+
+
+# --------------------------------------------------------------------------- ORBextractor
+class Extractor:
+    """ORB_SLAM2::ORBextractor(nfeatures, scaleFactor, nlevels, iniThFAST, minThFAST)."""
+
+    def __init__(self, nfeatures, scale_factor, nlevels, ini_th, min_th, cell_guard="strict",
+                 device=0):
+        self.params = params(nfeatures, scale_factor, nlevels, ini_th, min_th, cell_guard)
+        self._t = tables(self.params)
+        h = ctypes.c_void_p()
+        _check(_lib.orbx_extractor_create(ctypes.byref(self.params), device, ctypes.byref(h)),
+               "orbx_extractor_create")
+        self._h = h
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            _lib.orbx_extractor_destroy(self._h)
+            self._h = None
+
+    # getters (ORBextractor.h:43-63)
+    def GetLevels(self):
+        return self.params.nlevels
+
+    def GetScaleFactor(self):
+        return self.params.scale_factor
+
+    def GetScaleFactors(self):
+        return self._t["scale"].tolist()
+
+    def GetInverseScaleFactors(self):
+        return self._t["inv_scale"].tolist()
+
+    def GetScaleSigmaSquares(self):
+        return self._t["sigma2"].tolist()
+
+    def GetInverseScaleSigmaSquares(self):
+        return self._t["inv_sigma2"].tolist()
+
+    def __call__(self, image, mask=None):
+        """operator()(image, mask, keypoints, descriptors) -> (keypoints, descriptors)."""
+        return self.extract(image)
+
+    def extract(self, image):
+        img = np.ascontiguousarray(image, dtype=np.uint8)
+        if img.ndim != 2:
+            raise OrbxError(ERR_ARG, "CV_8UC1 image expected")
+        h, w = img.shape
+        cap = ctypes.c_int(0)
+        _check(_lib.orbx_extractor_capacity(self._h, w, h, ctypes.byref(cap)), "capacity")
+        kps = np.zeros(max(cap.value, 1), KEYPOINT_DTYPE)
+        desc = np.zeros((max(cap.value, 1), 32), np.uint8)
+        n = ctypes.c_int(0)
+        _check(_lib.orbx_extract(self._h, _p(img), w, h, w, _p(kps), cap.value, _p(desc),
+                                 ctypes.byref(n)), "orbx_extract")
+        return kps[:n.value].copy(), desc[:n.value].copy()
+
+    def level(self, l):
+        w, h = ctypes.c_int(), ctypes.c_int()
+        _check(_lib.orbx_extractor_level(self._h, l, None, 0, ctypes.byref(w), ctypes.byref(h)))
+        out = np.zeros((h.value, w.value), np.uint8)
+        _check(_lib.orbx_extractor_level(self._h, l, _p(out), w.value, None, None))
+        return out
+
+
+# --------------------------------------------------------------------------- ORBmatcher
+def _bow_struct(k, keep):
+    desc = np.ascontiguousarray(k["desc"], np.uint8).reshape(-1, 32)
+    ang = np.ascontiguousarray(k["angle"], np.float32)
+    valid = None if k.get("valid") is None else np.ascontiguousarray(k["valid"], np.uint8)
+    nid = np.ascontiguousarray(k["node_id"], np.uint32)
+    off = np.ascontiguousarray(k["off"], np.uint32)
+    feat = np.ascontiguousarray(k["feat"], np.uint32)
+    keep.extend([desc, ang, valid, nid, off, feat])
+    return BowFrame(len(desc), _p(desc), _p(ang), _p(valid), len(nid), _p(nid), _p(off), _p(feat))
+
+
+def search_by_bow(kf1, kf2, nnratio=0.6, check_ori=True, device=0):
+    """SearchByBoW(KF1, KF2): returns (match12 int32[N1], nmatches)."""
+    keep = []
+    b1, b2 = _bow_struct(kf1, keep), _bow_struct(kf2, keep)
+    m = np.full(max(b1.n, 1), -1, np.int32)
+    nm = ctypes.c_int(0)
+    _check(_lib.orbm_search_by_bow(ctypes.byref(b1), ctypes.byref(b2), float(nnratio),
+                                   1 if check_ori else 0, device, _p(m), ctypes.byref(nm)),
+           "orbm_search_by_bow")
+    return m[:b1.n].copy(), nm.value
+
+
+def descriptor_distance_batch(a, b, ia, ib, device=0):
+    a = np.ascontiguousarray(a, np.uint8).reshape(-1, 32)
+    b = np.ascontiguousarray(b, np.uint8).reshape(-1, 32)
+    ia = np.ascontiguousarray(ia, np.int32)
+    ib = np.ascontiguousarray(ib, np.int32)
+    out = np.zeros(len(ia), np.int32)
+    _check(_lib.orbm_descriptor_distance_batch(_p(a), len(a), _p(b), len(b), _p(ia), _p(ib),
+                                               len(ia), device, _p(out)))
+    return out
+
+
+# --------------------------------------------------------------------------- batched device path
+def _stream_handle(stream):
+    if stream is None:
+        import torch
+        return torch.cuda.current_stream().cuda_stream
+    return getattr(stream, "cuda_stream", stream)
+
+
+class Plan:
+    """Batched device-resident extraction of `max_batch` frames of W x H."""
+
+    def __init__(self, prm, width, height, max_batch, device=0):
+        import torch
+        self.params, self.W, self.H, self.max_batch, self.device = prm, width, height, max_batch, device
+        h = ctypes.c_void_p()
+        _check(_lib.orbx_plan_create(ctypes.byref(prm), width, height, max_batch, device,
+                                     ctypes.byref(h)), "orbx_plan_create")
+        self._h = h
+        self.geo = Geometry()
+        _check(_lib.orbx_plan_geometry(self._h, ctypes.byref(self.geo)))
+        self.kcap = self.geo.kcap
+        dev = torch.device("cuda", device)
+        self.kps = torch.empty((max_batch, max(self.kcap, 1), 28), dtype=torch.uint8, device=dev)
+        self.desc = torch.empty((max_batch, max(self.kcap, 1), 32), dtype=torch.uint8, device=dev)
+        self.counts = torch.zeros(max_batch, dtype=torch.int32, device=dev)
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            _lib.orbx_plan_destroy(self._h)
+            self._h = None
+
+    def extract(self, frames, stream=None):
+        """frames: cuda uint8 tensor [B, H, W] (row stride W).  Async."""
+        B = frames.shape[0]
+        assert frames.dtype.itemsize == 1 and frames.is_contiguous()
+        assert frames.shape[1] == self.H and frames.shape[2] == self.W and B <= self.max_batch
+        _check(_lib.orbx_plan_extract(self._h, frames.data_ptr(), B, self.W * self.H, self.W,
+                                      self.kps.data_ptr(), self.desc.data_ptr(),
+                                      self.counts.data_ptr(), _stream_handle(stream)),
+               "orbx_plan_extract")
+
+    def check(self, stream=None):
+        _check(_lib.orbx_plan_check(self._h, _stream_handle(stream)), "orbx_plan_check")
+
+    def set_timing(self, enable):
+        _check(_lib.orbx_plan_set_timing(self._h, 1 if enable else 0))
+
+    def stage_times(self):
+        n = _lib.orbx_stage_count()
+        ms = np.zeros(n, np.float64)
+        cnt = np.zeros(n, np.int32)
+        _check(_lib.orbx_plan_stage_times(self._h, _p(ms), _p(cnt), n))
+        return {name: (ms[i], int(cnt[i])) for i, name in enumerate(stage_names())}
+
+    def results(self, B):
+        """host copies: list of (keypoints structured array, descriptors) for frames 0..B-1"""
+        counts = self.counts[:B].cpu().numpy()
+        kraw = self.kps[:B].cpu().numpy()
+        draw = self.desc[:B].cpu().numpy()
+        out = []
+        for f in range(B):
+            n = int(counts[f])
+            k = kraw[f, :n].copy().view(KEYPOINT_DTYPE).reshape(n)
+            out.append((k, draw[f, :n].copy()))
+        return out
+
+
+class MatchPlan:
+    """Batched brute-force SearchByBoW between extractor frames (single node, top-N)."""
+
+    def __init__(self, max_pairs, kcap, topn=2000, device=0):
+        import torch
+        h = ctypes.c_void_p()
+        _check(_lib.orbm_plan_create(max_pairs, kcap, topn, device, ctypes.byref(h)),
+               "orbm_plan_create")
+        self._h, self.kcap, self.topn, self.max_pairs = h, kcap, topn, max_pairs
+        dev = torch.device("cuda", device)
+        self.match12 = torch.empty((max_pairs, kcap), dtype=torch.int32, device=dev)
+        self.nmatches = torch.zeros(max_pairs, dtype=torch.int32, device=dev)
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            _lib.orbm_plan_destroy(self._h)
+            self._h = None
+
+    def match(self, npairs, kps_a, desc_a, cnt_a, kps_b, desc_b, cnt_b, nnratio=0.6,
+              check_ori=True, stream=None, out_offset=0):
+        m = self.match12[out_offset:]
+        nm = self.nmatches[out_offset:]
+        _check(_lib.orbm_plan_match_frames(self._h, npairs, kps_a.data_ptr(), desc_a.data_ptr(),
+                                           cnt_a.data_ptr(), kps_b.data_ptr(), desc_b.data_ptr(),
+                                           cnt_b.data_ptr(), float(nnratio), 1 if check_ori else 0,
+                                           m.data_ptr(), nm.data_ptr(), _stream_handle(stream)),
+               "orbm_plan_match_frames")
+
+    def set_timing(self, enable):
+        _check(_lib.orbm_plan_set_timing(self._h, 1 if enable else 0))
+
+    def stage_times(self):
+        n = _lib.orbx_stage_count()
+        ms = np.zeros(n, np.float64)
+        cnt = np.zeros(n, np.int32)
+        _check(_lib.orbm_plan_stage_times(self._h, _p(ms), _p(cnt), n))
+        return {name: (ms[i], int(cnt[i])) for i, name in enumerate(stage_names())}
+
+
+def synth_frames(out, first_idx, kind="rects", stream=None):
+    """Fill a cuda uint8 tensor [B, H, W] with synthetic frames (orbx/synth.py spec)."""
+    from . import synth
+    B, H, W = out.shape
+    _check(_lib.orbx_synth_frames(out.data_ptr(), W, H, W * H, B, first_idx, synth.KINDS[kind],
+                                  _stream_handle(stream)), "orbx_synth_frames")

@@ -1,0 +1,189 @@
+"""GPU parity: liborbx.so (HIP kernels through the C ABI) vs the oracle.
+
+Bit-exact on every field: keypoint x/y/size/angle/response/octave/class_id,
+descriptor bytes, pyramid pixels, match indices and counts.
+"""
+import numpy as np
+import pytest
+
+from orbx import synth
+
+pytestmark = pytest.mark.gpu
+
+EXTRACT_CASES = [
+    # (w, h, nfeatures, nlevels, guard, kind, frame_idx)
+    (640, 480, 1000, 8, "strict", "rects", 0),     # BASELINE config 1
+    (640, 480, 1000, 8, "strict", "noise", 1),
+    (640, 480, 1000, 8, "strict", "flat", 2),      # K == 0 path
+    (640, 480, 1000, 1, "strict", "rects", 3),     # config 2: single level
+    (1241, 376, 2000, 8, "strict", "rects", 4),    # config 5 shape (KITTI)
+    (752, 480, 1200, 8, "strict", "noise", 5),     # EuRoC shape
+    (1920, 1080, 2000, 8, "empty", "rects", 6),    # config 3 (cell_guard=empty)
+    (1920, 1080, 2000, 8, "empty", "noise", 7),
+]
+
+
+def _cmp_kps(a, b, what):
+    assert len(a) == len(b), "%s: count %d vs %d" % (what, len(a), len(b))
+    for f in a.dtype.names:
+        if not np.array_equal(a[f], b[f]):
+            bad = np.nonzero(a[f] != b[f])[0]
+            raise AssertionError("%s: field %s differs at %d rows, first %d: %r vs %r" %
+                                 (what, f, len(bad), bad[0], a[bad[0]], b[bad[0]]))
+
+
+@pytest.mark.parametrize("w,h,nf,L,guard,kind,idx", EXTRACT_CASES)
+def test_extract_matches_oracle(gpu, oracle, w, h, nf, L, guard, kind, idx):
+    img = synth.frame(w, h, idx, kind)
+    ref = oracle.Extractor(nf, 1.2, L, 20, 7, cell_guard=guard)
+    rk, rd = ref.extract(img)
+    ex = gpu.Extractor(nf, 1.2, L, 20, 7, cell_guard=guard)
+    k, d = ex.extract(img)
+    _cmp_kps(k, rk, "keypoints")
+    assert np.array_equal(d, rd), "descriptors differ"
+    for l in range(L):
+        assert np.array_equal(ex.level(l), ref.level(l)), "pyramid level %d" % l
+
+
+def test_strict_guard_1080p_raises(gpu):
+    ex = gpu.Extractor(2000, 1.2, 8, 20, 7, cell_guard="strict")
+    with pytest.raises(gpu.OrbxError) as e:
+        ex.extract(synth.frame(1920, 1080, 0))
+    assert e.value.code == gpu.ERR_CELL_ROI
+
+
+def test_synth_device_matches_numpy(gpu):
+    import torch
+    for kind in ("rects", "noise", "flat"):
+        t = torch.empty((3, 376, 1241), dtype=torch.uint8, device="cuda")
+        gpu.synth_frames(t, 10, kind)
+        torch.cuda.synchronize()
+        ref = synth.frames(1241, 376, 10, 3, kind)
+        assert np.array_equal(t.cpu().numpy(), ref), kind
+
+
+def test_batched_plan_matches_single(gpu, oracle):
+    import torch
+    W, H, B = 640, 480, 5
+    prm = gpu.params(1000, 1.2, 8, 20, 7)
+    plan = gpu.Plan(prm, W, H, B)
+    frames = torch.from_numpy(synth.frames(W, H, 20, B, "rects")).cuda()
+    plan.extract(frames)
+    plan.check()
+    res = plan.results(B)
+    for f in range(B):
+        ref = oracle.Extractor(1000, 1.2, 8, 20, 7)
+        rk, rd = ref.extract(synth.frame(W, H, 20 + f))
+        _cmp_kps(res[f][0], rk, "frame %d" % f)
+        assert np.array_equal(res[f][1], rd)
+
+
+def _random_bow(rng, n, nnodes, vocab, desc=None, dup=False):
+    if desc is None:
+        desc = rng.integers(0, 256, (n, 32), dtype=np.uint8)
+    ang = rng.uniform(0, 360, n).astype(np.float32)
+    valid = (rng.uniform(size=n) > 0.1).astype(np.uint8)
+    nodes = np.sort(rng.choice(vocab, nnodes, replace=False)).astype(np.uint32)
+    assign = rng.integers(0, nnodes, n)
+    off = [0]
+    feat = []
+    for j in range(nnodes):
+        f = np.nonzero(assign == j)[0].tolist()
+        if dup and j > 0 and len(feat) > 0:
+            f = f + [feat[0]]
+        feat.extend(f)
+        off.append(len(feat))
+    return dict(desc=desc, angle=ang, valid=valid, node_id=nodes,
+                off=np.array(off, np.uint32), feat=np.array(feat, np.uint32))
+
+
+def _correlated(rng, base, flips):
+    d = base.copy()
+    for i in range(len(d)):
+        bits = rng.choice(256, flips[i], replace=False)
+        for b in bits:
+            d[i, b // 8] ^= np.uint8(1 << (b % 8))
+    return d
+
+
+@pytest.mark.parametrize("seed", range(6))
+@pytest.mark.parametrize("nnratio,check_ori", [(0.6, True), (0.75, True), (0.9, False)])
+def test_search_by_bow_matches_oracle(gpu, oracle, seed, nnratio, check_ori):
+    rng = np.random.default_rng(seed)
+    n1, n2 = int(rng.integers(50, 600)), int(rng.integers(50, 600))
+    d1 = rng.integers(0, 256, (n1, 32), dtype=np.uint8)
+    src = d1[rng.integers(0, n1, n2)]
+    d2 = _correlated(rng, src, rng.integers(0, 60, n2))
+    kf1 = _random_bow(rng, n1, int(rng.integers(1, 12)), 40, d1)
+    kf2 = _random_bow(rng, n2, int(rng.integers(1, 12)), 40, d2)
+    m, nm = gpu.search_by_bow(kf1, kf2, nnratio, check_ori)
+    rm, rnm = oracle.search_by_bow(kf1, kf2, nnratio, check_ori)
+    assert nm == rnm
+    assert np.array_equal(m, rm)
+
+
+def test_search_by_bow_single_node_bruteforce(gpu, oracle):
+    rng = np.random.default_rng(7)
+    n = 2000
+    d1 = rng.integers(0, 256, (n, 32), dtype=np.uint8)
+    d2 = _correlated(rng, d1[rng.permutation(n)], rng.integers(0, 40, n))
+    one = lambda d: dict(desc=d, angle=rng.uniform(0, 360, n).astype(np.float32), valid=None,
+                         node_id=np.array([7], np.uint32), off=np.array([0, n], np.uint32),
+                         feat=np.arange(n, dtype=np.uint32))
+    kf1, kf2 = one(d1), one(d2)
+    for ratio in (0.6, 0.75):
+        m, nm = gpu.search_by_bow(kf1, kf2, ratio, True)
+        rm, rnm = oracle.search_by_bow(kf1, kf2, ratio, True)
+        assert nm == rnm and np.array_equal(m, rm)
+
+
+def test_search_by_bow_duplicate_features_sequential(gpu, oracle):
+    rng = np.random.default_rng(11)
+    d = rng.integers(0, 256, (300, 32), dtype=np.uint8)
+    kf1 = _random_bow(rng, 300, 6, 20, d, dup=True)
+    kf2 = _random_bow(rng, 300, 6, 20, _correlated(rng, d, rng.integers(0, 30, 300)), dup=True)
+    m, nm = gpu.search_by_bow(kf1, kf2, 0.75, True)
+    rm, rnm = oracle.search_by_bow(kf1, kf2, 0.75, True)
+    assert nm == rnm and np.array_equal(m, rm)
+
+
+def test_descriptor_distance_batch(gpu, oracle):
+    rng = np.random.default_rng(3)
+    a = rng.integers(0, 256, (100, 32), dtype=np.uint8)
+    b = rng.integers(0, 256, (80, 32), dtype=np.uint8)
+    ia = rng.integers(0, 100, 1000).astype(np.int32)
+    ib = rng.integers(0, 80, 1000).astype(np.int32)
+    got = gpu.descriptor_distance_batch(a, b, ia, ib)
+    ref = np.array([oracle.descriptor_distance(a[i], b[j]) for i, j in zip(ia, ib)])
+    assert np.array_equal(got, ref)
+
+
+def _topn_bow(k, d, topn):
+    order = sorted(range(len(k)), key=lambda i: (-float(k["response"][i]), i))[:topn]
+    sel = np.sort(np.array(order, np.uint32))
+    return dict(desc=d, angle=k["angle"].astype(np.float32), valid=None,
+                node_id=np.array([0], np.uint32), off=np.array([0, len(sel)], np.uint32), feat=sel)
+
+
+@pytest.mark.parametrize("W,H,nf,kind", [(640, 480, 1000, "noise"), (1920, 1080, 2000, "rects")])
+def test_match_plan_matches_oracle(gpu, oracle, W, H, nf, kind):
+    import torch
+    B = 4
+    guard = "empty" if W == 1920 else "strict"
+    prm = gpu.params(nf, 1.2, 8, 20, 7, guard)
+    plan = gpu.Plan(prm, W, H, B)
+    frames = torch.from_numpy(synth.frames(W, H, 40, B, kind)).cuda()
+    plan.extract(frames)
+    mp = gpu.MatchPlan(B - 1, plan.kcap, topn=nf)
+    mp.match(B - 1, plan.kps[1:], plan.desc[1:], plan.counts[1:], plan.kps, plan.desc,
+             plan.counts, 0.75, True)
+    plan.check()
+    torch.cuda.synchronize()
+    res = plan.results(B)
+    m12 = mp.match12.cpu().numpy()
+    nm = mp.nmatches.cpu().numpy()
+    for p in range(B - 1):
+        (ka, da), (kb, db) = res[p + 1], res[p]
+        rm, rnm = oracle.search_by_bow(_topn_bow(ka, da, nf), _topn_bow(kb, db, nf), 0.75, True)
+        assert nm[p] == rnm
+        assert np.array_equal(m12[p, :len(ka)], rm)
