@@ -1,0 +1,221 @@
+"""Oracle (CPU restatement) known-answer tests and golden-fixture pins.
+
+Known answers come from the reference source itself (tables, pattern
+facts) or from definitions independent of the oracle's code (brute-force
+FAST by its definition, numpy Hamming, numpy separable blur).
+"""
+import glob
+import os
+import re
+
+import numpy as np
+import pytest
+
+from orbx import synth
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+REF_SRC = "/root/reference/src/ORBextractor.cc"
+
+
+def test_features_per_level(oracle):
+    # ORBextractor.cc:141-151 for the configs' nfeatures (1000 TUM, 2000 KITTI, 1200 EuRoC)
+    cases = {1000: [217, 181, 151, 126, 105, 87, 73, 60],
+             2000: [434, 362, 302, 251, 209, 175, 145, 122],
+             1200: [261, 217, 181, 151, 126, 105, 87, 72]}
+    for nf, want in cases.items():
+        t = oracle.Extractor(nf, 1.2, 8, 20, 7).tables()
+        assert t["features_per_level"].tolist() == want
+    assert oracle.Extractor(1000, 1.2, 1, 20, 7).tables()["features_per_level"].tolist() == [1000]
+
+
+def test_scale_table_partial_sum_semantics(oracle):
+    # std::partial_sum(begin, end-1, begin+1, op) stores d_first[0] = first[0]:
+    # mvScaleFactor = [1, 1, s, s^2, ...] (ORBextractor.cc:123-124)
+    t = oracle.Extractor(1000, 1.2, 8, 20, 7).tables()
+    s = t["scale"]
+    assert s[0] == 1.0 and s[1] == 1.0
+    acc = np.float32(1.0)
+    for i in range(2, 8):
+        acc = np.float32(np.float64(acc) * np.float64(np.float32(1.2)))
+        assert s[i] == acc
+    assert np.array_equal(t["inv_scale"], (np.float32(1) / s).astype(np.float32))
+
+
+def test_umax(oracle):
+    t = oracle.Extractor(1000, 1.2, 8, 20, 7).tables()
+    assert t["umax"].tolist() == [15, 15, 15, 15, 14, 14, 14, 13, 13, 12, 11, 10, 9, 8, 6, 3]
+    # disk of IC_Angle has 749 pixels
+    um = t["umax"]
+    assert 31 + 2 * sum(2 * um[v] + 1 for v in range(1, 16)) == 749
+
+
+def _inc_pattern():
+    path = os.path.join(os.path.dirname(GOLDEN), "..", "orb-slam-system_amd", "csrc",
+                        "brief_pattern.inc")
+    txt = open(path).read()
+    body = txt[txt.index("{", txt.index("ORBX_BRIEF_PATTERN")) + 1:]
+    vals = [int(v) for v in re.findall(r"-?\d+", body)]
+    return np.array(vals[:1024]).reshape(256, 4)
+
+
+def test_brief_pattern_facts():
+    pat = _inc_pattern()
+    assert (pat[182:] == 0).all(), "pairs 182..255 must be degenerate (728 initialisers)"
+    assert (pat[:182] != 0).any(axis=1).all()
+    assert np.abs(pat).max() <= 13
+
+
+@pytest.mark.skipif(not os.path.exists(REF_SRC), reason="reference source not mounted")
+def test_brief_pattern_matches_reference_source():
+    txt = open(REF_SRC).read()
+    m = re.search(r"bit_pattern_31_\s*\[\s*256\s*\*\s*4\s*\]\s*=\s*\{(.*?)\};", txt, re.S)
+    vals = [int(v) for v in re.findall(r"-?\d+", m.group(1))]
+    assert len(vals) == 728
+    full = np.array(vals + [0] * (1024 - 728)).reshape(256, 4)
+    assert np.array_equal(full, _inc_pattern())
+
+
+def test_gaussian_kernel(oracle):
+    assert oracle.gaussian_kernel7().tolist() == [18, 34, 48, 56, 48, 34, 18]
+
+
+def test_fast_atan2(oracle):
+    rng = np.random.default_rng(0)
+    for _ in range(2000):
+        y, x = rng.integers(-50000, 50000, 2)
+        a = oracle.fast_atan2(y, x)
+        assert 0.0 <= a <= 360.0
+        ref = np.degrees(np.arctan2(y, x)) % 360.0
+        d = abs(a - ref)
+        assert min(d, 360 - d) < 0.05
+
+
+def _fast_bruteforce(img, th):
+    """FAST-9 by definition + cornerScore as max-over-arcs + strict 3x3 NMS."""
+    img = img.astype(int)
+    h, w = img.shape
+    circ = [(0, 3), (1, 3), (2, 2), (3, 1), (3, 0), (3, -1), (2, -2), (1, -3), (0, -3), (-1, -3),
+            (-2, -2), (-3, -1), (-3, 0), (-3, 1), (-2, 2), (-1, 3)]
+    score = np.zeros((h, w), int)
+    corner = np.zeros((h, w), bool)
+    for y in range(3, h - 3):
+        for x in range(3, w - 3):
+            p = img[y, x]
+            ring = [img[y + dy, x + dx] for dx, dy in circ]
+            best = -1
+            for s in range(16):
+                arc = [ring[(s + k) % 16] for k in range(9)]
+                best = max(best, min(p - v for v in arc), min(v - p for v in arc))
+            if best > th:
+                corner[y, x] = True
+                score[y, x] = best - 1
+    out = []
+    for y in range(3, h - 3):
+        for x in range(3, w - 3):
+            if not corner[y, x]:
+                continue
+            ok = all(score[y, x] > (score[y + dy, x + dx] if 3 <= y + dy < h - 3 and 3 <= x + dx < w - 3 else 0)
+                     for dy in (-1, 0, 1) for dx in (-1, 0, 1) if dx or dy)
+            if ok:
+                out.append((x, y, score[y, x]))
+    return out
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_fast_detect_vs_definition(oracle, seed):
+    rng = np.random.default_rng(seed)
+    img = rng.integers(0, 256, (24, 30)).astype(np.uint8)
+    if seed % 2:
+        img = np.full((24, 30), 100, np.uint8)
+        for _ in range(6):
+            y, x = rng.integers(3, 21), rng.integers(3, 27)
+            img[y, x] = rng.choice([0, 255])
+    for th in (7, 20):
+        k = oracle.fast_detect(img, th)
+        got = [(int(a), int(b), int(c)) for a, b, c in zip(k["x"], k["y"], k["response"])]
+        assert got == _fast_bruteforce(img, th)
+
+
+def test_blur_vs_numpy(oracle):
+    rng = np.random.default_rng(1)
+    img = rng.integers(0, 256, (37, 53)).astype(np.uint8)
+    k = np.array([18, 34, 48, 56, 48, 34, 18])
+    pad = np.pad(img.astype(np.int64), 3, mode="reflect")  # numpy 'reflect' == REFLECT_101
+    H = sum(k[i] * pad[:, i:i + 53] for i in range(7))
+    V = sum(k[j] * H[j:j + 37, :] for j in range(7))
+    want = ((V + 32768) >> 16).astype(np.uint8)
+    assert np.array_equal(oracle.gaussian_blur7(img), want)
+    flat = np.full((20, 20), 77, np.uint8)
+    assert (oracle.gaussian_blur7(flat) == 77).all()
+
+
+def test_resize_identity_and_constant(oracle):
+    img = np.random.default_rng(2).integers(0, 256, (50, 60)).astype(np.uint8)
+    assert np.array_equal(oracle.resize_linear(img, 60, 50), img)
+    flat = np.full((120, 160), 200, np.uint8)
+    assert (oracle.resize_linear(flat, 133, 100) == 200).all()
+
+
+def test_brief_angle0_vs_pattern(oracle):
+    rng = np.random.default_rng(4)
+    img = rng.integers(0, 256, (64, 64)).astype(np.uint8)
+    d = oracle.brief_descriptor(img, 32, 32, 0.0)
+    pat = _inc_pattern()
+    bits = [img[32 + y0, 32 + x0] < img[32 + y1, 32 + x1] for x0, y0, x1, y1 in pat]
+    want = np.packbits(np.array(bits, np.uint8).reshape(32, 8)[:, ::-1], axis=1).ravel()
+    assert np.array_equal(d, want)
+    assert (d[23:] == 0).all()
+
+
+def test_descriptor_distance(oracle):
+    rng = np.random.default_rng(5)
+    for _ in range(200):
+        a, b = rng.integers(0, 256, (2, 32)).astype(np.uint8)
+        want = int(np.unpackbits(a ^ b).sum())
+        assert oracle.descriptor_distance(a, b) == want
+
+
+def test_search_by_bow_toy(oracle):
+    # idx1 0 -> idx2 1 (dist 0); idx1 1 shares nothing (dist >= 50); node 5 only in kf1
+    z = np.zeros((3, 32), np.uint8)
+    d1 = z.copy()
+    d1[1] = 0xFF
+    d2 = z.copy()
+    d2[0, :8] = 0xFF   # dist 64 to d1[0]
+    d2[2] = 0xF0
+    kf1 = dict(desc=d1, angle=np.array([10, 20, 30], np.float32), valid=None,
+               node_id=np.array([3, 5], np.uint32), off=np.array([0, 2, 3], np.uint32),
+               feat=np.array([0, 1, 2], np.uint32))
+    kf2 = dict(desc=d2, angle=np.array([0, 10, 0], np.float32), valid=None,
+               node_id=np.array([3], np.uint32), off=np.array([0, 3], np.uint32),
+               feat=np.array([0, 1, 2], np.uint32))
+    m, n = oracle.search_by_bow(kf1, kf2, 0.6, True)
+    assert n == 1 and m.tolist() == [1, -1, -1]
+
+
+@pytest.mark.parametrize("path", sorted(glob.glob(os.path.join(GOLDEN, "extract_*.npz"))),
+                         ids=lambda p: os.path.basename(p))
+def test_oracle_reproduces_golden(oracle, path):
+    g = np.load(path)
+    w, h, nf, L, guard, kind, idx = g["spec"].tolist()
+    kinds = {v: k for k, v in synth.KINDS.items()}
+    e = oracle.Extractor(nf, 1.2, L, 20, 7, cell_guard="empty" if guard else "strict")
+    k, d = e.extract(synth.frame(w, h, idx, kinds[kind]))
+    assert np.array_equal(k.view(np.uint8), g["keypoints"])
+    assert np.array_equal(d, g["descriptors"])
+
+
+def _golden_kfs(g):
+    kf1 = dict(desc=g["d1"], angle=g["a1"], valid=g["v1"], node_id=g["nid1"], off=g["off1"], feat=g["f1"])
+    kf2 = dict(desc=g["d2"], angle=g["a2"], valid=g["v2"], node_id=g["nid2"], off=g["off2"], feat=g["f2"])
+    return kf1, kf2
+
+
+def test_oracle_search_by_bow_golden(oracle):
+    g = np.load(os.path.join(GOLDEN, "search_by_bow_multinode.npz"))
+    kf1, kf2 = _golden_kfs(g)
+    for ratio, ori in ((0.6, True), (0.75, True), (0.75, False)):
+        tag = "r%02d_o%d" % (int(ratio * 100), int(ori))
+        m, n = oracle.search_by_bow(kf1, kf2, ratio, ori)
+        assert n == int(g["n_" + tag][0])
+        assert np.array_equal(m, g["match_" + tag])

@@ -1,0 +1,90 @@
+#!/usr/bin/env python3
+"""Generate tests/golden/*.npz: oracle outputs on seeded synthetic inputs.
+
+The reference ships no golden vectors for this path and
+cannot be built here (no OpenCV), so these fixtures pin the ORACLE (the CPU
+restatement, "parity unpinned" vs the reference binary) on fixed inputs.
+Inputs are not stored: frames are regenerated from orbx/synth.py specs.
+They guard the oracle against regressions and give the GPU tests a second,
+fixed checker.  Re-run after an intentional oracle change:
+    python tools/gen_golden.py
+"""
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "orb-slam-system_amd"))
+
+from oracle import oracle as O  # noqa: E402
+from orbx import synth  # noqa: E402
+
+OUT = os.path.join(ROOT, "tests", "golden")
+
+EXTRACT = [
+    # name, w, h, nfeatures, nlevels, guard, kind, frame_idx
+    ("c1_640x480_rects", 640, 480, 1000, 8, "strict", "rects", 100),
+    ("c1_640x480_noise", 640, 480, 1000, 8, "strict", "noise", 101),
+    ("c2_640x480_single_level", 640, 480, 1000, 1, "strict", "rects", 102),
+    ("c5_1241x376_kitti", 1241, 376, 2000, 8, "strict", "rects", 103),
+    ("c3_1920x1080_empty_guard", 1920, 1080, 2000, 8, "empty", "rects", 104),
+]
+
+
+def main():
+    os.makedirs(OUT, exist_ok=True)
+    O.build()
+    for name, w, h, nf, L, guard, kind, idx in EXTRACT:
+        e = O.Extractor(nf, 1.2, L, 20, 7, cell_guard=guard)
+        k, d = e.extract(synth.frame(w, h, idx, kind))
+        np.savez_compressed(os.path.join(OUT, "extract_%s.npz" % name), keypoints=k.view(np.uint8),
+                            descriptors=d, spec=np.array([w, h, nf, L, 1 if guard == "empty" else 0,
+                                                          synth.KINDS[kind], idx], np.int64))
+        print(name, len(k))
+    # matcher: two consecutive frames, top-n single node, and a multi-node random case
+    rng = np.random.default_rng(2024)
+    n1, n2 = 700, 650
+    d1 = rng.integers(0, 256, (n1, 32), dtype=np.uint8)
+    flips = rng.integers(0, 256, (n2, 12))
+
+    src = None
+
+    def fv(assign, nodes):
+        feat, off = [], [0]
+        for j in range(len(nodes)):
+            feat += np.nonzero(assign == j)[0].tolist()
+            off.append(len(feat))
+        return nodes, np.array(off, np.uint32), np.array(feat, np.uint32)
+
+    nodes = np.sort(rng.choice(100, 9, replace=False)).astype(np.uint32)
+    as1 = rng.integers(0, 9, n1)
+    src = rng.integers(0, n1, n2)
+    d2 = d1[src].copy()
+    for i in range(n2):
+        for b in flips[i, :rng.integers(0, 12)]:
+            d2[i, b // 8] ^= np.uint8(1 << (b % 8))
+    as2 = np.where(rng.uniform(size=n2) < 0.85, as1[src], rng.integers(0, 9, n2))
+    nid1, off1, f1 = fv(as1, nodes)
+    nid2, off2, f2 = fv(as2, nodes)
+    a1 = rng.uniform(0, 360, n1).astype(np.float32)
+    a2 = rng.uniform(0, 360, n2).astype(np.float32)
+    v1 = (rng.uniform(size=n1) > 0.05).astype(np.uint8)
+    v2 = (rng.uniform(size=n2) > 0.05).astype(np.uint8)
+    kf1 = dict(desc=d1, angle=a1, valid=v1, node_id=nid1, off=off1, feat=f1)
+    kf2 = dict(desc=d2, angle=a2, valid=v2, node_id=nid2, off=off2, feat=f2)
+    res = {}
+    for ratio, ori in ((0.6, True), (0.75, True), (0.75, False)):
+        m, nm = O.search_by_bow(kf1, kf2, ratio, ori)
+        tag = "r%02d_o%d" % (int(ratio * 100), int(ori))
+        res["match_" + tag] = m
+        res["n_" + tag] = np.array([nm])
+    np.savez_compressed(os.path.join(OUT, "search_by_bow_multinode.npz"), d1=d1, d2=d2, a1=a1,
+                        a2=a2, v1=v1, v2=v2, nid1=nid1, off1=off1, f1=f1, nid2=nid2, off2=off2,
+                        f2=f2, **res)
+    print("search_by_bow", {k: int(v[0]) for k, v in res.items() if k.startswith("n_")})
+
+
+if __name__ == "__main__":
+    main()
