@@ -132,7 +132,7 @@ int orbx_plan_geometry(const orbx_plan* plan, orbx_geometry* g);
 /* d_frames: nframes images, frame i at d_frames + i*frame_stride, rows of
  * row_stride bytes (device memory).  Outputs (device memory):
  *   d_kps  [nframes][kcap], d_desc [nframes][kcap][32], d_counts [nframes].
- * Asynchronous on `stream` (a hipStream_t; NULL = the plan's own stream).
+ * Asynchronous on `stream` (a hipStream_t; NULL = the default stream).
  * Device-side failures (quadtree stuck) are latched; read them with
  * orbx_plan_check(). */
 int orbx_plan_extract(orbx_plan* plan, const uint8_t* d_frames, int nframes, size_t frame_stride,

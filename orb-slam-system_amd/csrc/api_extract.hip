@@ -250,7 +250,7 @@ extern "C" int orbx_plan_extract(orbx_plan* p, const uint8_t* frames, int nframe
   const Plan& P = p->P;
   if (rstride < (size_t)P.W || fstride < rstride * (size_t)P.H) return ORBX_ERR_ARG;
   ORBX_TRY(hipSetDevice(p->device));
-  hipStream_t s = stream ? (hipStream_t)stream : p->stream;
+  hipStream_t s = (hipStream_t)stream; /* NULL = the default stream */
   const int L = P.params.nlevels, n = nframes;
   // K1 pyramid
   p->timer.begin(ORBX_STAGE_RESIZE, s);
@@ -302,7 +302,7 @@ extern "C" int orbx_plan_extract(orbx_plan* p, const uint8_t* frames, int nframe
 extern "C" int orbx_plan_check(orbx_plan* p, void* stream) {
   if (!p) return ORBX_ERR_ARG;
   ORBX_TRY(hipSetDevice(p->device));
-  hipStream_t s = stream ? (hipStream_t)stream : p->stream;
+  hipStream_t s = (hipStream_t)stream; /* NULL = the default stream */
   ORBX_TRY(hipStreamSynchronize(s));
   int err = 0;
   ORBX_TRY(hipMemcpy(&err, p->d_err, sizeof(int), hipMemcpyDeviceToHost));
