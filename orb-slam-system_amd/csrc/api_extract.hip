@@ -5,6 +5,7 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <algorithm>
 #include <mutex>
 #include <vector>
 
@@ -16,14 +17,14 @@ namespace orbx {
 __global__ void k_resize(const uint8_t*, size_t, size_t, uint8_t*, size_t, const LevelInfo*, int,
                          const int32_t*, const int32_t*, const int16_t*, const int32_t*,
                          const int16_t*);
-__global__ void k_fast_cells(const uint8_t*, size_t, size_t, const uint8_t*, size_t,
-                             const LevelInfo*, const CellInfo*, uint32_t*, size_t, uint32_t*, int,
-                             int, int);
+__global__ void k_fast_strips(const uint8_t*, size_t, size_t, const uint8_t*, size_t,
+                              const LevelInfo*, const CellInfo*, const StripInfo*, uint32_t*,
+                              size_t, uint32_t*, int, int, int, int, int, int, int);
 __global__ void k_quadtree(const LevelInfo*, const CellInfo*, const uint32_t*, size_t,
                            const uint32_t*, int, uint32_t*, int32_t*, size_t, uint32_t*, size_t,
                            int*, int, int, int, int*);
-__global__ void k_blur(const uint8_t*, size_t, size_t, const uint8_t*, size_t, uint8_t*, size_t,
-                       const LevelInfo*, int);
+__global__ void k_blur_tiles(const uint8_t*, size_t, size_t, const uint8_t*, size_t, uint8_t*,
+                             size_t, const LevelInfo*, int);
 __global__ void k_orient_brief(const uint8_t*, size_t, size_t, const uint8_t*, size_t,
                                const uint8_t*, size_t, const LevelInfo*, int, const uint32_t*,
                                size_t, const int*, const int16_t*, int, orbx_keypoint*, uint8_t*,
@@ -120,6 +121,9 @@ struct orbx_plan {
   hipStream_t stream = nullptr;
   LevelInfo* d_lv = nullptr;
   CellInfo* d_cells = nullptr;
+  StripInfo* d_strips = nullptr;
+  int fs_tpitch = 0, fs_tmaxh = 0, fs_qcap = 0, fs_mcells = 0;
+  size_t fs_lds = 0;
   int32_t *d_xofs = nullptr, *d_xofs1 = nullptr, *d_yofs = nullptr;
   int16_t *d_alpha = nullptr, *d_beta = nullptr, *d_disk = nullptr;
   int ndisk = 0;
@@ -137,7 +141,7 @@ static size_t round_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 static void plan_free(orbx_plan* p) {
   if (!p) return;
   hipSetDevice(p->device);
-  void* bufs[] = {p->d_lv, p->d_cells, p->d_xofs, p->d_xofs1, p->d_yofs, p->d_alpha, p->d_beta,
+  void* bufs[] = {p->d_lv, p->d_cells, p->d_strips, p->d_xofs, p->d_xofs1, p->d_yofs, p->d_alpha, p->d_beta,
                   p->d_disk, p->d_pyr, p->d_blur, p->d_slots, p->d_ccount, p->d_qkeys, p->d_qout,
                   p->d_qnode, p->d_lcount, p->d_err};
   for (void* b : bufs)
@@ -187,7 +191,22 @@ extern "C" int orbx_plan_create(const orbx_params* prm, int width, int height, i
     for (int u = -um; u <= um; ++u) { disk.push_back((int16_t)u); disk.push_back((int16_t)v); }
   }
   p->ndisk = (int)disk.size() / 2;
-  if (upload(&p->d_lv, P.levels) || upload(&p->d_cells, P.cells) || upload(&p->d_xofs, P.xofs) ||
+  // FAST strip LDS: tile + strength map + candidate queue + row masks + counts
+  {
+    int qmax = 1;
+    for (const StripInfo& st : P.strips) qmax = std::max(qmax, (st.w - 6) * (st.h - 6));
+    p->fs_tpitch = (3 + P.strip_max_w + 8 + 3) & ~3;
+    p->fs_tmaxh = std::max(P.strip_max_h, 7);
+    p->fs_qcap = qmax;
+    p->fs_mcells = std::max(P.strip_max_cells, 1);
+    p->fs_lds = 2 * (size_t)p->fs_tpitch * p->fs_tmaxh + 2 * (size_t)p->fs_qcap + 8 +
+                8 * (size_t)p->fs_mcells * (p->fs_tmaxh - 6) + 4 * (size_t)p->fs_mcells + 16;
+    if (p->fs_lds > 150 * 1024) { plan_free(p); return ORBX_ERR_UNSUPPORTED; }
+    if (hipFuncSetAttribute((const void*)k_fast_strips, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)p->fs_lds) != hipSuccess) { plan_free(p); return ORBX_ERR_HIP; }
+  }
+  if (upload(&p->d_lv, P.levels) || upload(&p->d_cells, P.cells) || upload(&p->d_strips, P.strips) ||
+      upload(&p->d_xofs, P.xofs) ||
       upload(&p->d_xofs1, P.xofs1) || upload(&p->d_yofs, P.yofs) || upload(&p->d_alpha, P.alpha) ||
       upload(&p->d_beta, P.beta) || upload(&p->d_disk, disk)) {
     plan_free(p);
@@ -257,7 +276,7 @@ extern "C" int orbx_plan_extract(orbx_plan* p, const uint8_t* frames, int nframe
   for (int l = 1; l < L; ++l) {
     const LevelInfo& lv = P.levels[l];
     if (lv.unique != l) continue;
-    dim3 grid((lv.w + 255) / 256, (lv.h + 3) / 4, n), block(64, 4);
+    dim3 grid((lv.w + 127) / 128, (lv.h + 15) / 16, n), block(256);
     hipLaunchKernelGGL(k_resize, grid, block, 0, s, frames, fstride, rstride, p->d_pyr,
                        p->pyr_stride, p->d_lv, l, p->d_xofs, p->d_xofs1, p->d_alpha, p->d_yofs,
                        p->d_beta);
@@ -265,10 +284,11 @@ extern "C" int orbx_plan_extract(orbx_plan* p, const uint8_t* frames, int nframe
   p->timer.end(ORBX_STAGE_RESIZE, s);
   // K2 FAST cells
   p->timer.begin(ORBX_STAGE_FAST, s);
-  if (P.ncells > 0) {
-    hipLaunchKernelGGL(k_fast_cells, dim3(P.ncells, n), dim3(256), 0, s, frames, fstride, rstride,
-                       p->d_pyr, p->pyr_stride, p->d_lv, p->d_cells, p->d_slots, p->slot_stride,
-                       p->d_ccount, P.ncells, P.ini_th, P.min_th);
+  if (!P.strips.empty()) {
+    hipLaunchKernelGGL(k_fast_strips, dim3((unsigned)P.strips.size(), n), dim3(256), p->fs_lds, s,
+                       frames, fstride, rstride, p->d_pyr, p->pyr_stride, p->d_lv, p->d_cells,
+                       p->d_strips, p->d_slots, p->slot_stride, p->d_ccount, P.ncells, P.ini_th,
+                       P.min_th, p->fs_tpitch, p->fs_tmaxh, p->fs_qcap, p->fs_mcells);
   }
   p->timer.end(ORBX_STAGE_FAST, s);
   // K3 DistributeOctTree
@@ -280,13 +300,9 @@ extern "C" int orbx_plan_extract(orbx_plan* p, const uint8_t* frames, int nframe
   p->timer.end(ORBX_STAGE_QUADTREE, s);
   // K5 blur of every unique level
   p->timer.begin(ORBX_STAGE_BLUR, s);
-  for (int l = 0; l < L; ++l) {
-    const LevelInfo& lv = P.levels[l];
-    if (lv.unique != l) continue;
-    dim3 grid((lv.w + 63) / 64, (lv.h + 15) / 16, n);
-    hipLaunchKernelGGL(k_blur, grid, dim3(256), 0, s, frames, fstride, rstride, p->d_pyr,
-                       p->pyr_stride, p->d_blur, p->blur_stride, p->d_lv, l);
-  }
+  if (P.blur_tiles > 0)
+    hipLaunchKernelGGL(k_blur_tiles, dim3(P.blur_tiles, n), dim3(256), 0, s, frames, fstride,
+                       rstride, p->d_pyr, p->pyr_stride, p->d_blur, p->blur_stride, p->d_lv, L);
   p->timer.end(ORBX_STAGE_BLUR, s);
   // K4+K6+K7 orientation, descriptors, assembly
   p->timer.begin(ORBX_STAGE_BRIEF, s);

@@ -11,11 +11,14 @@
 #include "match_internal.h"
 
 namespace orbx {
-__global__ void k_match_candidates(const MProblem*, const MNodePair*, int, int, uint32_t*, int4*,
+__global__ void k_match_candidates(const MProblem*, const MNodePair*, int, int, uint2*, int4*,
                                    int2*);
-__global__ void k_match_resolve(const MProblem*, const MNodePair*, int, int, const uint32_t*,
+template <int NJ>
+__global__ void k_match_cand_lds(const MProblem*, const MNodePair*, uint2*, int4*, int2*);
+__global__ void k_match_resolve(const MProblem*, const MNodePair*, int, int, const uint2*,
                                 const int4*, int2*);
-__global__ void k_match_finalize(const MProblem*, const int4*, const int2*, int*, const int*);
+__global__ void k_match_finalize(const MProblem*, const MNodePair*, const int4*, const int2*, int*,
+                                 const int*);
 __global__ void k_match_select(MProblem*, MNodePair*, const orbx_keypoint*, const int*,
                                const orbx_keypoint*, const int*, int, int, uint32_t*);
 __global__ void k_hamming_pairs(const uint8_t*, const uint8_t*, const int32_t*, const int32_t*,
@@ -64,18 +67,29 @@ int check_frame(const orbx_bow_frame* k) {
 }
 
 void launch_match(const MProblem* d_probs, int nprob, const MNodePair* d_nps, int nnp, int nrows,
-                  int sequential, int max_n2, uint32_t* d_cand, int4* d_rowinfo, int2* d_ev,
-                  int* d_last, const int* d_last_off, hipStream_t s, StageTimer* timer) {
+                  int sequential, int max_n1, int max_n2, int max_bitmap_n2, uint2* d_cand,
+                  int4* d_rowinfo, int2* d_ev, int* d_last, const int* d_last_off, hipStream_t s,
+                  StageTimer* timer) {
   if (timer) timer->begin(ORBX_STAGE_MCAND, s);
-  if (nrows > 0)
-    hipLaunchKernelGGL(k_match_candidates, dim3((nrows + 3) / 4), dim3(256), 0, s, d_probs, d_nps,
-                       nnp, nrows, d_cand, d_rowinfo, d_ev);
+  if (nrows > 0 && nnp > 0) {
+    if (max_n2 <= 64 * 32 && nnp <= 65535) {
+      // list2 staged in LDS, distances in registers (32 per lane)
+      const size_t lds = (size_t)std::max(max_n2, 1) * 32;
+      hipFuncSetAttribute((const void*)k_match_cand_lds<32>,
+                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      hipLaunchKernelGGL(k_match_cand_lds<32>, dim3((max_n1 + 63) / 64, nnp), dim3(256), lds, s,
+                         d_probs, d_nps, d_cand, d_rowinfo, d_ev);
+    } else {
+      hipLaunchKernelGGL(k_match_candidates, dim3((nrows + 3) / 4), dim3(256), 0, s, d_probs,
+                         d_nps, nnp, nrows, d_cand, d_rowinfo, d_ev);
+    }
+  }
   if (timer) timer->end(ORBX_STAGE_MCAND, s);
   if (timer) timer->begin(ORBX_STAGE_MRESOLVE, s);
   const int units = sequential ? nprob : nnp;
   if (nrows > 0 && units > 0) {
-    if (max_n2 > 16384) {
-      const size_t lds = (size_t)((max_n2 + 31) / 32) * 4;
+    if (max_bitmap_n2 > 16384) {
+      const size_t lds = (size_t)((max_bitmap_n2 + 31) / 32) * 4;
       hipFuncSetAttribute((const void*)k_match_resolve, hipFuncAttributeMaxDynamicSharedMemorySize,
                           (int)lds);
       hipLaunchKernelGGL(k_match_resolve, dim3(units), dim3(64), lds, s, d_probs, d_nps, units,
@@ -87,8 +101,8 @@ void launch_match(const MProblem* d_probs, int nprob, const MNodePair* d_nps, in
   }
   if (timer) timer->end(ORBX_STAGE_MRESOLVE, s);
   if (timer) timer->begin(ORBX_STAGE_MFINAL, s);
-  hipLaunchKernelGGL(k_match_finalize, dim3(nprob), dim3(256), 0, s, d_probs, d_rowinfo, d_ev,
-                     d_last, d_last_off);
+  hipLaunchKernelGGL(k_match_finalize, dim3(nprob), dim3(256), 0, s, d_probs, d_nps, d_rowinfo,
+                     d_ev, d_last, d_last_off);
   if (timer) timer->end(ORBX_STAGE_MFINAL, s);
 }
 
@@ -109,7 +123,7 @@ extern "C" int orbm_search_by_bow(const orbx_bow_frame* kf1, const orbx_bow_fram
   // merge-join of the two FeatureVectors (ORBmatcher.cc:305-350): common
   // NodeIds in ascending order
   std::vector<MNodePair> nps;
-  int rows = 0;
+  int rows = 0, max_n1 = 0, max_n2 = 0;
   {
     int f1 = 0, f2 = 0;
     while (f1 < kf1->nnodes && f2 < kf2->nnodes) {
@@ -125,6 +139,8 @@ extern "C" int orbm_search_by_bow(const orbx_bow_frame* kf1, const orbx_bow_fram
         np.row_base = rows;
         np.pad = 0;
         rows += np.n1;
+        max_n1 = std::max(max_n1, np.n1);
+        max_n2 = std::max(max_n2, np.n2);
         nps.push_back(np);
         ++f1;
         ++f2;
@@ -182,7 +198,7 @@ extern "C" int orbm_search_by_bow(const orbx_bow_frame* kf1, const orbx_bow_fram
     P.sequential = sequential;
     MProblem* d_prob = B.upload(&P, 1, s);
     MNodePair* d_nps = B.upload(nps.data(), nps.size(), s);
-    uint32_t* d_cand = B.alloc<uint32_t>((size_t)rows * ORBM_T);
+    uint2* d_cand = B.alloc<uint2>((size_t)rows * ORBM_T);
     int4* d_rowinfo = B.alloc<int4>(rows);
     int2* d_ev = B.alloc<int2>(rows);
     int* d_last = B.alloc<int>(kf1->n);
@@ -193,8 +209,8 @@ extern "C" int orbm_search_by_bow(const orbx_bow_frame* kf1, const orbx_bow_fram
         !d_last_off || (kf1->valid && !P.valid1) || (kf2->valid && !P.valid2)) {
       result = ORBX_ERR_HIP;
     } else {
-      launch_match(d_prob, 1, d_nps, (int)nps.size(), rows, sequential, kf2->n, d_cand,
-                   d_rowinfo, d_ev, d_last, d_last_off, s, nullptr);
+      launch_match(d_prob, 1, d_nps, (int)nps.size(), rows, sequential, max_n1, max_n2, kf2->n,
+                   d_cand, d_rowinfo, d_ev, d_last, d_last_off, s, nullptr);
       if (hipGetLastError() != hipSuccess ||
           hipMemcpyAsync(match12, P.match12, sizeof(int32_t) * (size_t)kf1->n,
                          hipMemcpyDeviceToHost, s) != hipSuccess ||
@@ -296,7 +312,8 @@ struct orbm_plan {
   int device = 0, max_pairs = 0, kcap = 0, topn = 0;
   MProblem* d_probs = nullptr;
   MNodePair* d_nps = nullptr;
-  uint32_t *d_sel = nullptr, *d_cand = nullptr;
+  uint32_t* d_sel = nullptr;
+  uint2* d_cand = nullptr;
   int4* d_rowinfo = nullptr;
   int2* d_ev = nullptr;
   int *d_last = nullptr, *d_last_off = nullptr;
@@ -331,7 +348,7 @@ extern "C" int orbm_plan_create(int max_pairs, int kcap, int topn, int device, o
   if (hipMalloc((void**)&m->d_probs, P * sizeof(MProblem)) != hipSuccess ||
       hipMalloc((void**)&m->d_nps, P * sizeof(MNodePair)) != hipSuccess ||
       hipMalloc((void**)&m->d_sel, P * 2 * topn * sizeof(uint32_t)) != hipSuccess ||
-      hipMalloc((void**)&m->d_cand, rows * ORBM_T * sizeof(uint32_t)) != hipSuccess ||
+      hipMalloc((void**)&m->d_cand, rows * ORBM_T * sizeof(uint2)) != hipSuccess ||
       hipMalloc((void**)&m->d_rowinfo, rows * sizeof(int4)) != hipSuccess ||
       hipMalloc((void**)&m->d_ev, rows * sizeof(int2)) != hipSuccess ||
       hipMalloc((void**)&m->d_last, P * kcap * sizeof(int)) != hipSuccess ||
@@ -378,7 +395,7 @@ extern "C" int orbm_plan_match_frames(orbm_plan* m, int npairs, const orbx_keypo
   hipLaunchKernelGGL(k_match_select, dim3(npairs, 2), dim3(256), 0, s, m->d_probs, m->d_nps,
                      kps_a, count_a, kps_b, count_b, m->kcap, m->topn, m->d_sel);
   m->timer.end(ORBX_STAGE_MSELECT, s);
-  launch_match(m->d_probs, npairs, m->d_nps, npairs, npairs * m->topn, 0, m->kcap, m->d_cand,
-               m->d_rowinfo, m->d_ev, m->d_last, m->d_last_off, s, &m->timer);
+  launch_match(m->d_probs, npairs, m->d_nps, npairs, npairs * m->topn, 0, m->topn, m->topn,
+               m->kcap, m->d_cand, m->d_rowinfo, m->d_ev, m->d_last, m->d_last_off, s, &m->timer);
   return hipGetLastError() == hipSuccess ? ORBX_OK : ORBX_ERR_HIP;
 }

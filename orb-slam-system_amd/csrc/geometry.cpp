@@ -129,6 +129,8 @@ int plan_geometry(const orbx_params& p, int width, int height, Plan& P) {
   const int L = p.nlevels;
   P.levels.assign(L, LevelInfo());
   P.cells.clear();
+  P.strips.clear();
+  P.strip_max_w = P.strip_max_h = P.strip_max_cells = 0;
   P.xofs.clear(); P.xofs1.clear(); P.alpha.clear(); P.yofs.clear(); P.beta.clear();
   memset(&P.geo, 0, sizeof(P.geo));
   P.geo.nlevels = L;
@@ -209,8 +211,10 @@ int plan_geometry(const orbx_params& p, int width, int height, Plan& P) {
     }
     lv.cell_begin = (int)P.cells.size();
     lv.slot_begin = slots;
+    lv.wcell = wCell;
     int bad = 0;
     for (int i = 0; i < nRows; ++i) {
+      const int row_first = (int)P.cells.size();
       const float iniY = (float)(minB + i * hCell);
       const float maxY = std::min(iniY + hCell + 6, (float)maxBY);
       for (int j = 0; j < nCols; ++j) {
@@ -229,6 +233,22 @@ int plan_geometry(const orbx_params& p, int width, int height, Plan& P) {
         slots += c.slot_cap;
         P.cells.push_back(c);
       }
+      /* valid cells of a row are a prefix (only the last columns can be
+       * negative / narrower than 7); group them into strips */
+      const int nvalid = (int)P.cells.size() - row_first;
+      const int per = std::max(1, ORBX_STRIP_MAXW / std::max(wCell, 1));
+      for (int j0 = 0; j0 < nvalid; j0 += per) {
+        const int j1 = std::min(nvalid, j0 + per);
+        const CellInfo& a = P.cells[row_first + j0];
+        const CellInfo& b = P.cells[row_first + j1 - 1];
+        StripInfo st;
+        st.level = l; st.x = a.x; st.y = a.y; st.w = b.x + b.w - a.x; st.h = a.h;
+        st.cell_begin = row_first + j0; st.ncells = j1 - j0; st.wcell = wCell;
+        P.strips.push_back(st);
+        P.strip_max_w = std::max(P.strip_max_w, st.w);
+        P.strip_max_h = std::max(P.strip_max_h, st.h);
+        P.strip_max_cells = std::max(P.strip_max_cells, st.ncells);
+      }
     }
     lv.ncells = (int)P.cells.size() - lv.cell_begin;
     lv.nslots = slots - lv.slot_begin;
@@ -237,6 +257,15 @@ int plan_geometry(const orbx_params& p, int width, int height, Plan& P) {
   }
   P.nslots = slots;
   P.ncells = (int)P.cells.size();
+  int bt = 0;
+  for (int l = 0; l < L; ++l) {
+    LevelInfo& lv = P.levels[l];
+    if (lv.unique != l) { lv.blur_tile_begin = -1; lv.blur_tiles_x = 0; continue; }
+    lv.blur_tile_begin = bt;
+    lv.blur_tiles_x = (lv.w + ORBX_BLUR_TW - 1) / ORBX_BLUR_TW;
+    bt += lv.blur_tiles_x * ((lv.h + ORBX_BLUR_TH - 1) / ORBX_BLUR_TH);
+  }
+  P.blur_tiles = bt;
 
   /* quadtree capacities */
   int kout = 0, smax = 1, maxc = 1;

@@ -31,6 +31,9 @@ struct Plan {
   int ini_th = 0, min_th = 0; /* clamped to [0,255] as cv::FAST does */
   std::vector<LevelInfo> levels;
   std::vector<CellInfo> cells;
+  std::vector<StripInfo> strips;
+  int strip_max_w = 0, strip_max_h = 0, strip_max_cells = 0;
+  int blur_tiles = 0;
   std::vector<int32_t> xofs;   /* concatenated per unique level >= 1 */
   std::vector<int16_t> alpha;  /* 2 per x */
   std::vector<int32_t> xofs1;  /* second tap column (clamped) */

@@ -41,8 +41,14 @@ __device__ __forceinline__ const uint8_t* level_base(const uint8_t* frames, size
 // k_resize: level l (unique, >= 1) from level l-1 with OpenCV's INTER_LINEAR
 // fixed-point arithmetic: D = S[sx]*a0 + S[sx1]*a1 (int32),
 // dst = (((b0*(D0>>4))>>16) + ((b1*(D1>>4))>>16) + 2) >> 2.
-// Block 64x4 threads, 4 output pixels per thread (one 32-bit store).
+// Workgroup = 128x16 output tile; the source footprint is staged in LDS
+// with dword loads; each thread makes 4 columns x 2 rows (two dword stores).
 // ---------------------------------------------------------------------------
+#define RS_TW 128
+#define RS_TH 16
+#define RS_SR 40   /* staged source rows  (level ratio <= ~2.2) */
+#define RS_SC 320  /* staged source bytes per row */
+
 __global__ __launch_bounds__(256) void k_resize(const uint8_t* __restrict__ frames, size_t fstride,
                                                 size_t rstride, uint8_t* __restrict__ pyr,
                                                 size_t pstride, const LevelInfo* __restrict__ lv,
@@ -51,40 +57,87 @@ __global__ __launch_bounds__(256) void k_resize(const uint8_t* __restrict__ fram
                                                 const int16_t* __restrict__ alpha,
                                                 const int32_t* __restrict__ yofs,
                                                 const int16_t* __restrict__ beta) {
+  __shared__ uint32_t ssrc[RS_SR][RS_SC / 4];
   const LevelInfo D = lv[l];
   const int u = D.src_level;
   const LevelInfo S = lv[u];
-  const int f = blockIdx.z;
+  const int f = blockIdx.z, tid = threadIdx.x;
   int spitch;
   const uint8_t* src = level_base(frames, fstride, rstride, pyr, pstride, S, u, f, &spitch);
   uint8_t* dst = pyr + (size_t)f * pstride + D.pyr_off;
-  const int y = blockIdx.y * 4 + threadIdx.y;
-  const int x0 = (blockIdx.x * 64 + threadIdx.x) * 4;
-  if (y >= D.h || x0 >= D.w) return;
-  const int sy = yofs[D.lut_y + y];
-  const int r0 = min(max(sy, 0), S.h - 1), r1 = min(max(sy + 1, 0), S.h - 1);
-  const int b0 = beta[2 * (D.lut_y + y)], b1 = beta[2 * (D.lut_y + y) + 1];
-  const uint8_t* S0 = src + (size_t)r0 * spitch;
-  const uint8_t* S1 = src + (size_t)r1 * spitch;
-  uint32_t packed = 0;
+  const int x0 = blockIdx.x * RS_TW, y0 = blockIdx.y * RS_TH;
+  const int xl = min(x0 + RS_TW, D.w) - 1, yl = min(y0 + RS_TH, D.h) - 1;
+  const int r_lo = min(max(yofs[D.lut_y + y0], 0), S.h - 1);
+  const int r_hi = min(max(yofs[D.lut_y + yl] + 1, 0), S.h - 1);
+  const bool aligned = ((reinterpret_cast<uintptr_t>(src) | (uintptr_t)spitch) & 3) == 0;
+  const int c_lo = aligned ? (xofs[D.lut_x + x0] & ~3) : xofs[D.lut_x + x0];
+  const int c_hi = xofs1[D.lut_x + xl];
+  const int nr = r_hi - r_lo + 1, nc = c_hi - c_lo + 1;
+  const bool staged = nr <= RS_SR && nc <= RS_SC;
+  if (staged) {
+    uint8_t* s8 = reinterpret_cast<uint8_t*>(ssrc);
+    if (aligned) {
+      const int nd = (nc + 3) >> 2;
+      for (int i = tid; i < nr * nd; i += 256) {
+        const int r = i / nd, c = i - r * nd;
+        const int gc = c_lo + 4 * c;
+        const uint8_t* p = src + (size_t)(r_lo + r) * spitch + gc;
+        ssrc[r][c] = (gc + 3 < S.w) ? *reinterpret_cast<const uint32_t*>(p)
+                                    : (uint32_t)p[0] | ((gc + 1 < S.w ? (uint32_t)p[1] : 0u) << 8) |
+                                          ((gc + 2 < S.w ? (uint32_t)p[2] : 0u) << 16);
+      }
+    } else {
+      for (int i = tid; i < nr * nc; i += 256) {
+        const int r = i / nc, c = i - r * nc;
+        s8[r * RS_SC + c] = src[(size_t)(r_lo + r) * spitch + c_lo + c];
+      }
+    }
+  }
+  __syncthreads();
+  const int tx = tid & 31, ty = tid >> 5;
+  const int xb = x0 + 4 * tx;
+  if (xb >= D.w) return;
+  int sx[4], sx1[4], a0[4], a1[4];
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
-    const int x = x0 + k;
-    if (x < D.w) {
-      const int j = D.lut_x + x;
-      const int sx = xofs[j], sx1 = xofs1[j];
-      const int a0 = alpha[2 * j], a1 = alpha[2 * j + 1];
-      const int d0 = S0[sx] * a0 + S0[sx1] * a1;
-      const int d1 = S1[sx] * a0 + S1[sx1] * a1;
+    const int j = D.lut_x + min(xb + k, D.w - 1);
+    sx[k] = xofs[j];
+    sx1[k] = xofs1[j];
+    a0[k] = alpha[2 * j];
+    a1[k] = alpha[2 * j + 1];
+  }
+  const uint8_t* s8 = reinterpret_cast<const uint8_t*>(ssrc);
+#pragma unroll
+  for (int rr = 0; rr < 2; ++rr) {
+    const int y = y0 + 2 * ty + rr;
+    if (y >= D.h) break;
+    const int sy = yofs[D.lut_y + y];
+    const int r0 = min(max(sy, 0), S.h - 1), r1 = min(max(sy + 1, 0), S.h - 1);
+    const int b0 = beta[2 * (D.lut_y + y)], b1 = beta[2 * (D.lut_y + y) + 1];
+    uint32_t packed = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      int p00, p01, p10, p11;
+      if (staged) {
+        const uint8_t* R0 = s8 + (r0 - r_lo) * RS_SC - c_lo;
+        const uint8_t* R1 = s8 + (r1 - r_lo) * RS_SC - c_lo;
+        p00 = R0[sx[k]]; p01 = R0[sx1[k]]; p10 = R1[sx[k]]; p11 = R1[sx1[k]];
+      } else {
+        const uint8_t* R0 = src + (size_t)r0 * spitch;
+        const uint8_t* R1 = src + (size_t)r1 * spitch;
+        p00 = R0[sx[k]]; p01 = R0[sx1[k]]; p10 = R1[sx[k]]; p11 = R1[sx1[k]];
+      }
+      const int d0 = p00 * a0[k] + p01 * a1[k];
+      const int d1 = p10 * a0[k] + p11 * a1[k];
       const int v = (((b0 * (d0 >> 4)) >> 16) + ((b1 * (d1 >> 4)) >> 16) + 2) >> 2;
       packed |= (uint32_t)(v & 0xFF) << (8 * k);
     }
-  }
-  uint8_t* out = dst + (size_t)y * D.pitch + x0;
-  if (x0 + 3 < D.w) {
-    *reinterpret_cast<uint32_t*>(out) = packed;  // pitch is a multiple of 16
-  } else {
-    for (int k = 0; x0 + k < D.w; ++k) out[k] = (uint8_t)(packed >> (8 * k));
+    uint8_t* out = dst + (size_t)y * D.pitch + xb;
+    if (xb + 3 < D.w) {
+      *reinterpret_cast<uint32_t*>(out) = packed;  // pitch and offsets are 16-B multiples
+    } else {
+      for (int k = 0; xb + k < D.w; ++k) out[k] = (uint8_t)(packed >> (8 * k));
+    }
   }
 }
 
@@ -146,79 +199,201 @@ __device__ __forceinline__ int nms_keep(const uint8_t* amap, int bw, int bh, int
   return 1;
 }
 
-__global__ __launch_bounds__(256) void k_fast_cells(
+// ---------------------------------------------------------------------------
+// k_fast_strips: one workgroup per (strip of cells, frame).
+//  1. the strip tile (cells + 3-px rings) is staged in LDS with dword loads;
+//  2. every thread tests 4 adjacent band pixels with the 4 cardinal circle
+//     points (necessary for a 9-arc at t_lo = min(ini, min) thresholds) and
+//     pushes survivors into an LDS queue;
+//  3. the full FAST strength A is computed only for queued pixels;
+//  4. cv::FAST's NMS per cell at iniThFAST, then minThFAST for cells left
+//     empty, into one 64-bit mask per (cell, band row);
+//  5. each (cell, row) writes its kept pixels at the cell's raster offset.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ int tbyte(const uint32_t* dw, int i) { return (dw[i >> 2] >> ((i & 3) * 8)) & 0xFF; }
+
+__global__ __launch_bounds__(256) void k_fast_strips(
     const uint8_t* __restrict__ frames, size_t fstride, size_t rstride,
     const uint8_t* __restrict__ pyr, size_t pstride, const LevelInfo* __restrict__ lv,
-    const CellInfo* __restrict__ cells, uint32_t* __restrict__ slots, size_t slot_stride,
-    uint32_t* __restrict__ ccount, int ncells, int ini_th, int min_th) {
-  __shared__ uint8_t tile[ORBX_CELL_MAX * ORBX_CELL_MAX];
-  __shared__ uint8_t amap[(ORBX_CELL_MAX - 6) * (ORBX_CELL_MAX - 6)];
-  __shared__ uint8_t keep[(ORBX_CELL_MAX - 6) * (ORBX_CELL_MAX - 6)];
-  __shared__ int s_wtot[4];
-  const int c = blockIdx.x, f = blockIdx.y, tid = threadIdx.x;
-  const CellInfo ci = cells[c];
+    const CellInfo* __restrict__ cells, const StripInfo* __restrict__ strips,
+    uint32_t* __restrict__ slots, size_t slot_stride, uint32_t* __restrict__ ccount, int ncells,
+    int ini_th, int min_th, int tpitch, int tmax_h, int qcap, int mcells) {
+  extern __shared__ __align__(16) uint32_t sm[];
+  uint8_t* tile = reinterpret_cast<uint8_t*>(sm);                    // tpitch * tmax_h
+  uint8_t* amap = tile + tpitch * tmax_h;                             // tpitch * tmax_h
+  uint16_t* queue = reinterpret_cast<uint16_t*>(amap + tpitch * tmax_h);  // qcap
+  unsigned long long* mask = reinterpret_cast<unsigned long long*>(
+      (reinterpret_cast<uintptr_t>(queue + qcap) + 7) & ~(uintptr_t)7);  // mcells * (tmax_h-6)
+  int* cnt = reinterpret_cast<int*>(mask + mcells * (tmax_h - 6));      // mcells
+  __shared__ int s_q;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const StripInfo st = strips[blockIdx.x];
+  const int f = blockIdx.y;
   int pitch;
-  const uint8_t* base =
-      level_base(frames, fstride, rstride, pyr, pstride, lv[ci.level], ci.level, f, &pitch);
-  const int tw = ci.w, th = ci.h, bw = tw - 6, bh = th - 6, nb = bw * bh;
-  for (int i = tid; i < tw * th; i += 256) {
-    const int ty = i / tw, tx = i - ty * tw;
-    tile[i] = base[(size_t)(ci.y + ty) * pitch + ci.x + tx];
+  const uint8_t* base = level_base(frames, fstride, rstride, pyr, pstride, lv[st.level], st.level, f, &pitch);
+  const int bh = st.h - 6;
+  // LDS tile column 0 = global column xal (dword aligned when the rows are)
+  const uintptr_t rowaddr = reinterpret_cast<uintptr_t>(base) + (size_t)st.y * pitch + st.x;
+  const bool aligned = ((reinterpret_cast<uintptr_t>(base) | (uintptr_t)pitch) & 3) == 0;
+  const int xal = aligned ? (st.x & ~3) : st.x;
+  const int lead = st.x - xal;          // tile col of global st.x
+  const int tw = lead + st.w;           // columns in use
+  const int nd = (tw + 3) >> 2;         // dwords per tile row
+  if (aligned) {
+    for (int i = tid; i < nd * st.h; i += 256) {
+      const int r = i / nd, c = i - r * nd;
+      const uint32_t* src = reinterpret_cast<const uint32_t*>(base + (size_t)(st.y + r) * pitch + xal);
+      reinterpret_cast<uint32_t*>(tile + r * tpitch)[c] = src[c];
+    }
+  } else {
+    for (int i = tid; i < tw * st.h; i += 256) {
+      const int r = i / tw, c = i - r * tw;
+      tile[r * tpitch + c] = base[(size_t)(st.y + r) * pitch + xal + c];
+    }
+  }
+  (void)rowaddr;
+  for (int i = tid; i < (tpitch >> 2) * st.h; i += 256) reinterpret_cast<uint32_t*>(amap)[i] = 0u;
+  for (int i = tid; i < st.ncells * bh; i += 256) mask[i] = 0ull;
+  if (tid < st.ncells) cnt[tid] = 0;
+  if (tid == 0) s_q = 0;
+  __syncthreads();
+  // band columns [c0, c1) in tile coordinates, rows [3, 3+bh)
+  const CellInfo lastc = cells[st.cell_begin + st.ncells - 1];
+  const int c0 = lead + 3, c1 = lead + (lastc.x + lastc.w - st.x) - 3;
+  const int t_lo = min(ini_th, min_th);
+  // pass 1: cardinal-point pre-test on groups of 4 pixels (tile cols 4g..4g+3)
+  const int g0 = c0 >> 2, g1 = (c1 + 3) >> 2, ng = g1 - g0;
+  const int ntask = ng * bh;
+  for (int it0 = 0; it0 < ntask; it0 += 256) {  // wave-uniform trip count (shuffles below)
+    const int it = it0 + tid;
+    const int r = 3 + it / ng, g = g0 + it % ng;
+    int flags = 0;
+    if (it < ntask) {
+      const uint32_t* rowm = reinterpret_cast<const uint32_t*>(tile + (r - 3) * tpitch);
+      const uint32_t* row0 = reinterpret_cast<const uint32_t*>(tile + r * tpitch);
+      const uint32_t* rowp = reinterpret_cast<const uint32_t*>(tile + (r + 3) * tpitch);
+      uint32_t m0[3];
+      m0[0] = g > 0 ? row0[g - 1] : 0u;
+      m0[1] = row0[g];
+      m0[2] = row0[g + 1];
+      const uint32_t up = rowm[g], dn = rowp[g];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int c = 4 * g + j;
+        const int v = tbyte(m0, 4 + j);
+        const int I0 = (dn >> (8 * j)) & 0xFF, I8 = (up >> (8 * j)) & 0xFF;
+        const int I4 = tbyte(m0, 4 + j + 3), I12 = tbyte(m0, 4 + j - 3);
+        const int hi = v + t_lo, lo = v - t_lo;
+        const bool br = (I0 > hi || I8 > hi) && (I4 > hi || I12 > hi);
+        const bool dk = (I0 < lo || I8 < lo) && (I4 < lo || I12 < lo);
+        if ((br || dk) && c >= c0 && c < c1) flags |= 1 << j;
+      }
+    }
+    // wave-aggregated queue push
+    const int n = __popc(flags);
+    int incl = n;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const int t = __shfl_up(incl, d, 64);
+      if (lane >= d) incl += t;
+    }
+    const int tot = __shfl(incl, 63, 64);
+    int wbase = 0;
+    if (lane == 63 && tot > 0) wbase = atomicAdd(&s_q, tot);
+    wbase = __shfl(wbase, 63, 64);
+    int pos = wbase + incl - n;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (flags & (1 << j)) {
+        if (pos < qcap) queue[pos] = (uint16_t)((r << 9) | (4 * g + j));
+        ++pos;
+      }
   }
   __syncthreads();
-  for (int i = tid; i < nb; i += 256) {
-    const int by = i / bw, bx = i - by * bw;
-    amap[i] = (uint8_t)fast_strength(&tile[(by + 3) * tw + bx + 3], tw);
+  const int nq = min(s_q, qcap);
+  // pass 2: full strength for queued pixels
+  for (int q = tid; q < nq; q += 256) {
+    const int r = queue[q] >> 9, c = queue[q] & 511;
+    const int a = fast_strength(tile + r * tpitch + c, tpitch);
+    amap[r * tpitch + c] = (uint8_t)(a > t_lo ? a : 0);
   }
   __syncthreads();
-  int cnt = 0;
-  for (int i0 = 0; i0 < nb; i0 += 256) {
-    const int i = i0 + tid;
-    int k = 0;
-    if (i < nb) {
-      const int by = i / bw, bx = i - by * bw;
-      k = nms_keep(amap, bw, bh, bx, by, ini_th);
-      keep[i] = (uint8_t)k;
-    }
-    cnt += __syncthreads_count(k);
-  }
-  if (cnt == 0) {  // handleKeyPoints: FAST again at minThFAST when the cell is empty
-    for (int i0 = 0; i0 < nb; i0 += 256) {
-      const int i = i0 + tid;
-      int k = 0;
-      if (i < nb) {
-        const int by = i / bw, bx = i - by * bw;
-        k = nms_keep(amap, bw, bh, bx, by, min_th);
-        keep[i] = (uint8_t)k;
+  // pass 3: NMS at iniThFAST
+  const int wcell = st.wcell;
+  for (int q = tid; q < nq; q += 256) {
+    const int r = queue[q] >> 9, c = queue[q] & 511;
+    const int a = amap[r * tpitch + c];
+    if (a <= ini_th) continue;
+    const int k = min((c - c0) / wcell, st.ncells - 1);
+    const int cb0 = c0 + k * wcell, cb1 = (k == st.ncells - 1) ? c1 : cb0 + wcell;
+    bool keep = true;
+#pragma unroll
+    for (int dy = -1; dy <= 1; ++dy)
+#pragma unroll
+      for (int dx = -1; dx <= 1; ++dx) {
+        if (!dx && !dy) continue;
+        const int rr = r + dy, cc = c + dx;
+        int nb = 0;
+        if (rr >= 3 && rr < 3 + bh && cc >= cb0 && cc < cb1) {
+          const int aq = amap[rr * tpitch + cc];
+          nb = aq > ini_th ? aq - 1 : 0;
+        }
+        keep = keep && (a - 1 > nb);
       }
-      cnt += __syncthreads_count(k);
+    if (keep) {
+      atomicOr(&mask[k * bh + (r - 3)], 1ull << (c - cb0));
+      atomicAdd(&cnt[k], 1);
     }
   }
-  // raster-order compaction
-  const int wave = tid >> 6, lane = tid & 63;
-  uint32_t* out = slots + (size_t)f * slot_stride + ci.slot_off;
-  int basepos = 0;
-  if (cnt > 0) {
-    for (int i0 = 0; i0 < nb; i0 += 256) {
-      const int i = i0 + tid;
-      const int k = (i < nb) ? keep[i] : 0;
-      const uint64_t m = __ballot(k);
-      const int rank = __popcll(m & ((1ull << lane) - 1ull));
-      if (lane == 0) s_wtot[wave] = __popcll(m);
-      __syncthreads();
-      int off = basepos;
-      for (int w = 0; w < wave; ++w) off += s_wtot[w];
-      if (k) {
-        const int by = i / bw, bx = i - by * bw;
-        const int gx = ci.x + 3 + bx - ORBX_MINB, gy = ci.y + 3 + by - ORBX_MINB;
-        const uint32_t score = (uint32_t)amap[i] - 1u;
-        out[off + rank] = orbx_pack_key((uint32_t)gx, (uint32_t)gy, score);
+  __syncthreads();
+  // pass 4: cells without a corner at iniThFAST retry at minThFAST (:293-296)
+  for (int q = tid; q < nq; q += 256) {
+    const int r = queue[q] >> 9, c = queue[q] & 511;
+    const int k = min((c - c0) / wcell, st.ncells - 1);
+    if (cnt[k] != 0) continue;
+    const int a = amap[r * tpitch + c];
+    if (a <= min_th) continue;
+    const int cb0 = c0 + k * wcell, cb1 = (k == st.ncells - 1) ? c1 : cb0 + wcell;
+    bool keep = true;
+#pragma unroll
+    for (int dy = -1; dy <= 1; ++dy)
+#pragma unroll
+      for (int dx = -1; dx <= 1; ++dx) {
+        if (!dx && !dy) continue;
+        const int rr = r + dy, cc = c + dx;
+        int nb = 0;
+        if (rr >= 3 && rr < 3 + bh && cc >= cb0 && cc < cb1) {
+          const int aq = amap[rr * tpitch + cc];
+          nb = aq > min_th ? aq - 1 : 0;
+        }
+        keep = keep && (a - 1 > nb);
       }
-      basepos += s_wtot[0] + s_wtot[1] + s_wtot[2] + s_wtot[3];
-      __syncthreads();
+    if (keep) atomicOr(&mask[k * bh + (r - 3)], 1ull << (c - cb0));
+  }
+  __syncthreads();
+  // pass 5: raster-order output per cell
+  uint32_t* fslots = slots + (size_t)f * slot_stride;
+  for (int i = tid; i < st.ncells * bh; i += 256) {
+    const int k = i / bh, br = i - k * bh;
+    int off = 0;
+    for (int t = 0; t < br; ++t) off += __popcll(mask[k * bh + t]);
+    unsigned long long m = mask[i];
+    const CellInfo ci = cells[st.cell_begin + k];
+    const int cb0 = c0 + k * wcell;
+    const int gy = st.y + 3 + br - ORBX_MINB;
+    while (m) {
+      const int b = __ffsll(m) - 1;
+      m &= m - 1;
+      const int c = cb0 + b;
+      const int gx = xal + c - ORBX_MINB;
+      fslots[ci.slot_off + off++] =
+          orbx_pack_key((uint32_t)gx, (uint32_t)gy, (uint32_t)amap[(3 + br) * tpitch + c] - 1u);
+    }
+    if (br == bh - 1) {
+      int total = off;
+      ccount[(size_t)f * ncells + st.cell_begin + k] = (uint32_t)total;
     }
   }
-  if (tid == 0) ccount[(size_t)f * ncells + c] = (uint32_t)cnt;
 }
 
 // ---------------------------------------------------------------------------
@@ -441,10 +616,11 @@ __global__ __launch_bounds__(256) void k_quadtree(
 }
 
 // ---------------------------------------------------------------------------
-// k_blur: cv::GaussianBlur(7x7, sigma 2, BORDER_REFLECT_101) on 8U with the
-// bit-exact fixed-point kernel [18,34,48,56,48,34,18]/256:
+// k_blur_tiles: cv::GaussianBlur(7x7, sigma 2, BORDER_REFLECT_101) on 8U with
+// the bit-exact fixed-point kernel [18,34,48,56,48,34,18]/256:
 // H = sum k_i p (u16), out = (sum k_j H_j + 32768) >> 16.
-// Tile 64x16 outputs per workgroup.
+// One launch for every unique level: workgroup = one 128x32 output tile;
+// 4 outputs per thread per pass, dword LDS reads, dword global stores.
 // ---------------------------------------------------------------------------
 __constant__ int c_gk[7] = {18, 34, 48, 56, 48, 34, 18};
 
@@ -453,44 +629,79 @@ __device__ __forceinline__ int reflect101(int p, int len) {
   return p >= len ? 2 * len - 2 - p : p;
 }
 
-__global__ __launch_bounds__(256) void k_blur(const uint8_t* __restrict__ frames, size_t fstride,
-                                              size_t rstride, const uint8_t* __restrict__ pyr,
-                                              size_t pstride, uint8_t* __restrict__ blur,
-                                              size_t bstride, const LevelInfo* __restrict__ lv,
-                                              int u) {
-  __shared__ uint8_t in[22][72];
-  __shared__ uint16_t hs[22][64];
+__global__ __launch_bounds__(256) void k_blur_tiles(const uint8_t* __restrict__ frames,
+                                                    size_t fstride, size_t rstride,
+                                                    const uint8_t* __restrict__ pyr, size_t pstride,
+                                                    uint8_t* __restrict__ blur, size_t bstride,
+                                                    const LevelInfo* __restrict__ lv, int nlevels) {
+  constexpr int TW = ORBX_BLUR_TW, TH = ORBX_BLUR_TH, IW = TW + 8, IH = TH + 6;
+  __shared__ uint32_t in32[IH][IW / 4];      // input tile, col 0 = global x0-4
+  __shared__ uint32_t hs32[IH][TW / 2];      // horizontal pass, u16 pairs
+  const int tid = threadIdx.x, f = blockIdx.y;
+  int u = 0;
+  for (int l = 0; l < nlevels; ++l)
+    if (lv[l].unique == l && (int)blockIdx.x >= lv[l].blur_tile_begin) u = l;
   const LevelInfo U = lv[u];
-  const int f = blockIdx.z, tid = threadIdx.x;
+  const int t = blockIdx.x - U.blur_tile_begin;
+  const int x0 = (t % U.blur_tiles_x) * TW, y0 = (t / U.blur_tiles_x) * TH;
   int pitch;
   const uint8_t* src = level_base(frames, fstride, rstride, pyr, pstride, U, u, f, &pitch);
-  const int bx0 = blockIdx.x * 64, by0 = blockIdx.y * 16;
-  for (int i = tid; i < 22 * 70; i += 256) {
-    const int ty = i / 70, tx = i - ty * 70;
-    const int gx = reflect101(min(bx0 + tx - 3, U.w + 2), U.w);
-    const int gy = reflect101(min(by0 + ty - 3, U.h + 2), U.h);
-    in[ty][tx] = src[(size_t)gy * pitch + gx];
+  const bool interior = x0 >= 4 && x0 + TW + 4 <= U.w && y0 >= 3 && y0 + TH + 3 <= U.h &&
+                        ((reinterpret_cast<uintptr_t>(src) | (uintptr_t)pitch) & 3) == 0;
+  if (interior) {
+    for (int i = tid; i < IH * (IW / 4); i += 256) {
+      const int r = i / (IW / 4), c = i - r * (IW / 4);
+      in32[r][c] = reinterpret_cast<const uint32_t*>(src + (size_t)(y0 - 3 + r) * pitch + x0 - 4)[c];
+    }
+  } else {
+    uint8_t* in8 = reinterpret_cast<uint8_t*>(in32);
+    for (int i = tid; i < IH * IW; i += 256) {
+      const int r = i / IW, c = i - r * IW;
+      const int gx = reflect101(min(max(x0 - 4 + c, -3), U.w + 2), U.w);
+      const int gy = reflect101(min(max(y0 - 3 + r, -3), U.h + 2), U.h);
+      in8[r * IW + c] = src[(size_t)gy * pitch + gx];
+    }
   }
   __syncthreads();
-  for (int i = tid; i < 22 * 64; i += 256) {
-    const int ty = i >> 6, tx = i & 63;
-    int s = 0;
+  // horizontal: 4 outputs (cols 4q..4q+3) per task, need input cols 4q+1 .. 4q+10
+  for (int i = tid; i < IH * (TW / 4); i += 256) {
+    const int r = i / (TW / 4), q = i - r * (TW / 4);
+    uint32_t w3[3] = {in32[r][q], in32[r][q + 1], in32[r][q + 2]};
+    int o[4];
 #pragma unroll
-    for (int k = 0; k < 7; ++k) s += c_gk[k] * in[ty][tx + k];
-    hs[ty][tx] = (uint16_t)s;
+    for (int j = 0; j < 4; ++j) {
+      int s = 0;
+#pragma unroll
+      for (int k = 0; k < 7; ++k) s += c_gk[k] * tbyte(w3, j + 1 + k);
+      o[j] = s;
+    }
+    hs32[r][2 * q] = (uint32_t)o[0] | ((uint32_t)o[1] << 16);
+    hs32[r][2 * q + 1] = (uint32_t)o[2] | ((uint32_t)o[3] << 16);
   }
   __syncthreads();
-  const int ox = tid & 63, oy0 = (tid >> 6) * 4;
-  const int gx = bx0 + ox;
-  const int bp = (int)((U.w + 15) & ~15);
+  // vertical: 4 outputs per task (cols 4q..4q+3 of one row)
+  const int bp = (U.w + 15) & ~15;
   uint8_t* dst = blur + (size_t)f * bstride + U.blur_off;
+  for (int i = tid; i < TH * (TW / 4); i += 256) {
+    const int r = i / (TW / 4), q = i - r * (TW / 4);
+    uint32_t acc[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int oy = oy0 + r, gy = by0 + oy;
-    uint32_t s = 0;
+    for (int k = 0; k < 7; ++k) {
+      const uint32_t a = hs32[r + k][2 * q], b = hs32[r + k][2 * q + 1];
+      acc[0] += (uint32_t)c_gk[k] * (a & 0xFFFFu);
+      acc[1] += (uint32_t)c_gk[k] * (a >> 16);
+      acc[2] += (uint32_t)c_gk[k] * (b & 0xFFFFu);
+      acc[3] += (uint32_t)c_gk[k] * (b >> 16);
+    }
+    const int gy = y0 + r, gx = x0 + 4 * q;
+    if (gy >= U.h || gx >= U.w) continue;
+    uint32_t packed = 0;
 #pragma unroll
-    for (int k = 0; k < 7; ++k) s += (uint32_t)c_gk[k] * hs[oy + k][ox];
-    if (gx < U.w && gy < U.h) dst[(size_t)gy * bp + gx] = (uint8_t)min((s + 32768u) >> 16, 255u);
+    for (int j = 0; j < 4; ++j) packed |= min((acc[j] + 32768u) >> 16, 255u) << (8 * j);
+    uint8_t* o = dst + (size_t)gy * bp + gx;
+    if (gx + 3 < U.w) *reinterpret_cast<uint32_t*>(o) = packed;
+    else
+      for (int j = 0; gx + j < U.w; ++j) o[j] = (uint8_t)(packed >> (8 * j));
   }
 }
 

@@ -50,7 +50,7 @@ __device__ __forceinline__ int find_node_pair(const MNodePair* nps, int nnp, int
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_match_candidates(
     const MProblem* __restrict__ probs, const MNodePair* __restrict__ nps, int nnp, int nrows,
-    uint32_t* __restrict__ cand, int4* __restrict__ rowinfo, int2* __restrict__ ev) {
+    uint2* __restrict__ cand, int4* __restrict__ rowinfo, int2* __restrict__ ev) {
   __shared__ int hist[4][320];
   __shared__ uint32_t lessl[4][ORBM_T], eql[4][ORBM_T];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -143,19 +143,108 @@ __global__ __launch_bounds__(256) void k_match_candidates(
   }
   __builtin_amdgcn_wave_barrier();
   const int nlt = min(nl, ORBM_T), neq = max(0, min(ne, needEq));
-  uint32_t* out = cand + (size_t)r * ORBM_T;
+  uint2* out = cand + (size_t)r * ORBM_T;
   if (lane < nlt) {  // rank sort of the (< T) entries below the cutoff
     const uint32_t k = lessl[wave][lane];
     int rank = 0;
     for (int t = 0; t < nlt; ++t) rank += lessl[wave][t] < k;
-    out[rank] = k;
+    out[rank] = make_uint2(k, f2[k & 0xFFFFu]);
   }
   if (lane < ORBM_T && lane >= nlt) {
     const int e = lane - nlt;
-    out[lane] = (e < neq) ? eql[wave][e] : 0xFFFFFFFFu;
+    const uint32_t k = (e < neq) ? eql[wave][e] : 0xFFFFFFFFu;
+    out[lane] = make_uint2(k, k != 0xFFFFFFFFu ? f2[k & 0xFFFFu] : 0u);
   }
   if (lane == 0) rowinfo[r] = make_int4(1, nvalid, minD, idx1);
 }
+
+
+// ---------------------------------------------------------------------------
+// k_match_cand_lds: node pairs with n2 <= 64*NJ.  Workgroup = 64 rows of one
+// node pair; list2 descriptors staged once in LDS; every row's distances stay
+// in registers (NJ per lane).  rowinfo for every row; the sorted top-T
+// (dist<<16|pos, idx2) list only for rows whose best distance is < TH_LOW
+// (other rows can never be accepted and never change vbMatched2).
+// ---------------------------------------------------------------------------
+template <int NJ>
+__global__ __launch_bounds__(256) void k_match_cand_lds(
+    const MProblem* __restrict__ probs, const MNodePair* __restrict__ nps,
+    uint2* __restrict__ cand, int4* __restrict__ rowinfo, int2* __restrict__ ev) {
+  extern __shared__ uint4 sdesc[];  // 2 per list2 position
+  __shared__ uint32_t svalid[NJ * 2];
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const MNodePair NP = nps[blockIdx.y];
+  const int a0 = blockIdx.x * 64;
+  if (a0 >= NP.n1) return;
+  const MProblem P = probs[NP.prob];
+  const uint32_t* f2 = P.feat2 + NP.off2;
+  const int n2 = NP.n2;
+  for (int i = tid; i < NJ * 2; i += 256) svalid[i] = 0u;
+  __syncthreads();
+  for (int i = tid; i < 2 * n2; i += 256) {
+    const uint32_t idx2 = f2[i >> 1];
+    sdesc[i] = reinterpret_cast<const uint4*>(P.desc2 + (size_t)idx2 * 32)[i & 1];
+    if ((i & 1) == 0 && !(P.valid2 && !P.valid2[idx2])) atomicOr(&svalid[(i >> 1) >> 5], 1u << ((i >> 1) & 31));
+  }
+  __syncthreads();
+  const int INF = 0x7FFF;
+  for (int rr = wave; rr < 64; rr += 4) {
+    const int a = a0 + rr;
+    if (a >= NP.n1) break;
+    const int r = NP.row_base + a;
+    if (lane == 0) ev[r] = make_int2(-1, 0);
+    const int idx1 = (int)P.feat1[NP.off1 + a];
+    if (P.valid1 && !P.valid1[idx1]) {
+      if (lane == 0) rowinfo[r] = make_int4(0, 0, 0, idx1);
+      continue;
+    }
+    const uint4 q0 = reinterpret_cast<const uint4*>(P.desc1 + (size_t)idx1 * 32)[0];
+    const uint4 q1 = reinterpret_cast<const uint4*>(P.desc1 + (size_t)idx1 * 32)[1];
+    int d[NJ];
+    int mn = INF, nv = 0;
+#pragma unroll
+    for (int i = 0; i < NJ; ++i) {
+      const int pos = lane + 64 * i;
+      int dd = INF;
+      if (pos < n2 && ((svalid[pos >> 5] >> (pos & 31)) & 1u)) {
+        const uint4 b0 = sdesc[2 * pos], b1 = sdesc[2 * pos + 1];
+        dd = __popc(q0.x ^ b0.x) + __popc(q0.y ^ b0.y) + __popc(q0.z ^ b0.z) + __popc(q0.w ^ b0.w) +
+             __popc(q1.x ^ b1.x) + __popc(q1.y ^ b1.y) + __popc(q1.z ^ b1.z) + __popc(q1.w ^ b1.w);
+        ++nv;
+      }
+      d[i] = dd;
+      mn = min(mn, dd);
+    }
+#pragma unroll
+    for (int s = 32; s >= 1; s >>= 1) {
+      mn = min(mn, __shfl_xor(mn, s, 64));
+      nv += __shfl_xor(nv, s, 64);
+    }
+    if (lane == 0) rowinfo[r] = make_int4(1, nv, mn >= INF ? (1 << 20) : mn, idx1);
+    if (mn >= ORBM_TH_LOW) continue;
+    uint2* out = cand + (size_t)r * ORBM_T;
+    uint32_t key[NJ];
+#pragma unroll
+    for (int i = 0; i < NJ; ++i)
+      key[i] = d[i] < INF ? (((uint32_t)d[i] << 16) | (uint32_t)(lane + 64 * i)) : 0xFFFFFFFFu;
+    for (int t = 0; t < ORBM_T; ++t) {
+      uint32_t best = key[0];
+#pragma unroll
+      for (int i = 1; i < NJ; ++i) best = min(best, key[i]);
+#pragma unroll
+      for (int s = 32; s >= 1; s >>= 1) best = min(best, (uint32_t)__shfl_xor((int)best, s, 64));
+      if (lane == 0) out[t] = make_uint2(best, best != 0xFFFFFFFFu ? f2[best & 0xFFFFu] : 0u);
+      if (best == 0xFFFFFFFFu) {
+        if (lane > t && lane < ORBM_T) out[lane] = make_uint2(0xFFFFFFFFu, 0u);
+        break;
+      }
+#pragma unroll
+      for (int i = 0; i < NJ; ++i)
+        if (key[i] == best) key[i] = 0xFFFFFFFFu;
+    }
+  }
+}
+template __global__ void k_match_cand_lds<32>(const MProblem*, const MNodePair*, uint2*, int4*, int2*);
 
 // ---------------------------------------------------------------------------
 // k_match_resolve: greedy, in list order.  unit = node pair (parallel mode)
@@ -170,9 +259,10 @@ __device__ __forceinline__ void best_merge(uint32_t& k1, int& d2, uint32_t ok1, 
 
 __global__ __launch_bounds__(256) void k_match_resolve(
     const MProblem* __restrict__ probs, const MNodePair* __restrict__ nps, int nunits,
-    int sequential, const uint32_t* __restrict__ cand, const int4* __restrict__ rowinfo,
+    int sequential, const uint2* __restrict__ cand, const int4* __restrict__ rowinfo,
     int2* __restrict__ ev) {
   __shared__ uint32_t bitmap[4][ORBM_MAX_N2 / 32 / 4];  // 512 words (16384 idx2) per wave
+  __shared__ uint2 scand[4][64 * ORBM_T];                // one 64-row chunk of candidates per wave
   extern __shared__ uint32_t bigmap[];                   // used when n2 > 16384 (1 wave/block)
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int unit = blockIdx.x * (blockDim.x >> 6) + wave;
@@ -197,62 +287,78 @@ __global__ __launch_bounds__(256) void k_match_resolve(
   for (int j = np0; j < np1; ++j) {
     const MNodePair NP = nps[j];
     const uint32_t* f2 = P.feat2 + NP.off2;
-    for (int a = 0; a < NP.n1; ++a) {
-      const int r = NP.row_base + a;
-      const int4 info = rowinfo[r];
-      if (!info.x || info.z >= ORBM_TH_LOW) continue;  // invalid MP1, or can never pass TH_LOW
-      const uint32_t key = lane < ORBM_T ? cand[(size_t)r * ORBM_T + lane] : 0xFFFFFFFFu;
-      const int idx2 = key != 0xFFFFFFFFu ? (int)f2[key & 0xFFFFu] : 0;
-      const bool un = key != 0xFFFFFFFFu && !((bm[idx2 >> 5] >> (idx2 & 31)) & 1u);
-      const uint64_t m = __ballot(un);
-      int best1 = INT_MAX, best2 = INT_MAX, bidx2 = -1;
-      if (__popcll(m) >= 2 || info.y <= ORBM_T) {
-        if (m) {
-          const int l1 = __ffsll((unsigned long long)m) - 1;
-          best1 = (int)(__shfl(key, l1, 64) >> 16);
-          bidx2 = __shfl(idx2, l1, 64);
-          const uint64_t m2 = m & (m - 1);
-          if (m2) best2 = (int)(__shfl(key, __ffsll((unsigned long long)m2) - 1, 64) >> 16);
-        }
-      } else {  // candidates exhausted: exact rescan of the node's list
-        const uint32_t* q1 = reinterpret_cast<const uint32_t*>(P.desc1 + (size_t)info.w * 32);
-        uint32_t d1[8];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) d1[k] = q1[k];
-        uint32_t k1 = 0xFFFFFFFFu;
-        int d2 = INT_MAX;
-        for (int jj = lane; jj < NP.n2; jj += 64) {
-          const int i2 = (int)f2[jj];
-          if (P.valid2 && !P.valid2[i2]) continue;
-          if ((bm[i2 >> 5] >> (i2 & 31)) & 1u) continue;
-          const int d = hamming_u(d1, reinterpret_cast<const uint32_t*>(P.desc2 + (size_t)i2 * 32));
-          best_merge(k1, d2, ((uint32_t)d << 16) | (uint32_t)jj, INT_MAX);
-        }
-#pragma unroll
-        for (int s = 32; s >= 1; s >>= 1) {
-          const uint32_t ok = __shfl_xor(k1, s, 64);
-          const int od = __shfl_xor(d2, s, 64);
-          best_merge(k1, d2, ok, od);
-        }
-        if (k1 != 0xFFFFFFFFu) {
-          best1 = (int)(k1 >> 16);
-          bidx2 = (int)f2[k1 & 0xFFFFu];
-          best2 = d2;
-        }
-      }
-      if (best1 < ORBM_TH_LOW && (float)best1 < P.nnratio * (float)best2) {
-        int bin = 0;
-        if (P.check_ori) {
-          float rot = P.ang1[(size_t)info.w * P.ang_stride] - P.ang2[(size_t)bidx2 * P.ang_stride];
-          if (rot < 0.0f) rot += 360.0f;
-          bin = (int)roundf(rot * factor);
-          if (bin == ORBM_HISTO) bin = 0;
-        }
-        if (lane == 0) {
-          bm[bidx2 >> 5] |= 1u << (bidx2 & 31);
-          ev[r] = make_int2(bidx2, bin);
-        }
+    for (int base = 0; base < NP.n1; base += 64) {
+      // rows in list order, 64 at a time; only rows that can pass TH_LOW matter
+      int4 inf = make_int4(0, 0, 0, 0);
+      if (base + lane < NP.n1) inf = rowinfo[NP.row_base + base + lane];
+      uint64_t feas = __ballot(inf.x != 0 && inf.z < ORBM_TH_LOW);
+      if (feas) {  // stage the chunk's candidate lists (contiguous rows) in LDS
+        const int nr = min(64, NP.n1 - base);
+        const uint4* src = reinterpret_cast<const uint4*>(cand + (size_t)(NP.row_base + base) * ORBM_T);
+        uint4* dst = reinterpret_cast<uint4*>(scand[wave]);
+        for (int q = lane; q < nr * ORBM_T / 2; q += 64) dst[q] = src[q];
         __builtin_amdgcn_wave_barrier();
+      }
+      while (feas) {
+        const int l = __ffsll((unsigned long long)feas) - 1;
+        feas &= feas - 1;
+        const int r = NP.row_base + base + l;
+        const int idx1 = __shfl(inf.w, l, 64);
+        const int nvalid2 = __shfl(inf.y, l, 64);
+        const uint2 c = lane < ORBM_T ? scand[wave][l * ORBM_T + lane] : make_uint2(0xFFFFFFFFu, 0u);
+        const uint32_t key = c.x;
+        const int idx2 = (int)c.y;
+        const bool un = key != 0xFFFFFFFFu && !((bm[idx2 >> 5] >> (idx2 & 31)) & 1u);
+        const uint64_t m = __ballot(un);
+        int best1 = INT_MAX, best2 = INT_MAX, bidx2 = -1;
+        if (__popcll(m) >= 2 || nvalid2 <= ORBM_T) {
+          if (m) {
+            const int l1 = __ffsll((unsigned long long)m) - 1;
+            best1 = (int)(__shfl(key, l1, 64) >> 16);
+            bidx2 = __shfl(idx2, l1, 64);
+            const uint64_t m2 = m & (m - 1);
+            if (m2) best2 = (int)(__shfl(key, __ffsll((unsigned long long)m2) - 1, 64) >> 16);
+          }
+        } else {  // candidates exhausted: exact rescan of the node's list
+          const uint32_t* q1 = reinterpret_cast<const uint32_t*>(P.desc1 + (size_t)idx1 * 32);
+          uint32_t d1[8];
+#pragma unroll
+          for (int k = 0; k < 8; ++k) d1[k] = q1[k];
+          uint32_t k1 = 0xFFFFFFFFu;
+          int d2 = INT_MAX;
+          for (int jj = lane; jj < NP.n2; jj += 64) {
+            const int i2 = (int)f2[jj];
+            if (P.valid2 && !P.valid2[i2]) continue;
+            if ((bm[i2 >> 5] >> (i2 & 31)) & 1u) continue;
+            const int d = hamming_u(d1, reinterpret_cast<const uint32_t*>(P.desc2 + (size_t)i2 * 32));
+            best_merge(k1, d2, ((uint32_t)d << 16) | (uint32_t)jj, INT_MAX);
+          }
+#pragma unroll
+          for (int s = 32; s >= 1; s >>= 1) {
+            const uint32_t ok = __shfl_xor(k1, s, 64);
+            const int od = __shfl_xor(d2, s, 64);
+            best_merge(k1, d2, ok, od);
+          }
+          if (k1 != 0xFFFFFFFFu) {
+            best1 = (int)(k1 >> 16);
+            bidx2 = (int)f2[k1 & 0xFFFFu];
+            best2 = d2;
+          }
+        }
+        if (best1 < ORBM_TH_LOW && (float)best1 < P.nnratio * (float)best2) {
+          int bin = 0;
+          if (P.check_ori) {
+            float rot = P.ang1[(size_t)idx1 * P.ang_stride] - P.ang2[(size_t)bidx2 * P.ang_stride];
+            if (rot < 0.0f) rot += 360.0f;
+            bin = (int)roundf(rot * factor);
+            if (bin == ORBM_HISTO) bin = 0;
+          }
+          if (lane == 0) {
+            bm[bidx2 >> 5] |= 1u << (bidx2 & 31);
+            ev[r] = make_int2(bidx2, bin);
+          }
+          __builtin_amdgcn_wave_barrier();
+        }
       }
     }
   }
@@ -262,6 +368,7 @@ __global__ __launch_bounds__(256) void k_match_resolve(
 // k_match_finalize: one workgroup per problem.
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_match_finalize(const MProblem* __restrict__ probs,
+                                                        const MNodePair* __restrict__ nps,
                                                         const int4* __restrict__ rowinfo,
                                                         const int2* __restrict__ ev,
                                                         int* __restrict__ last_scratch,
@@ -280,13 +387,16 @@ __global__ __launch_bounds__(256) void k_match_finalize(const MProblem* __restri
   if (tid == 0) { s_nev = 0; s_nfilt = 0; }
   __syncthreads();
   int nev = 0;
-  for (int r = P.row_begin + tid; r < P.row_end; r += 256) {
-    const int2 e = ev[r];
-    if (e.x < 0) continue;
-    const int idx1 = rowinfo[r].w;
-    atomicMax(&last[idx1], r);
-    atomicAdd(&hist[e.y], 1);
-    ++nev;
+  for (int j = P.np_begin; j < P.np_end; ++j) {
+    const MNodePair NP = nps[j];
+    for (int r = NP.row_base + tid; r < NP.row_base + NP.n1; r += 256) {
+      const int2 e = ev[r];
+      if (e.x < 0) continue;
+      const int idx1 = rowinfo[r].w;
+      atomicMax(&last[idx1], r);
+      atomicAdd(&hist[e.y], 1);
+      ++nev;
+    }
   }
   atomicAdd(&s_nev, nev);
   __syncthreads();
@@ -308,21 +418,27 @@ __global__ __launch_bounds__(256) void k_match_finalize(const MProblem* __restri
     ind[0] = ti[0]; ind[1] = ti[1]; ind[2] = ti[2];
   }
   __syncthreads();
-  for (int r = P.row_begin + tid; r < P.row_end; r += 256) {
-    const int2 e = ev[r];
-    if (e.x < 0) continue;
-    const int idx1 = rowinfo[r].w;
-    if (last[idx1] == r) P.match12[idx1] = e.x;
+  for (int j = P.np_begin; j < P.np_end; ++j) {
+    const MNodePair NP = nps[j];
+    for (int r = NP.row_base + tid; r < NP.row_base + NP.n1; r += 256) {
+      const int2 e = ev[r];
+      if (e.x < 0) continue;
+      const int idx1 = rowinfo[r].w;
+      if (last[idx1] == r) P.match12[idx1] = e.x;
+    }
   }
   __syncthreads();
   int nf = 0;
   if (P.check_ori) {
-    for (int r = P.row_begin + tid; r < P.row_end; r += 256) {
-      const int2 e = ev[r];
-      if (e.x < 0) continue;
-      if (e.y == ind[0] || e.y == ind[1] || e.y == ind[2]) continue;
-      P.match12[rowinfo[r].w] = -1;
-      ++nf;
+    for (int j = P.np_begin; j < P.np_end; ++j) {
+      const MNodePair NP = nps[j];
+      for (int r = NP.row_base + tid; r < NP.row_base + NP.n1; r += 256) {
+        const int2 e = ev[r];
+        if (e.x < 0) continue;
+        if (e.y == ind[0] || e.y == ind[1] || e.y == ind[2]) continue;
+        P.match12[rowinfo[r].w] = -1;
+        ++nf;
+      }
     }
   }
   atomicAdd(&s_nfilt, nf);

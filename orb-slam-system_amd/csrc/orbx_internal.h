@@ -47,8 +47,15 @@ struct LevelInfo {
   long long qk_off;    /* offset of this level's key scratch (per frame)        */
   float scale;
   int patch_size;
+  int blur_tile_begin; /* first blur tile of this unique level (ORBX_BLUR_TW x ORBX_BLUR_TH) */
+  int blur_tiles_x;
+  int wcell;
   int pad;
 };
+
+#define ORBX_BLUR_TW 128
+#define ORBX_BLUR_TH 32
+#define ORBX_STRIP_MAXW 256 /* FAST strip: band width budget per workgroup */
 
 struct CellInfo {
   int level; /* unique level */
@@ -56,6 +63,16 @@ struct CellInfo {
   int slot_off; /* relative to the frame's slot base */
   int slot_cap;
   int pad;
+};
+
+/* FAST strip = consecutive valid cells of one cell row, processed by one
+ * workgroup; all its cells share y/h and their scan bands are contiguous. */
+struct StripInfo {
+  int level;      /* unique level */
+  int x, y, w, h; /* tile = [x, x+w) x [y, y+h) */
+  int cell_begin; /* first cell (index into the CellInfo table) */
+  int ncells;
+  int wcell;
 };
 
 #if defined(__HIPCC__)
