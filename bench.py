@@ -119,30 +119,34 @@ def main():
     mp = orbx.MatchPlan(B, kcap, args.topn, device=local)
     frames = torch.empty((B, H, W), dtype=torch.uint8, device=dev)
     orbx.synth_frames(frames, rank * B, args.kind)
-    # exchange buffer: last frame's keypoints (28 B) + descriptors (32 B) + count
+    # frame slots: 0 = the frame preceding this batch, 1..B = this batch
+    kps = torch.zeros((B + 1, kcap, 28), dtype=torch.uint8, device=dev)
+    desc = torch.zeros((B + 1, kcap, 32), dtype=torch.uint8, device=dev)
+    counts = torch.zeros(B + 1, dtype=torch.int32, device=dev)
+    # exchange buffer: a frame's keypoints (28 B) + descriptors (32 B) + count
     xbytes = kcap * 60 + 16
     mine = torch.zeros(xbytes, dtype=torch.uint8, device=dev)
     gathered = torch.zeros((world, xbytes), dtype=torch.uint8, device=dev)
     prev_rank = (rank - 1) % world
 
     def step():
-        plan.extract(frames)
-        if B > 1:
-            mp.match(B - 1, plan.kps[1:], plan.desc[1:], plan.counts[1:], plan.kps, plan.desc,
-                     plan.counts, args.nnratio, True)
+        # slot 0 <- last frame of the previous step: own (1 GPU) or, in frame-
+        # sharded multi-GPU runs, the previous rank's via RCCL all-gather
         if world > 1:
-            mine[:kcap * 28].copy_(plan.kps[B - 1].reshape(-1))
-            mine[kcap * 28:kcap * 60].copy_(plan.desc[B - 1].reshape(-1))
-            mine[kcap * 60:kcap * 60 + 4].copy_(plan.counts[B - 1:B].view(torch.uint8))
+            mine[:kcap * 28].copy_(kps[B].reshape(-1))
+            mine[kcap * 28:kcap * 60].copy_(desc[B].reshape(-1))
+            mine[kcap * 60:kcap * 60 + 4].copy_(counts[B:B + 1].view(torch.uint8))
             dist.all_gather_into_tensor(gathered.view(-1), mine)
             src = gathered[prev_rank]
-            kb = src[:kcap * 28].view(1, kcap, 28)
-            db = src[kcap * 28:kcap * 60].view(1, kcap, 32)
-            cb = src[kcap * 60:kcap * 60 + 4].view(torch.int32)
+            kps[0].copy_(src[:kcap * 28].view(kcap, 28))
+            desc[0].copy_(src[kcap * 28:kcap * 60].view(kcap, 32))
+            counts[0:1].copy_(src[kcap * 60:kcap * 60 + 4].view(torch.int32))
         else:
-            kb, db, cb = plan.kps[B - 1:], plan.desc[B - 1:], plan.counts[B - 1:]
-        mp.match(1, plan.kps, plan.desc, plan.counts, kb, db, cb, args.nnratio, True,
-                 out_offset=B - 1)
+            kps[0].copy_(kps[B])
+            desc[0].copy_(desc[B])
+            counts[0:1].copy_(counts[B:B + 1])
+        plan.extract(frames, out=(kps[1:], desc[1:], counts[1:]))
+        mp.match(B, kps[1:], desc[1:], counts[1:], kps, desc, counts, args.nnratio, True)
 
     for _ in range(args.warmup):
         step()
@@ -170,7 +174,7 @@ def main():
         t = torch.tensor([el], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
-    kps_total = int(plan.counts[:B].sum().item())
+    kps_total = int(counts[1:].sum().item())
     nmatch = int(mp.nmatches[:B].sum().item())
     if rank != 0:
         if world > 1:

@@ -23,12 +23,9 @@ __global__ void k_fast_strips(const uint8_t*, size_t, size_t, const uint8_t*, si
 __global__ void k_quadtree(const LevelInfo*, const CellInfo*, const uint32_t*, size_t,
                            const uint32_t*, int, uint32_t*, int32_t*, size_t, uint32_t*, size_t,
                            int*, int, int, int, int*);
-__global__ void k_blur_tiles(const uint8_t*, size_t, size_t, const uint8_t*, size_t, uint8_t*,
-                             size_t, const LevelInfo*, int);
 __global__ void k_orient_brief(const uint8_t*, size_t, size_t, const uint8_t*, size_t,
-                               const uint8_t*, size_t, const LevelInfo*, int, const uint32_t*,
-                               size_t, const int*, const int16_t*, int, orbx_keypoint*, uint8_t*,
-                               int*, int);
+                               const LevelInfo*, int, const uint32_t*, size_t, const int*,
+                               const int16_t*, int, orbx_keypoint*, uint8_t*, int*, int);
 __global__ void k_synth(uint8_t*, int, int, size_t, int, int);
 }  // namespace orbx
 
@@ -219,7 +216,6 @@ extern "C" int orbx_plan_create(const orbx_params* prm, int width, int height, i
   p->qout_stride = round_up((size_t)P.kcap, 64);
   const size_t B = (size_t)max_batch;
   if (dev_alloc((void**)&p->d_pyr, B * p->pyr_stride) ||
-      dev_alloc((void**)&p->d_blur, B * p->blur_stride) ||
       dev_alloc((void**)&p->d_slots, B * p->slot_stride * 4) ||
       dev_alloc((void**)&p->d_ccount, B * (size_t)(P.ncells ? P.ncells : 1) * 4) ||
       dev_alloc((void**)&p->d_qkeys, B * p->qk_stride * 4) ||
@@ -298,17 +294,11 @@ extern "C" int orbx_plan_extract(orbx_plan* p, const uint8_t* frames, int nframe
                      p->qk_stride, p->d_qout, p->qout_stride, p->d_lcount, L, P.qt_smax,
                      P.qt_max_cells, p->d_err);
   p->timer.end(ORBX_STAGE_QUADTREE, s);
-  // K5 blur of every unique level
-  p->timer.begin(ORBX_STAGE_BLUR, s);
-  if (P.blur_tiles > 0)
-    hipLaunchKernelGGL(k_blur_tiles, dim3(P.blur_tiles, n), dim3(256), 0, s, frames, fstride,
-                       rstride, p->d_pyr, p->pyr_stride, p->d_blur, p->blur_stride, p->d_lv, L);
-  p->timer.end(ORBX_STAGE_BLUR, s);
-  // K4+K6+K7 orientation, descriptors, assembly
+  // K4+K5+K6+K7 orientation, blur-at-sample descriptors, assembly
   p->timer.begin(ORBX_STAGE_BRIEF, s);
   hipLaunchKernelGGL(k_orient_brief, dim3((P.kcap + 3) / 4 > 0 ? (P.kcap + 3) / 4 : 1, n),
                      dim3(256), 0, s, frames, fstride, rstride, p->d_pyr, p->pyr_stride,
-                     p->d_blur, p->blur_stride, p->d_lv, L, p->d_qout, p->qout_stride,
+                     p->d_lv, L, p->d_qout, p->qout_stride,
                      p->d_lcount, p->d_disk, p->ndisk, kps, desc, counts, P.kcap);
   p->timer.end(ORBX_STAGE_BRIEF, s);
   if (hipGetLastError() != hipSuccess) return ORBX_ERR_HIP;

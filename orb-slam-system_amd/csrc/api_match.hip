@@ -15,8 +15,11 @@ __global__ void k_match_candidates(const MProblem*, const MNodePair*, int, int, 
                                    int2*);
 template <int NJ>
 __global__ void k_match_cand_lds(const MProblem*, const MNodePair*, uint2*, int4*, int2*);
+__global__ void k_match_cand_rows(const MProblem*, const MNodePair*, uint2*, int4*, int2*);
 __global__ void k_match_resolve(const MProblem*, const MNodePair*, int, int, const uint2*,
                                 const int4*, int2*);
+__global__ void k_match_resolve_spec(const MProblem*, const MNodePair*, int, const uint2*,
+                                     const int4*, int2*, int);
 __global__ void k_match_finalize(const MProblem*, const MNodePair*, const int4*, const int2*, int*,
                                  const int*);
 __global__ void k_match_select(MProblem*, MNodePair*, const orbx_keypoint*, const int*,
@@ -72,7 +75,14 @@ void launch_match(const MProblem* d_probs, int nprob, const MNodePair* d_nps, in
                   StageTimer* timer) {
   if (timer) timer->begin(ORBX_STAGE_MCAND, s);
   if (nrows > 0 && nnp > 0) {
-    if (max_n2 <= 64 * 32 && nnp <= 65535) {
+    if (max_n2 <= 4096 && nnp <= 65535) {
+      // lane = row; list2 staged in LDS (broadcast reads); running top-T in registers
+      const size_t lds = (size_t)std::max(max_n2, 1) * 32 + ((size_t)(max_n2 + 31) / 32) * 4;
+      hipFuncSetAttribute((const void*)k_match_cand_rows,
+                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      hipLaunchKernelGGL(k_match_cand_rows, dim3((max_n1 + 255) / 256, nnp), dim3(256), lds, s,
+                         d_probs, d_nps, d_cand, d_rowinfo, d_ev);
+    } else if (max_n2 <= 64 * 32 && nnp <= 65535) {
       // list2 staged in LDS, distances in registers (32 per lane)
       const size_t lds = (size_t)std::max(max_n2, 1) * 32;
       hipFuncSetAttribute((const void*)k_match_cand_lds<32>,
@@ -87,7 +97,15 @@ void launch_match(const MProblem* d_probs, int nprob, const MNodePair* d_nps, in
   if (timer) timer->end(ORBX_STAGE_MCAND, s);
   if (timer) timer->begin(ORBX_STAGE_MRESOLVE, s);
   const int units = sequential ? nprob : nnp;
-  if (nrows > 0 && units > 0) {
+  if (nrows > 0 && units > 0 && !sequential && max_bitmap_n2 <= 16384) {
+    // speculative 64-row chunks; LDS = vbMatched2 bitmap + claim table
+    const int n2cap = std::max(max_bitmap_n2, 32);
+    const size_t lds = (size_t)((n2cap + 31) / 32) * 4 + (size_t)n2cap * 4;
+    hipFuncSetAttribute((const void*)k_match_resolve_spec,
+                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(k_match_resolve_spec, dim3(units), dim3(64), lds, s, d_probs, d_nps, units,
+                       d_cand, d_rowinfo, d_ev, n2cap);
+  } else if (nrows > 0 && units > 0) {
     if (max_bitmap_n2 > 16384) {
       const size_t lds = (size_t)((max_bitmap_n2 + 31) / 32) * 4;
       hipFuncSetAttribute((const void*)k_match_resolve, hipFuncAttributeMaxDynamicSharedMemorySize,

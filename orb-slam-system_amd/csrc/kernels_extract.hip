@@ -2,10 +2,10 @@
 //
 // Stage map (reference file:line -> kernel):
 //   ComputePyramid / cv::resize      ORBextractor.cc:497-515  -> k_resize
-//   cell FAST + NMS + retry          ORBextractor.cc:316-340  -> k_fast_cells
+//   cell FAST + NMS + retry          ORBextractor.cc:316-340  -> k_fast_strips
 //   DistributeOctTree                ORBextractor.cc:228-286  -> k_quadtree
-//   GaussianBlur 7x7 (descriptors)   ORBextractor.cc:478-479  -> k_blur
-//   IC_Angle + computeOrbDescriptor  ORBextractor.cc:21-73    -> k_orient_brief
+//   IC_Angle + GaussianBlur 7x7 +   ORBextractor.cc:21-73,   -> k_orient_brief
+//   computeOrbDescriptor             478-479
 //   + output assembly (:455-494)
 // All integer work is exact; the float work (fastAtan2, BRIEF rotation) is
 // written operation-for-operation with -ffp-contract=off and explicit fmaf.
@@ -616,93 +616,16 @@ __global__ __launch_bounds__(256) void k_quadtree(
 }
 
 // ---------------------------------------------------------------------------
-// k_blur_tiles: cv::GaussianBlur(7x7, sigma 2, BORDER_REFLECT_101) on 8U with
-// the bit-exact fixed-point kernel [18,34,48,56,48,34,18]/256:
-// H = sum k_i p (u16), out = (sum k_j H_j + 32768) >> 16.
-// One launch for every unique level: workgroup = one 128x32 output tile;
-// 4 outputs per thread per pass, dword LDS reads, dword global stores.
+// cv::GaussianBlur(7x7, sigma 2, BORDER_REFLECT_101) on 8U (ORBextractor.cc:479)
+// uses OpenCV's bit-exact fixed-point kernel [18,34,48,56,48,34,18]/256:
+// H = sum k_i p (u16 exact), out = (sum k_j H_j + 32768) >> 16.  All integer,
+// so it is evaluated only where BRIEF samples it (k_orient_brief).
 // ---------------------------------------------------------------------------
 __constant__ int c_gk[7] = {18, 34, 48, 56, 48, 34, 18};
 
 __device__ __forceinline__ int reflect101(int p, int len) {
   p = p < 0 ? -p : p;
   return p >= len ? 2 * len - 2 - p : p;
-}
-
-__global__ __launch_bounds__(256) void k_blur_tiles(const uint8_t* __restrict__ frames,
-                                                    size_t fstride, size_t rstride,
-                                                    const uint8_t* __restrict__ pyr, size_t pstride,
-                                                    uint8_t* __restrict__ blur, size_t bstride,
-                                                    const LevelInfo* __restrict__ lv, int nlevels) {
-  constexpr int TW = ORBX_BLUR_TW, TH = ORBX_BLUR_TH, IW = TW + 8, IH = TH + 6;
-  __shared__ uint32_t in32[IH][IW / 4];      // input tile, col 0 = global x0-4
-  __shared__ uint32_t hs32[IH][TW / 2];      // horizontal pass, u16 pairs
-  const int tid = threadIdx.x, f = blockIdx.y;
-  int u = 0;
-  for (int l = 0; l < nlevels; ++l)
-    if (lv[l].unique == l && (int)blockIdx.x >= lv[l].blur_tile_begin) u = l;
-  const LevelInfo U = lv[u];
-  const int t = blockIdx.x - U.blur_tile_begin;
-  const int x0 = (t % U.blur_tiles_x) * TW, y0 = (t / U.blur_tiles_x) * TH;
-  int pitch;
-  const uint8_t* src = level_base(frames, fstride, rstride, pyr, pstride, U, u, f, &pitch);
-  const bool interior = x0 >= 4 && x0 + TW + 4 <= U.w && y0 >= 3 && y0 + TH + 3 <= U.h &&
-                        ((reinterpret_cast<uintptr_t>(src) | (uintptr_t)pitch) & 3) == 0;
-  if (interior) {
-    for (int i = tid; i < IH * (IW / 4); i += 256) {
-      const int r = i / (IW / 4), c = i - r * (IW / 4);
-      in32[r][c] = reinterpret_cast<const uint32_t*>(src + (size_t)(y0 - 3 + r) * pitch + x0 - 4)[c];
-    }
-  } else {
-    uint8_t* in8 = reinterpret_cast<uint8_t*>(in32);
-    for (int i = tid; i < IH * IW; i += 256) {
-      const int r = i / IW, c = i - r * IW;
-      const int gx = reflect101(min(max(x0 - 4 + c, -3), U.w + 2), U.w);
-      const int gy = reflect101(min(max(y0 - 3 + r, -3), U.h + 2), U.h);
-      in8[r * IW + c] = src[(size_t)gy * pitch + gx];
-    }
-  }
-  __syncthreads();
-  // horizontal: 4 outputs (cols 4q..4q+3) per task, need input cols 4q+1 .. 4q+10
-  for (int i = tid; i < IH * (TW / 4); i += 256) {
-    const int r = i / (TW / 4), q = i - r * (TW / 4);
-    uint32_t w3[3] = {in32[r][q], in32[r][q + 1], in32[r][q + 2]};
-    int o[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      int s = 0;
-#pragma unroll
-      for (int k = 0; k < 7; ++k) s += c_gk[k] * tbyte(w3, j + 1 + k);
-      o[j] = s;
-    }
-    hs32[r][2 * q] = (uint32_t)o[0] | ((uint32_t)o[1] << 16);
-    hs32[r][2 * q + 1] = (uint32_t)o[2] | ((uint32_t)o[3] << 16);
-  }
-  __syncthreads();
-  // vertical: 4 outputs per task (cols 4q..4q+3 of one row)
-  const int bp = (U.w + 15) & ~15;
-  uint8_t* dst = blur + (size_t)f * bstride + U.blur_off;
-  for (int i = tid; i < TH * (TW / 4); i += 256) {
-    const int r = i / (TW / 4), q = i - r * (TW / 4);
-    uint32_t acc[4] = {0u, 0u, 0u, 0u};
-#pragma unroll
-    for (int k = 0; k < 7; ++k) {
-      const uint32_t a = hs32[r + k][2 * q], b = hs32[r + k][2 * q + 1];
-      acc[0] += (uint32_t)c_gk[k] * (a & 0xFFFFu);
-      acc[1] += (uint32_t)c_gk[k] * (a >> 16);
-      acc[2] += (uint32_t)c_gk[k] * (b & 0xFFFFu);
-      acc[3] += (uint32_t)c_gk[k] * (b >> 16);
-    }
-    const int gy = y0 + r, gx = x0 + 4 * q;
-    if (gy >= U.h || gx >= U.w) continue;
-    uint32_t packed = 0;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) packed |= min((acc[j] + 32768u) >> 16, 255u) << (8 * j);
-    uint8_t* o = dst + (size_t)gy * bp + gx;
-    if (gx + 3 < U.w) *reinterpret_cast<uint32_t*>(o) = packed;
-    else
-      for (int j = 0; gx + j < U.w; ++j) o[j] = (uint8_t)(packed >> (8 * j));
-  }
 }
 
 // ---------------------------------------------------------------------------
@@ -750,13 +673,19 @@ __device__ __forceinline__ void brief_sincos(float x, float* s, float* c) {
   }
 }
 
+// Keypoint patch: rows y-21..y+21, 48 columns from (x-21) & ~3 (dword aligned);
+// covers IC_Angle's radius-15 disk and every blur tap of the radius-18 samples.
+#define KP_R 21
+#define KP_ROWS 43
+#define KP_COLS 48
+
 __global__ __launch_bounds__(256) void k_orient_brief(
     const uint8_t* __restrict__ frames, size_t fstride, size_t rstride,
-    const uint8_t* __restrict__ pyr, size_t pstride, const uint8_t* __restrict__ blur,
-    size_t bstride, const LevelInfo* __restrict__ lv, int nlevels,
+    const uint8_t* __restrict__ pyr, size_t pstride, const LevelInfo* __restrict__ lv, int nlevels,
     const uint32_t* __restrict__ qout, size_t qout_stride, const int* __restrict__ lcount,
     const int16_t* __restrict__ disk, int ndisk, orbx_keypoint* __restrict__ kps,
     uint8_t* __restrict__ desc, int* __restrict__ counts, int kcap) {
+  __shared__ uint32_t patch[4][KP_ROWS][KP_COLS / 4];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int f = blockIdx.y;
   const int g = blockIdx.x * 4 + wave;
@@ -782,11 +711,34 @@ __global__ __launch_bounds__(256) void k_orient_brief(
   const LevelInfo U = lv[u];
   int pitch;
   const uint8_t* img = level_base(frames, fstride, rstride, pyr, pstride, U, u, f, &pitch);
-  const uint8_t* center = img + (size_t)y * pitch + x;
+  // stage the patch (unblurred level), reflect-101 outside the image
+  const int px0 = (x - KP_R) & ~3, py0 = y - KP_R;
+  uint32_t(*P)[KP_COLS / 4] = patch[wave];
+  const bool inside = px0 >= 0 && px0 + KP_COLS <= U.w && py0 >= 0 && py0 + KP_ROWS <= U.h &&
+                      ((reinterpret_cast<uintptr_t>(img) | (uintptr_t)pitch) & 3) == 0;
+  if (inside) {
+    for (int q = lane; q < KP_ROWS * (KP_COLS / 4); q += 64) {
+      const int r = q / (KP_COLS / 4), c = q - r * (KP_COLS / 4);
+      P[r][c] = reinterpret_cast<const uint32_t*>(img + (size_t)(py0 + r) * pitch + px0)[c];
+    }
+  } else {
+    uint8_t* P8 = reinterpret_cast<uint8_t*>(P);
+    for (int q = lane; q < KP_ROWS * KP_COLS; q += 64) {
+      const int r = q / KP_COLS, c = q - r * KP_COLS;
+      const int gy = reflect101(min(max(py0 + r, -3), U.h + 2), U.h);
+      const int gx = reflect101(min(max(px0 + c, -3), U.w + 2), U.w);
+      P8[q] = img[(size_t)gy * pitch + gx];
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  const uint8_t* P8 = reinterpret_cast<const uint8_t*>(P);
+  // IC_Angle (:21-48) on the unblurred level
+  const int cc = x - px0, cr = KP_R;
   int m10 = 0, m01 = 0;
   for (int j = lane; j < ndisk; j += 64) {
     const int du = disk[2 * j], dv = disk[2 * j + 1];
-    const int I = center[dv * pitch + du];
+    const int I = P8[(cr + dv) * KP_COLS + cc + du];
     m10 += du * I;
     m01 += dv * I;
   }
@@ -799,23 +751,35 @@ __global__ __launch_bounds__(256) void k_orient_brief(
   const float factorPI = (float)(3.1415926535897932384626433832795 / 180.f);
   float sn, cs;
   brief_sincos(angle * factorPI, &sn, &cs);
-  const int bp = (U.w + 15) & ~15;
-  const uint8_t* bc = blur + (size_t)f * bstride + U.blur_off + (size_t)y * bp + x;
+  // BRIEF (:57-73) on GaussianBlur(7x7, sigma 2) evaluated at each sample:
+  // out = (sum_j k_j * (sum_i k_i p) + 32768) >> 16, rows via v_dot4_u32_u8
+  const uint32_t K0 = 18u | (34u << 8) | (48u << 16) | (56u << 24), K1 = 48u | (34u << 8) | (18u << 16);
   uint64_t words[4];
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int p = lane + 64 * r;
+  for (int rr = 0; rr < 4; ++rr) {
+    const int p = lane + 64 * rr;
     int t[2];
 #pragma unroll
     for (int e = 0; e < 2; ++e) {
-      const float px = (float)ORBX_BRIEF_PATTERN[p][2 * e];
-      const float py = (float)ORBX_BRIEF_PATTERN[p][2 * e + 1];
-      const float ya = py * cs, yb = py * sn;
-      const int row = (int)__builtin_rintf(__builtin_fmaf(px, sn, ya));
-      const int col = (int)__builtin_rintf(__builtin_fmaf(px, cs, -yb));
-      t[e] = bc[row * bp + col];
+      const float fx = (float)ORBX_BRIEF_PATTERN[p][2 * e];
+      const float fy = (float)ORBX_BRIEF_PATTERN[p][2 * e + 1];
+      const float ya = fy * cs, yb = fy * sn;
+      const int row = (int)__builtin_rintf(__builtin_fmaf(fx, sn, ya));
+      const int col = (int)__builtin_rintf(__builtin_fmaf(fx, cs, -yb));
+      const int r0 = cr + row - 3, c0 = cc + col - 3;
+      const int qd = c0 >> 2, sh = c0 & 3;
+      uint32_t acc = 0;
+#pragma unroll
+      for (int jj = 0; jj < 7; ++jj) {
+        const uint32_t w0 = P[r0 + jj][qd], w1 = P[r0 + jj][qd + 1], w2 = P[r0 + jj][qd + 2];
+        const uint32_t lo4 = __builtin_amdgcn_alignbyte(w1, w0, sh);
+        const uint32_t hi4 = __builtin_amdgcn_alignbyte(w2, w1, sh);
+        const uint32_t h = __builtin_amdgcn_udot4(hi4, K1, __builtin_amdgcn_udot4(lo4, K0, 0u, false), false);
+        acc += (uint32_t)c_gk[jj] * h;
+      }
+      t[e] = (int)min((acc + 32768u) >> 16, 255u);
     }
-    words[r] = __ballot(t[0] < t[1]);
+    words[rr] = __ballot(t[0] < t[1]);
   }
   if (lane < 4) {
     const uint64_t w = lane == 0 ? words[0] : lane == 1 ? words[1] : lane == 2 ? words[2] : words[3];

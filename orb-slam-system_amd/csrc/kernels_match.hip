@@ -246,6 +246,96 @@ __global__ __launch_bounds__(256) void k_match_cand_lds(
 }
 template __global__ void k_match_cand_lds<32>(const MProblem*, const MNodePair*, uint2*, int4*, int2*);
 
+
+// ---------------------------------------------------------------------------
+// k_match_cand_rows: lane = row (KF1 feature), 256 rows per workgroup.
+// The node's list2 descriptors are staged once in LDS and read at a
+// wave-uniform address (broadcast); each lane keeps its 8 smallest
+// (distance<<16 | list position) keys sorted in registers, so the list is
+// exactly the first 8 of the reference's scan order.  Positions are visited
+// in list order; a wave skips the insertion network when no lane improves.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_match_cand_rows(
+    const MProblem* __restrict__ probs, const MNodePair* __restrict__ nps,
+    uint2* __restrict__ cand, int4* __restrict__ rowinfo, int2* __restrict__ ev) {
+  extern __shared__ uint4 sdesc[];  // 2 per list2 position, then validity bits
+  const int tid = threadIdx.x;
+  const MNodePair NP = nps[blockIdx.y];
+  const int a0 = blockIdx.x * 256;
+  if (a0 >= NP.n1) return;
+  const MProblem P = probs[NP.prob];
+  const uint32_t* f2 = P.feat2 + NP.off2;
+  const int n2 = NP.n2;
+  uint32_t* svalid = reinterpret_cast<uint32_t*>(sdesc + 2 * n2);
+  for (int i = tid; i < ((n2 + 31) >> 5); i += 256) svalid[i] = 0u;
+  __syncthreads();
+  for (int i = tid; i < 2 * n2; i += 256) {
+    const uint32_t idx2 = f2[i >> 1];
+    sdesc[i] = reinterpret_cast<const uint4*>(P.desc2 + (size_t)idx2 * 32)[i & 1];
+    if ((i & 1) == 0 && !(P.valid2 && !P.valid2[idx2]))
+      atomicOr(&svalid[(i >> 1) >> 5], 1u << ((i >> 1) & 31));
+  }
+  __syncthreads();
+  int nvalid = 0;
+  for (int w = 0; w < ((n2 + 31) >> 5); ++w) nvalid += __popc(svalid[w]);
+  const int a = a0 + tid;
+  const bool act = a < NP.n1;
+  const int r = NP.row_base + a;
+  int idx1 = 0;
+  bool v1 = false;
+  uint4 q0 = make_uint4(0, 0, 0, 0), q1 = q0;
+  if (act) {
+    idx1 = (int)P.feat1[NP.off1 + a];
+    v1 = !(P.valid1 && !P.valid1[idx1]);
+    q0 = reinterpret_cast<const uint4*>(P.desc1 + (size_t)idx1 * 32)[0];
+    q1 = reinterpret_cast<const uint4*>(P.desc1 + (size_t)idx1 * 32)[1];
+  }
+  uint32_t L[ORBM_T];
+#pragma unroll
+  for (int t = 0; t < ORBM_T; ++t) L[t] = 0xFFFFFFFFu;
+  for (int j0 = 0; j0 < n2; j0 += 4) {
+    uint32_t kk[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int j = min(j0 + q, n2 - 1);
+      const uint4 b0 = sdesc[2 * j], b1 = sdesc[2 * j + 1];
+      const bool ok = (j0 + q < n2) && ((svalid[j >> 5] >> (j & 31)) & 1u);
+      const uint32_t d = __popc(q0.x ^ b0.x) + __popc(q0.y ^ b0.y) + __popc(q0.z ^ b0.z) +
+                         __popc(q0.w ^ b0.w) + __popc(q1.x ^ b1.x) + __popc(q1.y ^ b1.y) +
+                         __popc(q1.z ^ b1.z) + __popc(q1.w ^ b1.w);
+      kk[q] = ok ? ((d << 16) | (uint32_t)j) : 0xFFFFFFFFu;
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      uint32_t k = kk[q];
+      if (__ballot(k < L[ORBM_T - 1])) {
+#pragma unroll
+        for (int t = 0; t < ORBM_T; ++t) {
+          const uint32_t lo = min(L[t], k);
+          k = max(L[t], k);
+          L[t] = lo;
+        }
+      }
+    }
+  }
+  if (!act) return;
+  ev[r] = make_int2(-1, 0);
+  if (!v1) {
+    rowinfo[r] = make_int4(0, 0, 0, idx1);
+    return;
+  }
+  const int minD = L[0] != 0xFFFFFFFFu ? (int)(L[0] >> 16) : (1 << 20);
+  rowinfo[r] = make_int4(1, nvalid, minD, idx1);
+  if (minD >= ORBM_TH_LOW) return;
+  uint4* out = reinterpret_cast<uint4*>(cand + (size_t)r * ORBM_T);
+#pragma unroll
+  for (int t = 0; t < ORBM_T / 2; ++t) {
+    const uint32_t ka = L[2 * t], kb = L[2 * t + 1];
+    out[t] = make_uint4(ka, ka != 0xFFFFFFFFu ? f2[ka & 0xFFFFu] : 0u, kb,
+                        kb != 0xFFFFFFFFu ? f2[kb & 0xFFFFu] : 0u);
+  }
+}
+
 // ---------------------------------------------------------------------------
 // k_match_resolve: greedy, in list order.  unit = node pair (parallel mode)
 // or problem (sequential mode: all its node pairs, one bitmap).
@@ -359,6 +449,138 @@ __global__ __launch_bounds__(256) void k_match_resolve(
           }
           __builtin_amdgcn_wave_barrier();
         }
+      }
+    }
+  }
+}
+
+
+// ---------------------------------------------------------------------------
+// k_match_resolve_spec: the greedy walk, 64 rows at a time, speculatively.
+// One wavefront per node pair (well-formed FeatureVectors, n2 <= n2cap).
+// Each round every pending row of the chunk decides against the committed
+// vbMatched2 bitmap; accepted rows claim their KF2 feature (LDS atomicMin of
+// the lane); a row whose examined candidates include a feature claimed by an
+// earlier row of the chunk -- or whose candidate list ran out -- is a
+// boundary: every pending row before it is exactly what the serial walk
+// would decide, so those commit together and the rest re-decide.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(64) void k_match_resolve_spec(
+    const MProblem* __restrict__ probs, const MNodePair* __restrict__ nps, int nunits,
+    const uint2* __restrict__ cand, const int4* __restrict__ rowinfo, int2* __restrict__ ev,
+    int n2cap) {
+  extern __shared__ uint32_t sm[];
+  uint32_t* bm = sm;                                   // (n2cap + 31) / 32 words
+  int* claim = reinterpret_cast<int*>(sm + ((n2cap + 31) >> 5));  // n2cap
+  const int lane = threadIdx.x;
+  const int unit = blockIdx.x;
+  if (unit >= nunits) return;
+  const MNodePair NP = nps[unit];
+  const MProblem P = probs[NP.prob];
+  const uint32_t* f2 = P.feat2 + NP.off2;
+  for (int w = lane; w < ((P.n2 + 31) >> 5); w += 64) bm[w] = 0u;
+  for (int w = lane; w < P.n2; w += 64) claim[w] = 64;
+  __builtin_amdgcn_wave_barrier();
+  const float factor = 1.0f / ORBM_HISTO;
+  const uint64_t below = (1ull << lane) - 1ull;
+  for (int base = 0; base < NP.n1; base += 64) {
+    const int r = NP.row_base + base + lane;
+    int4 inf = make_int4(0, 0, 0, 0);
+    if (base + lane < NP.n1) inf = rowinfo[r];
+    const bool feas = inf.x != 0 && inf.z < ORBM_TH_LOW;
+    uint64_t pend = __ballot(feas);
+    if (!pend) continue;
+    uint2 c[ORBM_T];
+#pragma unroll
+    for (int t = 0; t < ORBM_T; ++t) c[t] = make_uint2(0xFFFFFFFFu, 0u);
+    if (feas) {
+      const uint4* src = reinterpret_cast<const uint4*>(cand + (size_t)r * ORBM_T);
+#pragma unroll
+      for (int t = 0; t < ORBM_T / 2; ++t) {
+        const uint4 v = src[t];
+        c[2 * t] = make_uint2(v.x, v.y);
+        c[2 * t + 1] = make_uint2(v.z, v.w);
+      }
+    }
+    while (pend) {
+      const bool mine = (pend >> lane) & 1ull;
+      int k1 = INT_MAX, k2 = INT_MAX, id1 = -1, nun = 0, plen = ORBM_T;
+      if (mine) {
+#pragma unroll
+        for (int t = 0; t < ORBM_T; ++t) {
+          if (nun >= 2 || c[t].x == 0xFFFFFFFFu) continue;
+          const int i2 = (int)c[t].y;
+          if ((bm[i2 >> 5] >> (i2 & 31)) & 1u) continue;
+          if (nun == 0) { k1 = (int)(c[t].x >> 16); id1 = i2; }
+          else { k2 = (int)(c[t].x >> 16); plen = t + 1; }
+          ++nun;
+        }
+      }
+      const bool hard = mine && nun < 2 && inf.y > ORBM_T;  // list exhausted: needs a rescan
+      const bool acc = mine && !hard && k1 < ORBM_TH_LOW && (float)k1 < P.nnratio * (float)k2;
+      if (acc) atomicMin(&claim[id1], lane);
+      __builtin_amdgcn_wave_barrier();
+      bool conf = false;
+      if (mine) {
+#pragma unroll
+        for (int t = 0; t < ORBM_T; ++t)
+          if (t < plen && c[t].x != 0xFFFFFFFFu && claim[c[t].y] < lane) conf = true;
+      }
+      const uint64_t cm = __ballot(conf || hard);
+      const int bnd = cm ? (__ffsll((unsigned long long)cm) - 1) : 64;
+      __builtin_amdgcn_wave_barrier();
+      if (acc) claim[id1] = 64;
+      if (mine && lane < bnd && acc) {
+        int bin = 0;
+        if (P.check_ori) {
+          float rot = P.ang1[(size_t)inf.w * P.ang_stride] - P.ang2[(size_t)id1 * P.ang_stride];
+          if (rot < 0.0f) rot += 360.0f;
+          bin = (int)roundf(rot * factor);
+          if (bin == ORBM_HISTO) bin = 0;
+        }
+        atomicOr(&bm[id1 >> 5], 1u << (id1 & 31));
+        ev[r] = make_int2(id1, bin);
+      }
+      __builtin_amdgcn_wave_barrier();
+      pend &= (bnd >= 64) ? 0ull : ~((1ull << bnd) - 1ull);
+      if (pend && bnd < 64 && ((__ballot(hard) >> bnd) & 1ull)) {
+        // lowest pending row ran out of candidates: exact rescan of list2 (whole wave)
+        const int idx1 = __shfl(inf.w, bnd, 64);
+        const uint32_t* q1 = reinterpret_cast<const uint32_t*>(P.desc1 + (size_t)idx1 * 32);
+        uint32_t d1[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) d1[k] = q1[k];
+        uint32_t kb = 0xFFFFFFFFu;
+        int d2 = INT_MAX;
+        for (int jj = lane; jj < NP.n2; jj += 64) {
+          const int i2 = (int)f2[jj];
+          if (P.valid2 && !P.valid2[i2]) continue;
+          if ((bm[i2 >> 5] >> (i2 & 31)) & 1u) continue;
+          const int d = hamming_u(d1, reinterpret_cast<const uint32_t*>(P.desc2 + (size_t)i2 * 32));
+          best_merge(kb, d2, ((uint32_t)d << 16) | (uint32_t)jj, INT_MAX);
+        }
+#pragma unroll
+        for (int s = 32; s >= 1; s >>= 1) {
+          const uint32_t ok = __shfl_xor(kb, s, 64);
+          const int od = __shfl_xor(d2, s, 64);
+          best_merge(kb, d2, ok, od);
+        }
+        if (kb != 0xFFFFFFFFu) {
+          const int b1 = (int)(kb >> 16), bi = (int)f2[kb & 0xFFFFu];
+          if (b1 < ORBM_TH_LOW && (float)b1 < P.nnratio * (float)d2 && lane == bnd) {
+            int bin = 0;
+            if (P.check_ori) {
+              float rot = P.ang1[(size_t)idx1 * P.ang_stride] - P.ang2[(size_t)bi * P.ang_stride];
+              if (rot < 0.0f) rot += 360.0f;
+              bin = (int)roundf(rot * factor);
+              if (bin == ORBM_HISTO) bin = 0;
+            }
+            atomicOr(&bm[bi >> 5], 1u << (bi & 31));
+            ev[r] = make_int2(bi, bin);
+          }
+        }
+        __builtin_amdgcn_wave_barrier();
+        pend &= ~(1ull << bnd);
       }
     }
   }

@@ -302,15 +302,17 @@ class Plan:
             _lib.orbx_plan_destroy(self._h)
             self._h = None
 
-    def extract(self, frames, stream=None):
-        """frames: cuda uint8 tensor [B, H, W] (row stride W).  Async."""
+    def extract(self, frames, stream=None, out=None):
+        """frames: cuda uint8 tensor [B, H, W] (row stride W).  Async.
+        out: optional (kps [>=B, kcap, 28] u8, desc [>=B, kcap, 32] u8, counts [>=B] i32)."""
         B = frames.shape[0]
         assert frames.dtype.itemsize == 1 and frames.is_contiguous()
         assert frames.shape[1] == self.H and frames.shape[2] == self.W and B <= self.max_batch
+        kps, desc, counts = out if out is not None else (self.kps, self.desc, self.counts)
+        assert kps.shape[1] == self.kcap and desc.shape[1] == self.kcap
         _check(_lib.orbx_plan_extract(self._h, frames.data_ptr(), B, self.W * self.H, self.W,
-                                      self.kps.data_ptr(), self.desc.data_ptr(),
-                                      self.counts.data_ptr(), _stream_handle(stream)),
-               "orbx_plan_extract")
+                                      kps.data_ptr(), desc.data_ptr(), counts.data_ptr(),
+                                      _stream_handle(stream)), "orbx_plan_extract")
 
     def check(self, stream=None):
         _check(_lib.orbx_plan_check(self._h, _stream_handle(stream)), "orbx_plan_check")

@@ -187,3 +187,23 @@ def test_match_plan_matches_oracle(gpu, oracle, W, H, nf, kind):
         rm, rnm = oracle.search_by_bow(_topn_bow(ka, da, nf), _topn_bow(kb, db, nf), 0.75, True)
         assert nm[p] == rnm
         assert np.array_equal(m12[p, :len(ka)], rm)
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_search_by_bow_heavy_contention(gpu, oracle, seed):
+    """Many KF1 rows compete for few KF2 features: exercises speculative-chunk
+    conflicts and exhausted candidate lists (exact rescans)."""
+    rng = np.random.default_rng(100 + seed)
+    base = rng.integers(0, 256, (12, 32), dtype=np.uint8)
+    n1, n2 = 700, 40
+    d1 = _correlated(rng, base[rng.integers(0, 12, n1)], rng.integers(0, 20, n1))
+    d2 = _correlated(rng, base[rng.integers(0, 12, n2)], rng.integers(0, 20, n2))
+    one = lambda d: dict(desc=d, angle=rng.uniform(0, 360, len(d)).astype(np.float32),
+                         valid=(rng.uniform(size=len(d)) > 0.05).astype(np.uint8),
+                         node_id=np.array([3], np.uint32), off=np.array([0, len(d)], np.uint32),
+                         feat=np.arange(len(d), dtype=np.uint32))
+    kf1, kf2 = one(d1), one(d2)
+    for ratio in (0.6, 0.9, 1.0):
+        m, nm = gpu.search_by_bow(kf1, kf2, ratio, seed != 1)
+        rm, rnm = oracle.search_by_bow(kf1, kf2, ratio, seed != 1)
+        assert nm == rnm and np.array_equal(m, rm), ratio
