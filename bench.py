@@ -101,6 +101,7 @@ def main():
     import torch
     import torch.distributed as dist
     import orbx
+    from orbx.dist import BoundaryExchange, shard_first_frame
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -118,29 +119,21 @@ def main():
     kcap = plan.kcap
     mp = orbx.MatchPlan(B, kcap, args.topn, device=local)
     frames = torch.empty((B, H, W), dtype=torch.uint8, device=dev)
-    orbx.synth_frames(frames, rank * B, args.kind)
+    orbx.synth_frames(frames, shard_first_frame(rank, B), args.kind)
     # frame slots: 0 = the frame preceding this batch, 1..B = this batch
     kps = torch.zeros((B + 1, kcap, 28), dtype=torch.uint8, device=dev)
     desc = torch.zeros((B + 1, kcap, 32), dtype=torch.uint8, device=dev)
     counts = torch.zeros(B + 1, dtype=torch.int32, device=dev)
-    # exchange buffer: a frame's keypoints (28 B) + descriptors (32 B) + count
-    xbytes = kcap * 60 + 16
-    mine = torch.zeros(xbytes, dtype=torch.uint8, device=dev)
-    gathered = torch.zeros((world, xbytes), dtype=torch.uint8, device=dev)
+    xch = BoundaryExchange(kcap, world, dev)
     prev_rank = (rank - 1) % world
 
     def step():
         # slot 0 <- last frame of the previous step: own (1 GPU) or, in frame-
         # sharded multi-GPU runs, the previous rank's via RCCL all-gather
         if world > 1:
-            mine[:kcap * 28].copy_(kps[B].reshape(-1))
-            mine[kcap * 28:kcap * 60].copy_(desc[B].reshape(-1))
-            mine[kcap * 60:kcap * 60 + 4].copy_(counts[B:B + 1].view(torch.uint8))
-            dist.all_gather_into_tensor(gathered.view(-1), mine)
-            src = gathered[prev_rank]
-            kps[0].copy_(src[:kcap * 28].view(kcap, 28))
-            desc[0].copy_(src[kcap * 28:kcap * 60].view(kcap, 32))
-            counts[0:1].copy_(src[kcap * 60:kcap * 60 + 4].view(torch.int32))
+            xch.pack(kps[B], desc[B], counts[B:B + 1])
+            xch.exchange(dist)
+            xch.unpack_into(prev_rank, kps[0], desc[0], counts[0:1])
         else:
             kps[0].copy_(kps[B])
             desc[0].copy_(desc[B])
