@@ -58,10 +58,12 @@ def stage_bytes(geo, nframes, kps_total, npairs, topn):
     uniq = [l for l in range(L) if alias[l] == l]
     resize = sum(P[l] + P[alias[l - 1]] for l in uniq if l > 0)
     fast = sum(P[l] for l in uniq)
-    blur = 2 * sum(P[l] for l in uniq)
-    brief = 1321 * kps_total  # 749 disk + 512 samples + 60 output bytes per keypoint
+    # per keypoint: the 43x43 source patch the IC disk (r=15) and the blurred
+    # BRIEF samples (|offset| <= 13*sqrt(2), +3 blur taps) cover, + 28 B
+    # keypoint + 32 B descriptor out
+    brief = (43 * 43 + 60) * kps_total
     match = npairs * (2 * topn * 32 + topn * 8)
-    return {"resize": resize * nframes, "fast_cells": fast * nframes, "blur": blur * nframes,
+    return {"resize": resize * nframes, "fast_cells": fast * nframes,
             "orient_brief": brief, "match_candidates": match}
 
 
@@ -184,14 +186,17 @@ def main():
         ach = by[dom] / (per_step[dom] * 1e-3) / 1e9
         traffic = None
         if os.path.exists(args.traffic):
-            try:
-                traffic = json.load(open(args.traffic)).get(dom)
-            except Exception:
+            try:  # tools/pmc_traffic.py: corrected FETCH_SIZE+WRITE_SIZE per launch
+                ent = json.load(open(args.traffic)).get(dom)
+                traffic = ent["bytes_per_launch"] if ent else None
+            except (OSError, ValueError, KeyError):
                 traffic = None
         roof = {"bound": "hbm", "kernel": dom, "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
-                "bytes_per_step": by[dom], "launches_per_step": dom_launches,
-                "ms_per_step": round(per_step[dom], 4)}
+                "traffic_unit": "HBM bytes per launch (rocprofv3 PMC, batch %d)" % B,
+                "algorithmic_bytes_per_launch": round(by[dom] / dom_launches),
+                "launches_per_step": dom_launches,
+                "avg_launch_ms": round(per_step[dom] / dom_launches, 5)}
     out = {
         "metric": "ORB extract+match frames/sec at %dx%d, %d pyramid levels" % (W, H, args.nlevels),
         "value": round(frames_total / el, 2),

@@ -14,18 +14,17 @@
 #include "geometry.h"
 
 namespace orbx {
-__global__ void k_resize(const uint8_t*, size_t, size_t, uint8_t*, size_t, const LevelInfo*, int,
-                         const int32_t*, const int32_t*, const int16_t*, const int32_t*,
-                         const int16_t*);
+__global__ void k_pyramid(const uint8_t*, size_t, size_t, uint8_t*, size_t, const PyrSeg,
+                          const int4*, const int4*, const uint4*, const int*);
 __global__ void k_fast_strips(const uint8_t*, size_t, size_t, const uint8_t*, size_t,
                               const LevelInfo*, const CellInfo*, const StripInfo*, uint32_t*,
-                              size_t, uint32_t*, int, int, int, int, int, int, int);
+                              size_t, uint32_t*, int, int, int, int, int, int);
 __global__ void k_quadtree(const LevelInfo*, const CellInfo*, const uint32_t*, size_t,
                            const uint32_t*, int, uint32_t*, int32_t*, size_t, uint32_t*, size_t,
                            int*, int, int, int, int*);
 __global__ void k_orient_brief(const uint8_t*, size_t, size_t, const uint8_t*, size_t,
-                               const LevelInfo*, int, const uint32_t*, size_t, const int*,
-                               const int16_t*, int, orbx_keypoint*, uint8_t*, int*, int);
+                               const BriefArgs, const uint32_t*, size_t, const int*,
+                               const int16_t*, int, orbx_keypoint*, uint8_t*, int*);
 __global__ void k_synth(uint8_t*, int, int, size_t, int, int);
 }  // namespace orbx
 
@@ -122,6 +121,8 @@ struct orbx_plan {
   int fs_tpitch = 0, fs_tmaxh = 0, fs_qcap = 0, fs_mcells = 0;
   size_t fs_lds = 0;
   int32_t *d_xofs = nullptr, *d_xofs1 = nullptr, *d_yofs = nullptr;
+  int32_t *d_pyr_xs = nullptr, *d_pyr_ys = nullptr, *d_pyr_bo = nullptr;
+  uint32_t* d_pyr_blob = nullptr;
   int16_t *d_alpha = nullptr, *d_beta = nullptr, *d_disk = nullptr;
   int ndisk = 0;
   uint8_t *d_pyr = nullptr, *d_blur = nullptr;
@@ -130,6 +131,7 @@ struct orbx_plan {
   int *d_lcount = nullptr, *d_err = nullptr;
   size_t pyr_stride = 0, blur_stride = 0, slot_stride = 0, qk_stride = 0, qout_stride = 0;
   size_t qt_lds = 0;
+  BriefArgs bargs;
   StageTimer timer;
 };
 
@@ -140,7 +142,7 @@ static void plan_free(orbx_plan* p) {
   hipSetDevice(p->device);
   void* bufs[] = {p->d_lv, p->d_cells, p->d_strips, p->d_xofs, p->d_xofs1, p->d_yofs, p->d_alpha, p->d_beta,
                   p->d_disk, p->d_pyr, p->d_blur, p->d_slots, p->d_ccount, p->d_qkeys, p->d_qout,
-                  p->d_qnode, p->d_lcount, p->d_err};
+                  p->d_qnode, p->d_lcount, p->d_err, p->d_pyr_xs, p->d_pyr_ys, p->d_pyr_bo, p->d_pyr_blob};
   for (void* b : bufs)
     if (b) hipFree(b);
   p->timer.release();
@@ -188,15 +190,28 @@ extern "C" int orbx_plan_create(const orbx_params* prm, int width, int height, i
     for (int u = -um; u <= um; ++u) { disk.push_back((int16_t)u); disk.push_back((int16_t)v); }
   }
   p->ndisk = (int)disk.size() / 2;
-  // FAST strip LDS: tile + strength map + candidate queue + row masks + counts
+  memset(&p->bargs, 0, sizeof(p->bargs));
+  p->bargs.nlevels = P.params.nlevels;
+  p->bargs.kcap = P.kcap;
+  for (int l = 0; l < P.params.nlevels; ++l) {
+    const LevelInfo& lv = P.levels[l];
+    p->bargs.kout_off[l] = lv.kout_off;
+    p->bargs.lcap[l] = lv.kcap;
+    p->bargs.unique[l] = lv.unique;
+    p->bargs.w[l] = lv.w;
+    p->bargs.h[l] = lv.h;
+    p->bargs.pitch[l] = lv.pitch;
+    p->bargs.pyr_off[l] = lv.pyr_off;
+    p->bargs.scale[l] = lv.scale;
+    p->bargs.patch[l] = lv.patch_size;
+  }
+  // FAST strip LDS: tile + strength map + row masks + counts
   {
-    int qmax = 1;
-    for (const StripInfo& st : P.strips) qmax = std::max(qmax, (st.w - 6) * (st.h - 6));
-    p->fs_tpitch = (3 + P.strip_max_w + 8 + 3) & ~3;
+    p->fs_tpitch = (3 + P.strip_max_w + 8 + 3 + 7) & ~7;
     p->fs_tmaxh = std::max(P.strip_max_h, 7);
-    p->fs_qcap = qmax;
+    p->fs_qcap = 0;
     p->fs_mcells = std::max(P.strip_max_cells, 1);
-    p->fs_lds = 2 * (size_t)p->fs_tpitch * p->fs_tmaxh + 2 * (size_t)p->fs_qcap + 8 +
+    p->fs_lds = 2 * (size_t)p->fs_tpitch * p->fs_tmaxh +
                 8 * (size_t)p->fs_mcells * (p->fs_tmaxh - 6) + 4 * (size_t)p->fs_mcells + 16;
     if (p->fs_lds > 150 * 1024) { plan_free(p); return ORBX_ERR_UNSUPPORTED; }
     if (hipFuncSetAttribute((const void*)k_fast_strips, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -205,7 +220,9 @@ extern "C" int orbx_plan_create(const orbx_params* prm, int width, int height, i
   if (upload(&p->d_lv, P.levels) || upload(&p->d_cells, P.cells) || upload(&p->d_strips, P.strips) ||
       upload(&p->d_xofs, P.xofs) ||
       upload(&p->d_xofs1, P.xofs1) || upload(&p->d_yofs, P.yofs) || upload(&p->d_alpha, P.alpha) ||
-      upload(&p->d_beta, P.beta) || upload(&p->d_disk, disk)) {
+      upload(&p->d_beta, P.beta) || upload(&p->d_disk, disk) ||
+      upload(&p->d_pyr_xs, P.pyr_xs) || upload(&p->d_pyr_ys, P.pyr_ys) ||
+      upload(&p->d_pyr_bo, P.pyr_bo) || upload(&p->d_pyr_blob, P.pyr_blob)) {
     plan_free(p);
     return ORBX_ERR_HIP;
   }
@@ -269,13 +286,12 @@ extern "C" int orbx_plan_extract(orbx_plan* p, const uint8_t* frames, int nframe
   const int L = P.params.nlevels, n = nframes;
   // K1 pyramid
   p->timer.begin(ORBX_STAGE_RESIZE, s);
-  for (int l = 1; l < L; ++l) {
-    const LevelInfo& lv = P.levels[l];
-    if (lv.unique != l) continue;
-    dim3 grid((lv.w + 127) / 128, (lv.h + 15) / 16, n), block(256);
-    hipLaunchKernelGGL(k_resize, grid, block, 0, s, frames, fstride, rstride, p->d_pyr,
-                       p->pyr_stride, p->d_lv, l, p->d_xofs, p->d_xofs1, p->d_alpha, p->d_yofs,
-                       p->d_beta);
+  for (const PyrSeg& g : P.segs) {
+    hipLaunchKernelGGL(k_pyramid, dim3(g.ntx * g.nty, n), dim3(256),
+                       g.lds_a + g.lds_b + g.lds_xl + g.lds_yl, s, frames, fstride, rstride,
+                       p->d_pyr, p->pyr_stride, g, reinterpret_cast<const int4*>(p->d_pyr_xs),
+                       reinterpret_cast<const int4*>(p->d_pyr_ys),
+                       reinterpret_cast<const uint4*>(p->d_pyr_blob), p->d_pyr_bo);
   }
   p->timer.end(ORBX_STAGE_RESIZE, s);
   // K2 FAST cells
@@ -284,7 +300,7 @@ extern "C" int orbx_plan_extract(orbx_plan* p, const uint8_t* frames, int nframe
     hipLaunchKernelGGL(k_fast_strips, dim3((unsigned)P.strips.size(), n), dim3(256), p->fs_lds, s,
                        frames, fstride, rstride, p->d_pyr, p->pyr_stride, p->d_lv, p->d_cells,
                        p->d_strips, p->d_slots, p->slot_stride, p->d_ccount, P.ncells, P.ini_th,
-                       P.min_th, p->fs_tpitch, p->fs_tmaxh, p->fs_qcap, p->fs_mcells);
+                       P.min_th, p->fs_tpitch, p->fs_tmaxh, p->fs_mcells);
   }
   p->timer.end(ORBX_STAGE_FAST, s);
   // K3 DistributeOctTree
@@ -297,9 +313,9 @@ extern "C" int orbx_plan_extract(orbx_plan* p, const uint8_t* frames, int nframe
   // K4+K5+K6+K7 orientation, blur-at-sample descriptors, assembly
   p->timer.begin(ORBX_STAGE_BRIEF, s);
   hipLaunchKernelGGL(k_orient_brief, dim3((P.kcap + 3) / 4 > 0 ? (P.kcap + 3) / 4 : 1, n),
-                     dim3(256), 0, s, frames, fstride, rstride, p->d_pyr, p->pyr_stride,
-                     p->d_lv, L, p->d_qout, p->qout_stride,
-                     p->d_lcount, p->d_disk, p->ndisk, kps, desc, counts, P.kcap);
+                     dim3(256), 0, s, frames, fstride, rstride, p->d_pyr, p->pyr_stride, p->bargs,
+                     p->d_qout, p->qout_stride, p->d_lcount, p->d_disk, p->ndisk, kps, desc,
+                     counts);
   p->timer.end(ORBX_STAGE_BRIEF, s);
   if (hipGetLastError() != hipSuccess) return ORBX_ERR_HIP;
   return ORBX_OK;

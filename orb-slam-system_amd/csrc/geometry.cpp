@@ -117,6 +117,218 @@ static bool area_fast_2x(int sw, int sh, int dw, int dh) {
          ix == 2 && iy == 2;
 }
 
+/* ---- fused pyramid tiling (k_pyramid) ----------------------------------
+ * 1-D chain for one axis of segment levels lev[0..ns-1] (lev[0] = source).
+ * The last level is cut into tiles of T; each coarser level's owned
+ * intervals are the source positions of the finer level's tile starts, so
+ * they partition the level.  Computed intervals are built from the last
+ * level back: C(s-1) = hull(footprint of C(s), owned(s-1)). */
+struct Iv { int clo, chi, plo, phi; };
+
+static void src_span(const Plan& P, int l, bool isx, int d, int& lo, int& hi) {
+  const LevelInfo& lv = P.levels[l];
+  const LevelInfo& sv = P.levels[lv.src_level];
+  if (isx) {
+    lo = P.xofs[lv.lut_x + d];
+    hi = P.xofs1[lv.lut_x + d];
+  } else {
+    const int sy = P.yofs[lv.lut_y + d];
+    lo = std::min(std::max(sy, 0), sv.h - 1);
+    hi = std::min(std::max(sy + 1, 0), sv.h - 1);
+  }
+}
+
+static int chain_1d(const Plan& P, const std::vector<int>& lev, bool isx, int T,
+                    std::vector<Iv>& out) {
+  const int ns = (int)lev.size();
+  auto size = [&](int s) { return isx ? P.levels[lev[s]].w : P.levels[lev[s]].h; };
+  const int nt = (size(ns - 1) + T - 1) / T;
+  out.assign((size_t)ns * nt, Iv{0, 0, 0, 0});
+  std::vector<int> X(nt + 1);
+  for (int t = 0; t <= nt; ++t) X[t] = std::min(t * T, size(ns - 1));
+  for (int s = ns - 1; s >= 1; --s) {
+    for (int t = 0; t < nt; ++t) {
+      out[(size_t)s * nt + t].plo = X[t];
+      out[(size_t)s * nt + t].phi = X[t + 1];
+    }
+    std::vector<int> Xn(nt + 1);
+    Xn[0] = 0;
+    Xn[nt] = size(s - 1);
+    for (int t = 1; t < nt; ++t) {
+      int lo = size(s - 1), hi;
+      if (X[t] < size(s)) src_span(P, lev[s], isx, X[t], lo, hi);
+      Xn[t] = std::min(std::max(lo, Xn[t - 1]), size(s - 1));
+    }
+    X.swap(Xn);
+  }
+  for (int t = 0; t < nt; ++t) {
+    int clo = out[(size_t)(ns - 1) * nt + t].plo, chi = out[(size_t)(ns - 1) * nt + t].phi;
+    for (int s = ns - 1; s >= 1; --s) {
+      out[(size_t)s * nt + t].clo = clo;
+      out[(size_t)s * nt + t].chi = chi;
+      int flo = 1 << 30, fhi = -1;
+      for (int d = clo; d < chi; ++d) { /* footprint (LUTs are monotone; scan to be safe) */
+        int lo, hi;
+        src_span(P, lev[s], isx, d, lo, hi);
+        flo = std::min(flo, lo);
+        fhi = std::max(fhi, hi);
+      }
+      if (s - 1 >= 1) {
+        const Iv& o = out[(size_t)(s - 1) * nt + t];
+        if (o.phi > o.plo) { flo = std::min(flo, o.plo); fhi = std::max(fhi, o.phi - 1); }
+      }
+      if (fhi < flo) { clo = chi = 0; } else { clo = flo; chi = fhi + 1; }
+    }
+    out[t].clo = clo;
+    out[t].chi = chi;
+    out[t].plo = out[t].phi = 0;
+  }
+  return nt;
+}
+
+/* LDS bytes of level s's region (formulas shared with k_pyramid) */
+static long long region_bytes(const Iv& x, const Iv& y, int s) {
+  if (x.chi <= x.clo || y.chi <= y.clo) return 0;
+  long long pitch;
+  if (s == 0) pitch = ((x.chi + 15) & ~15) - (x.clo & ~15);
+  else pitch = (long long)((x.chi - (x.clo & ~3) + 3) >> 2) * 4;
+  return pitch * (y.chi - y.clo);
+}
+
+static bool try_segment(Plan& P, const std::vector<int>& lev, int TW, int TH, PyrSeg& g,
+                        std::vector<Iv>& xs, std::vector<Iv>& ys) {
+  const int ns = (int)lev.size();
+  const int ntx = chain_1d(P, lev, true, TW, xs);
+  const int nty = chain_1d(P, lev, false, TH, ys);
+  long long a = 0, b = 0;
+  for (int s = 0; s < ns; ++s) {
+    long long m = 0;
+    for (int tx = 0; tx < ntx; ++tx) {
+      const Iv& x = xs[(size_t)s * ntx + tx];
+      if (s > 0 && ((x.chi - (x.clo & ~3) + 3) >> 2) > 256) return false;
+      for (int ty = 0; ty < nty; ++ty) m = std::max(m, region_bytes(x, ys[(size_t)s * nty + ty], s));
+    }
+    if (s % 2 == 0) a = std::max(a, m); else b = std::max(b, m);
+  }
+  a = (a + 15) & ~15LL;
+  b = (b + 15) & ~15LL;
+  if (a + b > ORBX_PYR_LDS_BUDGET) return false;
+  long long bx = 0, by = 0; /* LUT blob entries (build_blobs layout) */
+  for (int tx = 0; tx < ntx; ++tx) {
+    long long n = 0;
+    for (int s = 1; s < ns; ++s) {
+      const Iv& x = xs[(size_t)s * ntx + tx];
+      if (x.chi > x.clo) n += 4 * ((x.chi - (x.clo & ~3) + 3) >> 2);
+    }
+    bx = std::max(bx, (n + 1) & ~1LL);
+  }
+  for (int ty = 0; ty < nty; ++ty) {
+    long long n = 0;
+    for (int s = 1; s < ns; ++s) n += std::max(0, ys[(size_t)s * nty + ty].chi - ys[(size_t)s * nty + ty].clo);
+    by = std::max(by, (n + 1) & ~1LL);
+  }
+  if (a + b + 8 * (bx + by) > ORBX_PYR_LDS_MAX) return false;
+  memset(&g, 0, sizeof(g));
+  g.nl = ns - 1;
+  g.ntx = ntx;
+  g.nty = nty;
+  g.lds_a = (int)a;
+  g.lds_b = (int)b;
+  for (int s = 0; s < ns; ++s) {
+    const LevelInfo& lv = P.levels[lev[s]];
+    g.lev[s] = lev[s];
+    g.w[s] = lv.w;
+    g.h[s] = lv.h;
+    g.pitch[s] = lv.pitch;
+    g.off[s] = lev[s] == 0 ? -1 : lv.pyr_off;
+    g.lut_x[s] = s ? lv.lut_x : 0;
+    g.lut_y[s] = s ? lv.lut_y : 0;
+  }
+  return true;
+}
+
+/* per tile column / row LUT blobs (layout: orbx_internal.h) */
+static void build_blobs(Plan& P, const std::vector<int>& lev, PyrSeg& g, const std::vector<Iv>& xs,
+                        const std::vector<Iv>& ys) {
+  const int ns = (int)lev.size();
+  for (int axis = 0; axis < 2; ++axis) {
+    const bool isx = axis == 0;
+    const int nt = isx ? g.ntx : g.nty;
+    const std::vector<Iv>& v = isx ? xs : ys;
+    (isx ? g.xbo_off : g.ybo_off) = (int)P.pyr_bo.size();
+    int maxn = 0;
+    for (int t = 0; t < nt; ++t) {
+      P.pyr_bo.push_back((int)(P.pyr_blob.size() / 2));
+      int n = 0;
+      for (int s = 1; s < ns; ++s) {
+        const Iv& c = v[(size_t)s * nt + t];
+        const Iv& pc = v[(size_t)(s - 1) * nt + t];
+        const int origin = isx ? (s - 1 == 0 ? (pc.clo & ~15) : (pc.clo & ~3)) : pc.clo;
+        const LevelInfo& lv = P.levels[lev[s]];
+        int b, e;
+        if (isx) {
+          b = c.clo & ~3;
+          e = b + 4 * ((c.chi - b + 3) >> 2);
+        } else {
+          b = c.clo;
+          e = c.chi;
+        }
+        if (c.chi <= c.clo) e = b;
+        for (int d = b; d < e; ++d) {
+          const int dd = std::min(std::max(d, c.clo), c.chi - 1);
+          int lo, hi;
+          src_span(P, lev[s], isx, dd, lo, hi);
+          const int16_t* cf = isx ? &P.alpha[2 * (lv.lut_x + dd)] : &P.beta[2 * (lv.lut_y + dd)];
+          P.pyr_blob.push_back((uint32_t)(lo - origin) | ((uint32_t)(hi - origin) << 16));
+          P.pyr_blob.push_back((uint32_t)(uint16_t)cf[0] | ((uint32_t)(uint16_t)cf[1] << 16));
+          ++n;
+        }
+      }
+      while (n & 1) { P.pyr_blob.push_back(0); P.pyr_blob.push_back(0); ++n; } /* 16-B pad */
+      maxn = std::max(maxn, n);
+    }
+    P.pyr_bo.push_back((int)(P.pyr_blob.size() / 2));
+    (isx ? g.lds_xl : g.lds_yl) = 8 * maxn;
+  }
+}
+
+/* greedy: longest run of unique levels from `first` that fits a tile of at
+ * least 32x16 at its last level (smaller tiles only for a single level) */
+static int plan_pyramid(Plan& P) {
+  P.segs.clear();
+  P.pyr_xs.clear();
+  P.pyr_ys.clear();
+  P.pyr_blob.clear();
+  P.pyr_bo.clear();
+  std::vector<int> uniq;
+  for (int l = 0; l < (int)P.levels.size(); ++l)
+    if (P.levels[l].unique == l) uniq.push_back(l);
+  static const int tiles[][2] = {{64, 32}, {64, 16}, {32, 32}, {32, 16}, {16, 16}, {16, 8}, {8, 8}};
+  size_t i = 1;
+  while (i < uniq.size()) {
+    bool done = false;
+    for (size_t j = uniq.size(); j > i && !done; --j) {
+      std::vector<int> lev(uniq.begin() + (i - 1), uniq.begin() + j);
+      const int ntile = (j == i + 1) ? 7 : 4;
+      for (int k = 0; k < ntile && !done; ++k) {
+        PyrSeg g;
+        std::vector<Iv> xs, ys;
+        if (!try_segment(P, lev, tiles[k][0], tiles[k][1], g, xs, ys)) continue;
+        g.xs_off = (int)(P.pyr_xs.size() / 4);
+        g.ys_off = (int)(P.pyr_ys.size() / 4);
+        for (const Iv& v : xs) P.pyr_xs.insert(P.pyr_xs.end(), {v.clo, v.chi, v.plo, v.phi});
+        for (const Iv& v : ys) P.pyr_ys.insert(P.pyr_ys.end(), {v.clo, v.chi, v.plo, v.phi});
+        build_blobs(P, lev, g, xs, ys);
+        P.segs.push_back(g);
+        i = j;
+        done = true;
+      }
+    }
+    if (!done) return ORBX_ERR_UNSUPPORTED; /* level ratio too large for one tile */
+  }
+  return ORBX_OK;
+}
+
 int plan_geometry(const orbx_params& p, int width, int height, Plan& P) {
   int rc = compute_tables(p, P.tables);
   if (rc) return rc;
@@ -183,6 +395,8 @@ int plan_geometry(const orbx_params& p, int width, int height, Plan& P) {
     lv.lut_y = (int)P.yofs.size();
     resize_lut(src.w, src.h, lv.w, lv.h, P.xofs, P.xofs1, P.alpha, P.yofs, P.beta);
   }
+  rc = plan_pyramid(P);
+  if (rc) return rc;
 
   /* FAST cell grid (ComputeKeyPointsOctTree :298-340) for unique levels */
   long long slots = 0;

@@ -39,6 +39,11 @@ struct Plan {
   std::vector<int32_t> xofs1;  /* second tap column (clamped) */
   std::vector<int32_t> yofs;
   std::vector<int16_t> beta;
+  std::vector<PyrSeg> segs;      /* fused pyramid launches, in dependency order */
+  std::vector<int32_t> pyr_xs;   /* {clo, chi, plo, phi} quads */
+  std::vector<int32_t> pyr_ys;
+  std::vector<uint32_t> pyr_blob; /* LUT blobs (pairs of u32 = uint2 entries) */
+  std::vector<int32_t> pyr_bo;    /* blob start offsets (uint2 units), per segment ntx+1, nty+1 */
   long long pyr_bytes = 0, blur_bytes = 0, nslots = 0, qk_elems = 0;
   int ncells = 0, kcap = 0;
   int qt_smax = 0;     /* max DistributeOctTree splittable list length */

@@ -1,7 +1,7 @@
 // kernels_extract.hip -- gfx950 kernels of the ORB extractor hot path.
 //
 // Stage map (reference file:line -> kernel):
-//   ComputePyramid / cv::resize      ORBextractor.cc:497-515  -> k_resize
+//   ComputePyramid / cv::resize      ORBextractor.cc:497-515  -> k_pyramid
 //   cell FAST + NMS + retry          ORBextractor.cc:316-340  -> k_fast_strips
 //   DistributeOctTree                ORBextractor.cc:228-286  -> k_quadtree
 //   IC_Angle + GaussianBlur 7x7 +   ORBextractor.cc:21-73,   -> k_orient_brief
@@ -38,106 +38,145 @@ __device__ __forceinline__ const uint8_t* level_base(const uint8_t* frames, size
 }
 
 // ---------------------------------------------------------------------------
-// k_resize: level l (unique, >= 1) from level l-1 with OpenCV's INTER_LINEAR
-// fixed-point arithmetic: D = S[sx]*a0 + S[sx1]*a1 (int32),
+// k_pyramid: a chain of unique levels (PyrSeg) with OpenCV's INTER_LINEAR
+// fixed-point arithmetic (resize.cpp HResizeLinear / VResizeLinear<uchar>):
+// D = S[sx]*a0 + S[sx1]*a1 (int32),
 // dst = (((b0*(D0>>4))>>16) + ((b1*(D1>>4))>>16) + 2) >> 2.
-// Workgroup = 128x16 output tile; the source footprint is staged in LDS
-// with dword loads; each thread makes 4 columns x 2 rows (two dword stores).
+// Workgroup = one tile of the segment's last level.  The source region is
+// staged in LDS once; every finer level is computed into the other LDS
+// buffer (ping-pong) and only the owned interval goes to HBM, so each level
+// is written once and the intermediate levels are never re-read from HBM.
+// Thread = 4 consecutive columns (dword in LDS and HBM) of a row.
 // ---------------------------------------------------------------------------
-#define RS_TW 128
-#define RS_TH 16
-#define RS_SR 40   /* staged source rows  (level ratio <= ~2.2) */
-#define RS_SC 320  /* staged source bytes per row */
-
-__global__ __launch_bounds__(256) void k_resize(const uint8_t* __restrict__ frames, size_t fstride,
-                                                size_t rstride, uint8_t* __restrict__ pyr,
-                                                size_t pstride, const LevelInfo* __restrict__ lv,
-                                                int l, const int32_t* __restrict__ xofs,
-                                                const int32_t* __restrict__ xofs1,
-                                                const int16_t* __restrict__ alpha,
-                                                const int32_t* __restrict__ yofs,
-                                                const int16_t* __restrict__ beta) {
-  __shared__ uint32_t ssrc[RS_SR][RS_SC / 4];
-  const LevelInfo D = lv[l];
-  const int u = D.src_level;
-  const LevelInfo S = lv[u];
-  const int f = blockIdx.z, tid = threadIdx.x;
-  int spitch;
-  const uint8_t* src = level_base(frames, fstride, rstride, pyr, pstride, S, u, f, &spitch);
-  uint8_t* dst = pyr + (size_t)f * pstride + D.pyr_off;
-  const int x0 = blockIdx.x * RS_TW, y0 = blockIdx.y * RS_TH;
-  const int xl = min(x0 + RS_TW, D.w) - 1, yl = min(y0 + RS_TH, D.h) - 1;
-  const int r_lo = min(max(yofs[D.lut_y + y0], 0), S.h - 1);
-  const int r_hi = min(max(yofs[D.lut_y + yl] + 1, 0), S.h - 1);
-  const bool aligned = ((reinterpret_cast<uintptr_t>(src) | (uintptr_t)spitch) & 3) == 0;
-  const int c_lo = aligned ? (xofs[D.lut_x + x0] & ~3) : xofs[D.lut_x + x0];
-  const int c_hi = xofs1[D.lut_x + xl];
-  const int nr = r_hi - r_lo + 1, nc = c_hi - c_lo + 1;
-  const bool staged = nr <= RS_SR && nc <= RS_SC;
-  if (staged) {
-    uint8_t* s8 = reinterpret_cast<uint8_t*>(ssrc);
-    if (aligned) {
-      const int nd = (nc + 3) >> 2;
-      for (int i = tid; i < nr * nd; i += 256) {
-        const int r = i / nd, c = i - r * nd;
-        const int gc = c_lo + 4 * c;
-        const uint8_t* p = src + (size_t)(r_lo + r) * spitch + gc;
-        ssrc[r][c] = (gc + 3 < S.w) ? *reinterpret_cast<const uint32_t*>(p)
-                                    : (uint32_t)p[0] | ((gc + 1 < S.w ? (uint32_t)p[1] : 0u) << 8) |
-                                          ((gc + 2 < S.w ? (uint32_t)p[2] : 0u) << 16);
+__global__ __launch_bounds__(256) void k_pyramid(const uint8_t* __restrict__ frames, size_t fstride,
+                                                 size_t rstride, uint8_t* __restrict__ pyr,
+                                                 size_t pstride, const PyrSeg S,
+                                                 const int4* __restrict__ xs,
+                                                 const int4* __restrict__ ys,
+                                                 const uint4* __restrict__ blob,
+                                                 const int* __restrict__ bo) {
+  extern __shared__ __align__(16) uint8_t plds[];
+  const int tid = threadIdx.x;
+  const int tx = blockIdx.x % S.ntx, ty = blockIdx.x / S.ntx, f = blockIdx.y;
+  uint8_t* cur = plds;
+  uint8_t* nxt = plds + S.lds_a;
+  uint2* xl = reinterpret_cast<uint2*>(plds + S.lds_a + S.lds_b);
+  uint2* yl = reinterpret_cast<uint2*>(plds + S.lds_a + S.lds_b + S.lds_xl);
+  // ---- LUT blobs of this tile column / row -> LDS ----
+  {
+    const int x0 = bo[S.xbo_off + tx], nx = (bo[S.xbo_off + tx + 1] - x0) >> 1;
+    const int y0 = bo[S.ybo_off + ty], ny = (bo[S.ybo_off + ty + 1] - y0) >> 1;
+    const uint4* xb = blob + (x0 >> 1);
+    const uint4* yb = blob + (y0 >> 1);
+    for (int i = tid; i < nx + ny; i += 256) {
+      if (i < nx) reinterpret_cast<uint4*>(xl)[i] = xb[i];
+      else reinterpret_cast<uint4*>(yl)[i - nx] = yb[i - nx];
+    }
+  }
+  // ---- stage the source region (level lev[0]) ----
+  int4 X = xs[S.xs_off + tx], Y = ys[S.ys_off + ty];
+  int cay = Y.x, cax = X.x & ~15;
+  int cpitch = ((X.y + 15) & ~15) - cax;
+  {
+    const uint8_t* src;
+    size_t sp;
+    if (S.off[0] < 0) {
+      src = frames + (size_t)f * fstride;
+      sp = rstride;
+    } else {
+      src = pyr + (size_t)f * pstride + S.off[0];
+      sp = (size_t)S.pitch[0];
+    }
+    const int nr = Y.y - Y.x;
+    const uintptr_t al = reinterpret_cast<uintptr_t>(src) | (uintptr_t)sp;
+    if ((al & 15) == 0) {
+      const int nq = cpitch >> 4;
+      for (int i = tid; i < nq * nr; i += 256) {
+        const int r = i / nq, q = i - r * nq;
+        const uint4 v = *reinterpret_cast<const uint4*>(src + (size_t)(cay + r) * sp + cax + 16 * q);
+        *reinterpret_cast<uint4*>(cur + r * cpitch + 16 * q) = v;
+      }
+    } else if ((al & 3) == 0) {
+      const int d0 = (X.x & ~3) - cax, nd = (((X.y + 3) & ~3) - (X.x & ~3)) >> 2;
+      for (int i = tid; i < nd * nr; i += 256) {
+        const int r = i / nd, q = i - r * nd;
+        const uint32_t v =
+            *reinterpret_cast<const uint32_t*>(src + (size_t)(cay + r) * sp + cax + d0 + 4 * q);
+        *reinterpret_cast<uint32_t*>(cur + r * cpitch + d0 + 4 * q) = v;
       }
     } else {
-      for (int i = tid; i < nr * nc; i += 256) {
+      const int nc = X.y - X.x;
+      for (int i = tid; i < nc * nr; i += 256) {
         const int r = i / nc, c = i - r * nc;
-        s8[r * RS_SC + c] = src[(size_t)(r_lo + r) * spitch + c_lo + c];
+        cur[r * cpitch + X.x - cax + c] = src[(size_t)(cay + r) * sp + X.x + c];
       }
     }
   }
   __syncthreads();
-  const int tx = tid & 31, ty = tid >> 5;
-  const int xb = x0 + 4 * tx;
-  if (xb >= D.w) return;
-  int sx[4], sx1[4], a0[4], a1[4];
+  // ---- levels 1..nl ----
+  int xo = 0, yo = 0;  // this level's entries in the LUT blobs
+  for (int s = 1; s <= S.nl; ++s) {
+    X = xs[S.xs_off + s * S.ntx + tx];
+    Y = ys[S.ys_off + s * S.nty + ty];
+    const int dax = X.x & ~3;
+    const int ncg = X.y > X.x ? (X.y - dax + 3) >> 2 : 0;
+    const int nrows = max(Y.y - Y.x, 0);
+    const int dpitch = 4 * ncg;
+    if (ncg > 0 && nrows > 0) {
+      const int R = 256 / ncg;
+      if (tid < R * ncg) {
+        const int cg = tid % ncg, r0 = tid / ncg;
+        int sx[4], sx1[4], a0[4], a1[4];
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const int j = D.lut_x + min(xb + k, D.w - 1);
-    sx[k] = xofs[j];
-    sx1[k] = xofs1[j];
-    a0[k] = alpha[2 * j];
-    a1[k] = alpha[2 * j + 1];
-  }
-  const uint8_t* s8 = reinterpret_cast<const uint8_t*>(ssrc);
+        for (int k = 0; k < 4; ++k) {
+          const uint2 e = xl[xo + 4 * cg + k];
+          sx[k] = e.x & 0xFFFF;
+          sx1[k] = e.x >> 16;
+          a0[k] = (int)(int16_t)(e.y & 0xFFFF);
+          a1[k] = (int)e.y >> 16;
+        }
+        const int gx0 = dax + 4 * cg;
+        const bool in_x = gx0 >= X.z && gx0 + 4 <= X.w;
+        const bool any_x = gx0 + 4 > X.z && gx0 < X.w;
+        uint8_t* gdst = pyr + (size_t)f * pstride + S.off[s];
+        const int gp = S.pitch[s];
+        for (int r = r0; r < nrows; r += R) {
+          const int y = Y.x + r;
+          const uint2 e = yl[yo + r];
+          const int b0 = (int)(int16_t)(e.y & 0xFFFF), b1 = (int)e.y >> 16;
+          const uint8_t* R0 = cur + (int)(e.x & 0xFFFF) * cpitch;
+          const uint8_t* R1 = cur + (int)(e.x >> 16) * cpitch;
+          uint32_t packed = 0;
 #pragma unroll
-  for (int rr = 0; rr < 2; ++rr) {
-    const int y = y0 + 2 * ty + rr;
-    if (y >= D.h) break;
-    const int sy = yofs[D.lut_y + y];
-    const int r0 = min(max(sy, 0), S.h - 1), r1 = min(max(sy + 1, 0), S.h - 1);
-    const int b0 = beta[2 * (D.lut_y + y)], b1 = beta[2 * (D.lut_y + y) + 1];
-    uint32_t packed = 0;
+          for (int k = 0; k < 4; ++k) {
+            const int d0 = R0[sx[k]] * a0[k] + R0[sx1[k]] * a1[k];
+            const int d1 = R1[sx[k]] * a0[k] + R1[sx1[k]] * a1[k];
+            const int v = (((b0 * (d0 >> 4)) >> 16) + ((b1 * (d1 >> 4)) >> 16) + 2) >> 2;
+            packed |= (uint32_t)(v & 0xFF) << (8 * k);
+          }
+          *reinterpret_cast<uint32_t*>(nxt + r * dpitch + 4 * cg) = packed;
+          if (y >= Y.z && y < Y.w && any_x) {
+            uint8_t* o = gdst + (size_t)y * gp + gx0;
+            if (in_x) {
+              *reinterpret_cast<uint32_t*>(o) = packed;  // pyr offsets/pitches are 16-B multiples
+            } else {
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      int p00, p01, p10, p11;
-      if (staged) {
-        const uint8_t* R0 = s8 + (r0 - r_lo) * RS_SC - c_lo;
-        const uint8_t* R1 = s8 + (r1 - r_lo) * RS_SC - c_lo;
-        p00 = R0[sx[k]]; p01 = R0[sx1[k]]; p10 = R1[sx[k]]; p11 = R1[sx1[k]];
-      } else {
-        const uint8_t* R0 = src + (size_t)r0 * spitch;
-        const uint8_t* R1 = src + (size_t)r1 * spitch;
-        p00 = R0[sx[k]]; p01 = R0[sx1[k]]; p10 = R1[sx[k]]; p11 = R1[sx1[k]];
+              for (int k = 0; k < 4; ++k)
+                if (gx0 + k >= X.z && gx0 + k < X.w) o[k] = (uint8_t)(packed >> (8 * k));
+            }
+          }
+        }
       }
-      const int d0 = p00 * a0[k] + p01 * a1[k];
-      const int d1 = p10 * a0[k] + p11 * a1[k];
-      const int v = (((b0 * (d0 >> 4)) >> 16) + ((b1 * (d1 >> 4)) >> 16) + 2) >> 2;
-      packed |= (uint32_t)(v & 0xFF) << (8 * k);
     }
-    uint8_t* out = dst + (size_t)y * D.pitch + xb;
-    if (xb + 3 < D.w) {
-      *reinterpret_cast<uint32_t*>(out) = packed;  // pitch and offsets are 16-B multiples
-    } else {
-      for (int k = 0; xb + k < D.w; ++k) out[k] = (uint8_t)(packed >> (8 * k));
-    }
+    __syncthreads();
+    uint8_t* t = cur;
+    cur = nxt;
+    nxt = t;
+    cax = dax;
+    cay = Y.x;
+    cpitch = dpitch;
+    xo += dpitch;
+    yo += nrows;
   }
 }
 
@@ -212,28 +251,43 @@ __device__ __forceinline__ int nms_keep(const uint8_t* amap, int bw, int bh, int
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ int tbyte(const uint32_t* dw, int i) { return (dw[i >> 2] >> ((i & 3) * 8)) & 0xFF; }
 
+__device__ __forceinline__ bool nms_keep_tile(const uint8_t* amap, int tpitch, int r, int c, int a,
+                                              int th, int bh, int cb0, int cb1) {
+  bool keep = true;
+#pragma unroll
+  for (int dy = -1; dy <= 1; ++dy)
+#pragma unroll
+    for (int dx = -1; dx <= 1; ++dx) {
+      if (!dx && !dy) continue;
+      const int rr = r + dy, cc = c + dx;
+      int nb = 0;
+      if (rr >= 3 && rr < 3 + bh && cc >= cb0 && cc < cb1) {
+        const int aq = amap[rr * tpitch + cc];
+        nb = aq > th ? aq - 1 : 0;
+      }
+      keep = keep && (a - 1 > nb);
+    }
+  return keep;
+}
+
 __global__ __launch_bounds__(256) void k_fast_strips(
     const uint8_t* __restrict__ frames, size_t fstride, size_t rstride,
     const uint8_t* __restrict__ pyr, size_t pstride, const LevelInfo* __restrict__ lv,
     const CellInfo* __restrict__ cells, const StripInfo* __restrict__ strips,
     uint32_t* __restrict__ slots, size_t slot_stride, uint32_t* __restrict__ ccount, int ncells,
-    int ini_th, int min_th, int tpitch, int tmax_h, int qcap, int mcells) {
+    int ini_th, int min_th, int tpitch, int tmax_h, int mcells) {
   extern __shared__ __align__(16) uint32_t sm[];
   uint8_t* tile = reinterpret_cast<uint8_t*>(sm);                    // tpitch * tmax_h
   uint8_t* amap = tile + tpitch * tmax_h;                             // tpitch * tmax_h
-  uint16_t* queue = reinterpret_cast<uint16_t*>(amap + tpitch * tmax_h);  // qcap
-  unsigned long long* mask = reinterpret_cast<unsigned long long*>(
-      (reinterpret_cast<uintptr_t>(queue + qcap) + 7) & ~(uintptr_t)7);  // mcells * (tmax_h-6)
-  int* cnt = reinterpret_cast<int*>(mask + mcells * (tmax_h - 6));      // mcells
-  __shared__ int s_q;
-  const int tid = threadIdx.x, lane = tid & 63;
+  unsigned long long* mask = reinterpret_cast<unsigned long long*>(amap + tpitch * tmax_h);
+  int* cnt = reinterpret_cast<int*>(mask + mcells * (tmax_h - 6));   // mcells
+  __shared__ uint16_t wlist[4][256];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const StripInfo st = strips[blockIdx.x];
   const int f = blockIdx.y;
   int pitch;
   const uint8_t* base = level_base(frames, fstride, rstride, pyr, pstride, lv[st.level], st.level, f, &pitch);
   const int bh = st.h - 6;
-  // LDS tile column 0 = global column xal (dword aligned when the rows are)
-  const uintptr_t rowaddr = reinterpret_cast<uintptr_t>(base) + (size_t)st.y * pitch + st.x;
   const bool aligned = ((reinterpret_cast<uintptr_t>(base) | (uintptr_t)pitch) & 3) == 0;
   const int xal = aligned ? (st.x & ~3) : st.x;
   const int lead = st.x - xal;          // tile col of global st.x
@@ -251,21 +305,21 @@ __global__ __launch_bounds__(256) void k_fast_strips(
       tile[r * tpitch + c] = base[(size_t)(st.y + r) * pitch + xal + c];
     }
   }
-  (void)rowaddr;
-  for (int i = tid; i < (tpitch >> 2) * st.h; i += 256) reinterpret_cast<uint32_t*>(amap)[i] = 0u;
   for (int i = tid; i < st.ncells * bh; i += 256) mask[i] = 0ull;
   if (tid < st.ncells) cnt[tid] = 0;
-  if (tid == 0) s_q = 0;
   __syncthreads();
   // band columns [c0, c1) in tile coordinates, rows [3, 3+bh)
   const CellInfo lastc = cells[st.cell_begin + st.ncells - 1];
   const int c0 = lead + 3, c1 = lead + (lastc.x + lastc.w - st.x) - 3;
   const int t_lo = min(ini_th, min_th);
-  // pass 1: cardinal-point pre-test on groups of 4 pixels (tile cols 4g..4g+3)
+  // pass 1 (per wave, no block barrier): cardinal-point pre-test on groups of
+  // 4 pixels (tile cols 4g..4g+3), zero-fill of the strength map, then the
+  // wave's own candidates get the full FAST strength.
   const int g0 = c0 >> 2, g1 = (c1 + 3) >> 2, ng = g1 - g0;
   const int ntask = ng * bh;
-  for (int it0 = 0; it0 < ntask; it0 += 256) {  // wave-uniform trip count (shuffles below)
-    const int it = it0 + tid;
+  uint16_t* wl = wlist[wave];
+  for (int it0 = wave * 64; it0 < ntask; it0 += 256) {  // wave-uniform trip count
+    const int it = it0 + lane;
     const int r = 3 + it / ng, g = g0 + it % ng;
     int flags = 0;
     if (it < ntask) {
@@ -288,8 +342,8 @@ __global__ __launch_bounds__(256) void k_fast_strips(
         const bool dk = (I0 < lo || I8 < lo) && (I4 < lo || I12 < lo);
         if ((br || dk) && c >= c0 && c < c1) flags |= 1 << j;
       }
+      reinterpret_cast<uint32_t*>(amap + r * tpitch)[g] = 0u;
     }
-    // wave-aggregated queue push
     const int n = __popc(flags);
     int incl = n;
 #pragma unroll
@@ -298,80 +352,61 @@ __global__ __launch_bounds__(256) void k_fast_strips(
       if (lane >= d) incl += t;
     }
     const int tot = __shfl(incl, 63, 64);
-    int wbase = 0;
-    if (lane == 63 && tot > 0) wbase = atomicAdd(&s_q, tot);
-    wbase = __shfl(wbase, 63, 64);
-    int pos = wbase + incl - n;
+    int pos = incl - n;
 #pragma unroll
     for (int j = 0; j < 4; ++j)
-      if (flags & (1 << j)) {
-        if (pos < qcap) queue[pos] = (uint16_t)((r << 9) | (4 * g + j));
-        ++pos;
-      }
+      if (flags & (1 << j)) wl[pos++] = (uint16_t)((r << 9) | (4 * g + j));
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    for (int q = lane; q < tot; q += 64) {
+      const int e = wl[q];
+      const int rr = e >> 9, cc = e & 511;
+      const int a = fast_strength(tile + rr * tpitch + cc, tpitch);
+      amap[rr * tpitch + cc] = (uint8_t)(a > t_lo ? a : 0);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   }
   __syncthreads();
-  const int nq = min(s_q, qcap);
-  // pass 2: full strength for queued pixels
-  for (int q = tid; q < nq; q += 256) {
-    const int r = queue[q] >> 9, c = queue[q] & 511;
-    const int a = fast_strength(tile + r * tpitch + c, tpitch);
-    amap[r * tpitch + c] = (uint8_t)(a > t_lo ? a : 0);
-  }
-  __syncthreads();
-  // pass 3: NMS at iniThFAST
+  // pass 2: NMS at iniThFAST over the (sparse) nonzero strength map
   const int wcell = st.wcell;
-  for (int q = tid; q < nq; q += 256) {
-    const int r = queue[q] >> 9, c = queue[q] & 511;
-    const int a = amap[r * tpitch + c];
-    if (a <= ini_th) continue;
-    const int k = min((c - c0) / wcell, st.ncells - 1);
-    const int cb0 = c0 + k * wcell, cb1 = (k == st.ncells - 1) ? c1 : cb0 + wcell;
-    bool keep = true;
+  for (int it = tid; it < ntask; it += 256) {
+    const int r = 3 + it / ng, g = g0 + it % ng;
+    const uint32_t w4 = reinterpret_cast<const uint32_t*>(amap + r * tpitch)[g];
+    if (!w4) continue;
 #pragma unroll
-    for (int dy = -1; dy <= 1; ++dy)
-#pragma unroll
-      for (int dx = -1; dx <= 1; ++dx) {
-        if (!dx && !dy) continue;
-        const int rr = r + dy, cc = c + dx;
-        int nb = 0;
-        if (rr >= 3 && rr < 3 + bh && cc >= cb0 && cc < cb1) {
-          const int aq = amap[rr * tpitch + cc];
-          nb = aq > ini_th ? aq - 1 : 0;
-        }
-        keep = keep && (a - 1 > nb);
+    for (int j = 0; j < 4; ++j) {
+      const int a = (w4 >> (8 * j)) & 0xFF, c = 4 * g + j;
+      if (a <= ini_th || c < c0 || c >= c1) continue;
+      const int k = min((c - c0) / wcell, st.ncells - 1);
+      const int cb0 = c0 + k * wcell, cb1 = (k == st.ncells - 1) ? c1 : cb0 + wcell;
+      if (nms_keep_tile(amap, tpitch, r, c, a, ini_th, bh, cb0, cb1)) {
+        atomicOr(&mask[k * bh + (r - 3)], 1ull << (c - cb0));
+        atomicAdd(&cnt[k], 1);
       }
-    if (keep) {
-      atomicOr(&mask[k * bh + (r - 3)], 1ull << (c - cb0));
-      atomicAdd(&cnt[k], 1);
     }
   }
   __syncthreads();
-  // pass 4: cells without a corner at iniThFAST retry at minThFAST (:293-296)
-  for (int q = tid; q < nq; q += 256) {
-    const int r = queue[q] >> 9, c = queue[q] & 511;
-    const int k = min((c - c0) / wcell, st.ncells - 1);
-    if (cnt[k] != 0) continue;
-    const int a = amap[r * tpitch + c];
-    if (a <= min_th) continue;
-    const int cb0 = c0 + k * wcell, cb1 = (k == st.ncells - 1) ? c1 : cb0 + wcell;
-    bool keep = true;
+  // pass 3: cells without a corner at iniThFAST retry at minThFAST (:293-296)
+  for (int it = tid; it < ntask; it += 256) {
+    const int r = 3 + it / ng, g = g0 + it % ng;
+    const uint32_t w4 = reinterpret_cast<const uint32_t*>(amap + r * tpitch)[g];
+    if (!w4) continue;
 #pragma unroll
-    for (int dy = -1; dy <= 1; ++dy)
-#pragma unroll
-      for (int dx = -1; dx <= 1; ++dx) {
-        if (!dx && !dy) continue;
-        const int rr = r + dy, cc = c + dx;
-        int nb = 0;
-        if (rr >= 3 && rr < 3 + bh && cc >= cb0 && cc < cb1) {
-          const int aq = amap[rr * tpitch + cc];
-          nb = aq > min_th ? aq - 1 : 0;
-        }
-        keep = keep && (a - 1 > nb);
-      }
-    if (keep) atomicOr(&mask[k * bh + (r - 3)], 1ull << (c - cb0));
+    for (int j = 0; j < 4; ++j) {
+      const int a = (w4 >> (8 * j)) & 0xFF, c = 4 * g + j;
+      if (a <= min_th || c < c0 || c >= c1) continue;
+      const int k = min((c - c0) / wcell, st.ncells - 1);
+      if (cnt[k] != 0) continue;
+      const int cb0 = c0 + k * wcell, cb1 = (k == st.ncells - 1) ? c1 : cb0 + wcell;
+      if (nms_keep_tile(amap, tpitch, r, c, a, min_th, bh, cb0, cb1))
+        atomicOr(&mask[k * bh + (r - 3)], 1ull << (c - cb0));
+    }
   }
   __syncthreads();
-  // pass 5: raster-order output per cell
+  // pass 4: raster-order output per cell
   uint32_t* fslots = slots + (size_t)f * slot_stride;
   for (int i = tid; i < st.ncells * bh; i += 256) {
     const int k = i / bh, br = i - k * bh;
@@ -389,10 +424,7 @@ __global__ __launch_bounds__(256) void k_fast_strips(
       fslots[ci.slot_off + off++] =
           orbx_pack_key((uint32_t)gx, (uint32_t)gy, (uint32_t)amap[(3 + br) * tpitch + c] - 1u);
     }
-    if (br == bh - 1) {
-      int total = off;
-      ccount[(size_t)f * ncells + st.cell_begin + k] = (uint32_t)total;
-    }
+    if (br == bh - 1) ccount[(size_t)f * ncells + st.cell_begin + k] = (uint32_t)off;
   }
 }
 
@@ -681,40 +713,43 @@ __device__ __forceinline__ void brief_sincos(float x, float* s, float* c) {
 
 __global__ __launch_bounds__(256) void k_orient_brief(
     const uint8_t* __restrict__ frames, size_t fstride, size_t rstride,
-    const uint8_t* __restrict__ pyr, size_t pstride, const LevelInfo* __restrict__ lv, int nlevels,
+    const uint8_t* __restrict__ pyr, size_t pstride, const BriefArgs A,
     const uint32_t* __restrict__ qout, size_t qout_stride, const int* __restrict__ lcount,
     const int16_t* __restrict__ disk, int ndisk, orbx_keypoint* __restrict__ kps,
-    uint8_t* __restrict__ desc, int* __restrict__ counts, int kcap) {
+    uint8_t* __restrict__ desc, int* __restrict__ counts) {
   __shared__ uint32_t patch[4][KP_ROWS][KP_COLS / 4];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int f = blockIdx.y;
   const int g = blockIdx.x * 4 + wave;
-  const int* lc = lcount + (size_t)f * nlevels;
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
-    int t = 0;
-    for (int l = 0; l < nlevels; ++l) t += lc[l];
-    counts[f] = t;
+  const int nlevels = A.nlevels, kcap = A.kcap;
+  // per-level counts of this frame: one vector load + wave prefix
+  const int lcv = lane < nlevels ? lcount[(size_t)f * nlevels + lane] : 0;
+  int incl = lcv;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int t = __shfl_up(incl, d, 64);
+    if (lane >= d) incl += t;
   }
+  const int total = __shfl(incl, 63, 64);  // all lanes active here
+  if (blockIdx.x == 0 && threadIdx.x == 0) counts[f] = total;
   if (g >= kcap) return;
   int l = 0;
-  while (l < nlevels && !(g >= lv[l].kout_off && g < lv[l].kout_off + lv[l].kcap)) ++l;
+  while (l < nlevels && !(g >= A.kout_off[l] && g < A.kout_off[l] + A.lcap[l])) ++l;
   if (l >= nlevels) return;
-  const LevelInfo L = lv[l];
-  const int i = g - L.kout_off;
-  if (i >= lc[l]) return;
-  int o = i;
-  for (int t = 0; t < l; ++t) o += lc[t];
-  const uint32_t key = qout[(size_t)f * qout_stride + L.kout_off + i];
+  const int i = g - A.kout_off[l];
+  if (i >= __shfl(lcv, l, 64)) return;
+  const int o = i + __shfl(incl - lcv, l, 64);
+  const uint32_t key = qout[(size_t)f * qout_stride + A.kout_off[l] + i];
   const int x = (int)(key >> 20) + ORBX_MINB, y = (int)((key >> 8) & 0xFFF) + ORBX_MINB;
   const int score = (int)(key & 0xFF);
-  const int u = L.unique;
-  const LevelInfo U = lv[u];
-  int pitch;
-  const uint8_t* img = level_base(frames, fstride, rstride, pyr, pstride, U, u, f, &pitch);
+  const int u = A.unique[l];
+  const int pitch = u == 0 ? (int)rstride : A.pitch[u];
+  const uint8_t* img = u == 0 ? frames + (size_t)f * fstride : pyr + (size_t)f * pstride + A.pyr_off[u];
+  const int UW = A.w[u], UH = A.h[u];
   // stage the patch (unblurred level), reflect-101 outside the image
   const int px0 = (x - KP_R) & ~3, py0 = y - KP_R;
   uint32_t(*P)[KP_COLS / 4] = patch[wave];
-  const bool inside = px0 >= 0 && px0 + KP_COLS <= U.w && py0 >= 0 && py0 + KP_ROWS <= U.h &&
+  const bool inside = px0 >= 0 && px0 + KP_COLS <= UW && py0 >= 0 && py0 + KP_ROWS <= UH &&
                       ((reinterpret_cast<uintptr_t>(img) | (uintptr_t)pitch) & 3) == 0;
   if (inside) {
     for (int q = lane; q < KP_ROWS * (KP_COLS / 4); q += 64) {
@@ -725,8 +760,8 @@ __global__ __launch_bounds__(256) void k_orient_brief(
     uint8_t* P8 = reinterpret_cast<uint8_t*>(P);
     for (int q = lane; q < KP_ROWS * KP_COLS; q += 64) {
       const int r = q / KP_COLS, c = q - r * KP_COLS;
-      const int gy = reflect101(min(max(py0 + r, -3), U.h + 2), U.h);
-      const int gx = reflect101(min(max(px0 + c, -3), U.w + 2), U.w);
+      const int gy = reflect101(min(max(py0 + r, -3), UH + 2), UH);
+      const int gx = reflect101(min(max(px0 + c, -3), UW + 2), UW);
       P8[q] = img[(size_t)gy * pitch + gx];
     }
   }
@@ -790,10 +825,10 @@ __global__ __launch_bounds__(256) void k_orient_brief(
     kp.x = (float)x;
     kp.y = (float)y;
     if (l != 0) {
-      kp.x *= L.scale;
-      kp.y *= L.scale;
+      kp.x *= A.scale[l];
+      kp.y *= A.scale[l];
     }
-    kp.size = (float)L.patch_size;
+    kp.size = (float)A.patch[l];
     kp.angle = angle;
     kp.response = (float)score;
     kp.octave = l;

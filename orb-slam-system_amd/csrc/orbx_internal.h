@@ -75,6 +75,41 @@ struct StripInfo {
   int wcell;
 };
 
+/* per-level constants of k_orient_brief, passed by value (kernel arguments
+ * live in SGPRs: no dependent global loads to find a keypoint's level) */
+struct BriefArgs {
+  int nlevels, kcap;
+  int kout_off[ORBX_MAX_LEVELS], lcap[ORBX_MAX_LEVELS];
+  int unique[ORBX_MAX_LEVELS], w[ORBX_MAX_LEVELS], h[ORBX_MAX_LEVELS], pitch[ORBX_MAX_LEVELS];
+  long long pyr_off[ORBX_MAX_LEVELS];
+  float scale[ORBX_MAX_LEVELS];
+  int patch[ORBX_MAX_LEVELS];
+};
+
+/* fused pyramid segment: destination levels lev[1..nl] computed in one
+ * launch from source level lev[0] (read from HBM).  Workgroup = one tile of
+ * the last level; per tile and level s the region tables hold
+ * {clo, chi, plo, phi}: the computed interval (everything level s+1 of this
+ * tile reads) and the owned interval (written to HBM; the owned intervals of
+ * a level partition it).  Row and column tables are separate (ys / xs). */
+#define ORBX_PYR_LDS_BUDGET 40960 /* level buffers */
+#define ORBX_PYR_LDS_MAX 61440    /* + LUT blobs (below the 64 KiB default limit) */
+/* per tile column (row) a LUT blob of uint2 {src0 | src1 << 16, coef pair}
+ * for every level s = 1..nl and every computed column c in [dax, dax+4*ncg)
+ * (row in [clo, chi)), source positions relative to the LDS origin of level
+ * s-1's region; blobs are padded to 16 B */
+struct PyrSeg {
+  int nl;
+  int ntx, nty;
+  int xs_off, ys_off; /* in quads; table index (s * ntx + tx) / (s * nty + ty) */
+  int lds_a, lds_b;   /* ping-pong buffer bytes (source staged in A) */
+  int lds_xl, lds_yl; /* LUT blob bytes (max over tile columns / rows) */
+  int xbo_off, ybo_off; /* into the blob offset tables (ntx+1 / nty+1 entries) */
+  int lev[ORBX_MAX_LEVELS], w[ORBX_MAX_LEVELS], h[ORBX_MAX_LEVELS], pitch[ORBX_MAX_LEVELS];
+  int lut_x[ORBX_MAX_LEVELS], lut_y[ORBX_MAX_LEVELS];
+  long long off[ORBX_MAX_LEVELS]; /* pyr offset; -1 = the caller's frame (level 0) */
+};
+
 #if defined(__HIPCC__)
 #define ORBX_HDI __host__ __device__ inline
 #else

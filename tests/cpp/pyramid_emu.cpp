@@ -1,0 +1,123 @@
+// CPU emulation of k_pyramid's tiling (kernels_extract.hip) on the host
+// planner's tables (geometry.cpp): every tile of every segment is computed
+// from its LDS regions only, exactly as the kernel indexes them, with
+// out-of-region reads trapped.  Writes the unique levels to argv[7] for the
+// oracle comparison in tests/test_host.py.
+// usage: pyramid_emu in.raw W H nfeatures nlevels scale out.bin
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <vector>
+
+#include "geometry.h"
+
+using namespace orbx;
+
+static int fail(const char* m, int a, int b) {
+  fprintf(stderr, "FAIL %s %d %d\n", m, a, b);
+  exit(2);
+}
+
+int main(int argc, char** argv) {
+  if (argc < 8) return 1;
+  const int W = atoi(argv[2]), H = atoi(argv[3]);
+  orbx_params prm = {atoi(argv[4]), (float)atof(argv[6]), atoi(argv[5]), 20, 7, 1};
+  std::vector<uint8_t> img((size_t)W * H);
+  FILE* f = fopen(argv[1], "rb");
+  if (!f || fread(img.data(), 1, img.size(), f) != img.size()) return 1;
+  fclose(f);
+  Plan P;
+  int rc = plan_geometry(prm, W, H, P);
+  if (rc) { printf("rc %d\n", rc); return 3; }
+  std::vector<uint8_t> pyr(P.pyr_bytes + 16, 0xCD);
+  std::vector<uint8_t> owner(P.pyr_bytes + 16, 0);
+  for (const PyrSeg& g : P.segs) {
+    if (g.lds_a + g.lds_b + g.lds_xl + g.lds_yl > ORBX_PYR_LDS_MAX) fail("lds total", 0, 0);
+    for (int ty = 0; ty < g.nty; ++ty)
+      for (int tx = 0; tx < g.ntx; ++tx) {
+        const int xb = P.pyr_bo[g.xbo_off + tx], yb = P.pyr_bo[g.ybo_off + ty];
+        if ((P.pyr_bo[g.xbo_off + tx + 1] - xb) * 8 > g.lds_xl) fail("xblob", tx, 0);
+        if ((P.pyr_bo[g.ybo_off + ty + 1] - yb) * 8 > g.lds_yl) fail("yblob", ty, 0);
+        if ((xb | yb) & 1) fail("blob align", xb, yb);
+        int xo = 0, yo = 0;
+        // staged source region (only [clo,chi) x rows valid; other bytes poisoned)
+        const int* X = &P.pyr_xs[4 * (g.xs_off + tx)];
+        const int* Y = &P.pyr_ys[4 * (g.ys_off + ty)];
+        int cax = X[0] & ~15, cay = Y[0], cpitch = ((X[1] + 15) & ~15) - cax;
+        int cx0 = X[0], cx1 = X[1], cy0 = Y[0], cy1 = Y[1];
+        if ((long long)cpitch * (cy1 - cy0) > g.lds_a) fail("lds_a", tx, ty);
+        std::vector<int> cur((size_t)cpitch * (cy1 - cy0), -1);
+        for (int r = cy0; r < cy1; ++r)
+          for (int c = cx0; c < cx1; ++c) {
+            int v = g.off[0] < 0 ? img[(size_t)r * W + c] : pyr[g.off[0] + (size_t)r * g.pitch[0] + c];
+            cur[(size_t)(r - cay) * cpitch + c - cax] = v;
+          }
+        for (int s = 1; s <= g.nl; ++s) {
+          X = &P.pyr_xs[4 * (g.xs_off + s * g.ntx + tx)];
+          Y = &P.pyr_ys[4 * (g.ys_off + s * g.nty + ty)];
+          const int dax = X[0] & ~3, ncg = (X[1] - dax + 3) >> 2, nrows = Y[1] - Y[0];
+          const int dpitch = 4 * ncg;
+          if ((long long)dpitch * nrows > ((s & 1) ? g.lds_b : g.lds_a)) fail("lds", s, tx);
+          if (ncg > 256) fail("ncg", ncg, s);
+          std::vector<int> nxt((size_t)std::max(dpitch * nrows, 1), -1);
+          const LevelInfo& lv = P.levels[g.lev[s]];
+          for (int r = 0; r < nrows; ++r) {
+            const int y = Y[0] + r;
+            const uint32_t* ye = &P.pyr_blob[2 * (yb + yo + r)];
+            const int ry0 = ye[0] & 0xFFFF, ry1 = ye[0] >> 16;
+            const int b0 = (int16_t)(ye[1] & 0xFFFF), b1 = (int16_t)(ye[1] >> 16);
+            {  // blob vs the LUTs it packs
+              const int sy = P.yofs[g.lut_y[s] + y], shm1 = g.h[s - 1] - 1;
+              if (ry0 != std::min(std::max(sy, 0), shm1) - cay || ry1 != std::min(std::max(sy + 1, 0), shm1) - cay ||
+                  b0 != P.beta[2 * (g.lut_y[s] + y)] || b1 != P.beta[2 * (g.lut_y[s] + y) + 1])
+                fail("yblob entry", s, y);
+            }
+            for (int c = dax; c < dax + dpitch; ++c) {
+              const uint32_t* xe = &P.pyr_blob[2 * (xb + xo + c - dax)];
+              const int sx = xe[0] & 0xFFFF, sx1 = xe[0] >> 16;
+              const int a0 = (int16_t)(xe[1] & 0xFFFF), a1 = (int16_t)(xe[1] >> 16);
+              auto rd = [&](int rr, int cc) {
+                if (rr < 0 || rr >= cy1 - cay || cc < 0 || cc >= cpitch) fail("oob", rr, cc);
+                int v = cur[(size_t)rr * cpitch + cc];
+                if (v < 0) fail("uninit", rr + cay, cc + cax);
+                return v;
+              };
+              if (c < X[0] || c >= X[1]) continue;  // pad columns: garbage in the kernel
+              const int d0 = rd(ry0, sx) * a0 + rd(ry0, sx1) * a1;
+              const int d1 = rd(ry1, sx) * a0 + rd(ry1, sx1) * a1;
+              const int v = (((b0 * (d0 >> 4)) >> 16) + ((b1 * (d1 >> 4)) >> 16) + 2) >> 2;
+              nxt[(size_t)r * dpitch + c - dax] = v & 0xFF;
+              if (y >= Y[2] && y < Y[3] && c >= X[2] && c < X[3]) {
+                const size_t o = g.off[s] + (size_t)y * g.pitch[s] + c;
+                if (owner[o]) fail("double write", y, c);
+                owner[o] = 1;
+                pyr[o] = (uint8_t)v;
+              }
+            }
+          }
+          (void)lv;
+          xo += dpitch;
+          yo += nrows;
+          cur.swap(nxt);
+          cax = dax; cay = Y[0]; cpitch = dpitch;
+          cx0 = X[0]; cx1 = X[1]; cy0 = Y[0]; cy1 = Y[1];
+        }
+      }
+  }
+  FILE* o = fopen(argv[7], "wb");
+  for (int l = 1; l < prm.nlevels; ++l) {
+    const LevelInfo& lv = P.levels[l];
+    if (lv.unique != l) continue;
+    for (int y = 0; y < lv.h; ++y)
+      for (int x = 0; x < lv.w; ++x)
+        if (!owner[lv.pyr_off + (size_t)y * lv.pitch + x]) fail("unwritten", l, y * 100000 + x);
+    for (int y = 0; y < lv.h; ++y) fwrite(&pyr[lv.pyr_off + (size_t)y * lv.pitch], 1, lv.w, o);
+  }
+  fclose(o);
+  int nt = 0;
+  for (const PyrSeg& g : P.segs) nt += g.ntx * g.nty;
+  printf("segs %zu tiles %d lds %d+%d\n", P.segs.size(), nt, P.segs.empty() ? 0 : P.segs[0].lds_a,
+         P.segs.empty() ? 0 : P.segs[0].lds_b);
+  return 0;
+}
