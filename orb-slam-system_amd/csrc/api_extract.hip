@@ -15,10 +15,10 @@
 
 namespace orbx {
 __global__ void k_pyramid(const uint8_t*, size_t, size_t, uint8_t*, size_t, const PyrSeg,
-                          const int4*, const int4*, const uint4*, const int*);
+                          const int4*, const int4*, const uint4*, const int*, int);
 __global__ void k_fast_strips(const uint8_t*, size_t, size_t, const uint8_t*, size_t,
                               const LevelInfo*, const CellInfo*, const StripInfo*, uint32_t*,
-                              size_t, uint32_t*, int, int, int, int, int, int);
+                              size_t, uint32_t*, int, int, int, int, int, int, int);
 __global__ void k_quadtree(const LevelInfo*, const CellInfo*, const uint32_t*, size_t,
                            const uint32_t*, int, uint32_t*, int32_t*, size_t, uint32_t*, size_t,
                            int*, int, int, int, int*);
@@ -133,6 +133,7 @@ struct orbx_plan {
   size_t qt_lds = 0;
   BriefArgs bargs;
   StageTimer timer;
+  int dbg = 0; /* ORBX_DEBUG_STOP: kernel phase early-exit for profiling only */
 };
 
 static size_t round_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
@@ -171,6 +172,7 @@ extern "C" int orbx_plan_create(const orbx_params* prm, int width, int height, i
   int ndev = orbx_device_count();
   if (device < 0 || device >= ndev) return ORBX_ERR_NO_DEVICE;
   orbx_plan* p = new orbx_plan();
+  if (const char* e = getenv("ORBX_DEBUG_STOP")) p->dbg = atoi(e);
   int rc = plan_geometry(*prm, width, height, p->P);
   if (rc) { delete p; return rc; }
   const Plan& P = p->P;
@@ -207,12 +209,12 @@ extern "C" int orbx_plan_create(const orbx_params* prm, int width, int height, i
   }
   // FAST strip LDS: tile + strength map + row masks + counts
   {
-    p->fs_tpitch = (3 + P.strip_max_w + 8 + 3 + 7) & ~7;
+    p->fs_tpitch = (15 + P.strip_max_w + 8 + 15) & ~15; /* lead <= 15, row reads up to +8 */
     p->fs_tmaxh = std::max(P.strip_max_h, 7);
     p->fs_qcap = 0;
     p->fs_mcells = std::max(P.strip_max_cells, 1);
     p->fs_lds = 2 * (size_t)p->fs_tpitch * p->fs_tmaxh +
-                8 * (size_t)p->fs_mcells * (p->fs_tmaxh - 6) + 4 * (size_t)p->fs_mcells + 16;
+                16 * (size_t)p->fs_mcells * (p->fs_tmaxh - 6) + 4 * (size_t)p->fs_mcells + 16;
     if (p->fs_lds > 150 * 1024) { plan_free(p); return ORBX_ERR_UNSUPPORTED; }
     if (hipFuncSetAttribute((const void*)k_fast_strips, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)p->fs_lds) != hipSuccess) { plan_free(p); return ORBX_ERR_HIP; }
@@ -291,7 +293,7 @@ extern "C" int orbx_plan_extract(orbx_plan* p, const uint8_t* frames, int nframe
                        g.lds_a + g.lds_b + g.lds_xl + g.lds_yl, s, frames, fstride, rstride,
                        p->d_pyr, p->pyr_stride, g, reinterpret_cast<const int4*>(p->d_pyr_xs),
                        reinterpret_cast<const int4*>(p->d_pyr_ys),
-                       reinterpret_cast<const uint4*>(p->d_pyr_blob), p->d_pyr_bo);
+                       reinterpret_cast<const uint4*>(p->d_pyr_blob), p->d_pyr_bo, p->dbg);
   }
   p->timer.end(ORBX_STAGE_RESIZE, s);
   // K2 FAST cells
@@ -300,9 +302,10 @@ extern "C" int orbx_plan_extract(orbx_plan* p, const uint8_t* frames, int nframe
     hipLaunchKernelGGL(k_fast_strips, dim3((unsigned)P.strips.size(), n), dim3(256), p->fs_lds, s,
                        frames, fstride, rstride, p->d_pyr, p->pyr_stride, p->d_lv, p->d_cells,
                        p->d_strips, p->d_slots, p->slot_stride, p->d_ccount, P.ncells, P.ini_th,
-                       P.min_th, p->fs_tpitch, p->fs_tmaxh, p->fs_mcells);
+                       P.min_th, p->fs_tpitch, p->fs_tmaxh, p->fs_mcells, p->dbg);
   }
   p->timer.end(ORBX_STAGE_FAST, s);
+  if (p->dbg) return ORBX_OK; /* phase probe: later stages would read partial results */
   // K3 DistributeOctTree
   p->timer.begin(ORBX_STAGE_QUADTREE, s);
   hipLaunchKernelGGL(k_quadtree, dim3(L, n), dim3(256), p->qt_lds, s, p->d_lv, p->d_cells,

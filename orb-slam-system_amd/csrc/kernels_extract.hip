@@ -37,6 +37,36 @@ __device__ __forceinline__ const uint8_t* level_base(const uint8_t* frames, size
   return pyr + (size_t)f * pstride + U.pyr_off;
 }
 
+// Block-cooperative copy of a 2-D byte region into LDS with U loads in flight
+// per thread: all loads of a round are issued before the first LDS store,
+// so a workgroup pays one memory latency per round instead of one per load.
+// T = uint4 / uint32_t / uint8_t (src, pitches and offsets aligned to T).
+template <typename T, int U, int NT>
+__device__ __forceinline__ void stage_region(uint8_t* __restrict__ lds, int lpitch,
+                                             const uint8_t* __restrict__ src, size_t sp, int nrows,
+                                             int nper, int tid) {
+  const int total = nrows * nper;
+  for (int i0 = tid; i0 < total; i0 += NT * U) {
+    T v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = i0 + NT * u;
+      if (i < total) {
+        const int r = i / nper, c = i - r * nper;
+        v[u] = reinterpret_cast<const T*>(src + (size_t)r * sp)[c];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = i0 + NT * u;
+      if (i < total) {
+        const int r = i / nper, c = i - r * nper;
+        reinterpret_cast<T*>(lds + r * lpitch)[c] = v[u];
+      }
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------
 // k_pyramid: a chain of unique levels (PyrSeg) with OpenCV's INTER_LINEAR
 // fixed-point arithmetic (resize.cpp HResizeLinear / VResizeLinear<uchar>):
@@ -54,7 +84,7 @@ __global__ __launch_bounds__(256) void k_pyramid(const uint8_t* __restrict__ fra
                                                  const int4* __restrict__ xs,
                                                  const int4* __restrict__ ys,
                                                  const uint4* __restrict__ blob,
-                                                 const int* __restrict__ bo) {
+                                                 const int* __restrict__ bo, int dbg) {
   extern __shared__ __align__(16) uint8_t plds[];
   const int tid = threadIdx.x;
   const int tx = blockIdx.x % S.ntx, ty = blockIdx.x / S.ntx, f = blockIdx.y;
@@ -89,30 +119,18 @@ __global__ __launch_bounds__(256) void k_pyramid(const uint8_t* __restrict__ fra
     }
     const int nr = Y.y - Y.x;
     const uintptr_t al = reinterpret_cast<uintptr_t>(src) | (uintptr_t)sp;
+    const uint8_t* s0 = src + (size_t)cay * sp;
     if ((al & 15) == 0) {
-      const int nq = cpitch >> 4;
-      for (int i = tid; i < nq * nr; i += 256) {
-        const int r = i / nq, q = i - r * nq;
-        const uint4 v = *reinterpret_cast<const uint4*>(src + (size_t)(cay + r) * sp + cax + 16 * q);
-        *reinterpret_cast<uint4*>(cur + r * cpitch + 16 * q) = v;
-      }
+      stage_region<uint4, 4, 256>(cur, cpitch, s0 + cax, sp, nr, cpitch >> 4, tid);
     } else if ((al & 3) == 0) {
       const int d0 = (X.x & ~3) - cax, nd = (((X.y + 3) & ~3) - (X.x & ~3)) >> 2;
-      for (int i = tid; i < nd * nr; i += 256) {
-        const int r = i / nd, q = i - r * nd;
-        const uint32_t v =
-            *reinterpret_cast<const uint32_t*>(src + (size_t)(cay + r) * sp + cax + d0 + 4 * q);
-        *reinterpret_cast<uint32_t*>(cur + r * cpitch + d0 + 4 * q) = v;
-      }
+      stage_region<uint32_t, 8, 256>(cur + d0, cpitch, s0 + cax + d0, sp, nr, nd, tid);
     } else {
-      const int nc = X.y - X.x;
-      for (int i = tid; i < nc * nr; i += 256) {
-        const int r = i / nc, c = i - r * nc;
-        cur[r * cpitch + X.x - cax + c] = src[(size_t)(cay + r) * sp + X.x + c];
-      }
+      stage_region<uint8_t, 16, 256>(cur + (X.x - cax), cpitch, s0 + X.x, sp, nr, X.y - X.x, tid);
     }
   }
   __syncthreads();
+  if (dbg == 11) return;
   // ---- levels 1..nl ----
   int xo = 0, yo = 0;  // this level's entries in the LUT blobs
   for (int s = 1; s <= S.nl; ++s) {
@@ -191,8 +209,9 @@ __global__ __launch_bounds__(256) void k_pyramid(const uint8_t* __restrict__ fra
 // (ORBextractor.cc:293-296,330-331).  Survivors are compacted in raster order
 // into the cell's slot list, packed (x-16)<<20 | (y-16)<<8 | score.
 // ---------------------------------------------------------------------------
-__constant__ int8_t c_circle_dx[16] = {0, 1, 2, 3, 3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1};
-__constant__ int8_t c_circle_dy[16] = {3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1, 0, 1, 2, 3};
+// FAST radius-3 circle (cv::makeOffsets, patternSize 16), as immediates
+__device__ constexpr int8_t c_circle_dx[16] = {0, 1, 2, 3, 3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1};
+__device__ constexpr int8_t c_circle_dy[16] = {3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1, 0, 1, 2, 3};
 
 __device__ __forceinline__ int min3i(int a, int b, int c) { return min(min(a, b), c); }
 __device__ __forceinline__ int max3i(int a, int b, int c) { return max(max(a, b), c); }
@@ -270,149 +289,236 @@ __device__ __forceinline__ bool nms_keep_tile(const uint8_t* amap, int tpitch, i
   return keep;
 }
 
+// 4 cyclically consecutive points of {0,2,..,14} all brighter (darker) than
+// v +- t: necessary for a 9-arc (any 9 contiguous circle points contain 4
+// consecutive even ones), i.e. for A > t.
+__device__ __forceinline__ bool fast_even_test(const uint8_t* t, int tw, int th) {
+  const int v = t[0];
+  const int hi = v + th, lo = v - th;
+  int mb = 0, md = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const int I = t[c_circle_dy[2 * k] * tw + c_circle_dx[2 * k]];
+    mb |= (I > hi) << k;
+    md |= (I < lo) << k;
+  }
+  mb |= mb << 8;
+  md |= md << 8;
+  const int rb = mb & (mb >> 1) & (mb >> 2) & (mb >> 3);
+  const int rd = md & (md >> 1) & (md >> 2) & (md >> 3);
+  return ((rb | rd) & 0xFF) != 0;
+}
+
+__device__ __forceinline__ int wave_excl_scan(int n, int lane, int* total) {
+  int incl = n;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int t = __shfl_up(incl, d, 64);
+    if (lane >= d) incl += t;
+  }
+  *total = __shfl(incl, 63, 64);
+  return incl - n;
+}
+
+__device__ __forceinline__ void wave_sync_lds() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+#define FS_L1CAP 320 /* per-wave cardinal survivors: < 64 carried + <= 256 new */
+#define FS_L2CAP 128 /* per-wave even-test survivors: < 64 carried + <= 64 new */
+
+typedef unsigned short us2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ us2 as_us2(uint32_t x) { return __builtin_bit_cast(us2, x); }
+__device__ __forceinline__ uint32_t as_u32(us2 x) { return __builtin_bit_cast(uint32_t, x); }
+
 __global__ __launch_bounds__(256) void k_fast_strips(
     const uint8_t* __restrict__ frames, size_t fstride, size_t rstride,
     const uint8_t* __restrict__ pyr, size_t pstride, const LevelInfo* __restrict__ lv,
     const CellInfo* __restrict__ cells, const StripInfo* __restrict__ strips,
     uint32_t* __restrict__ slots, size_t slot_stride, uint32_t* __restrict__ ccount, int ncells,
-    int ini_th, int min_th, int tpitch, int tmax_h, int mcells) {
+    int ini_th, int min_th, int tpitch, int tmax_h, int mcells, int dbg) {
   extern __shared__ __align__(16) uint32_t sm[];
   uint8_t* tile = reinterpret_cast<uint8_t*>(sm);                    // tpitch * tmax_h
   uint8_t* amap = tile + tpitch * tmax_h;                             // tpitch * tmax_h
   unsigned long long* mask = reinterpret_cast<unsigned long long*>(amap + tpitch * tmax_h);
-  int* cnt = reinterpret_cast<int*>(mask + mcells * (tmax_h - 6));   // mcells
-  __shared__ uint16_t wlist[4][256];
+  unsigned long long* mask2 = mask + mcells * (tmax_h - 6);
+  int* cnt = reinterpret_cast<int*>(mask2 + mcells * (tmax_h - 6));  // mcells
+  __shared__ uint16_t wlist1[4][FS_L1CAP];
+  __shared__ uint16_t wlist2[4][FS_L2CAP];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const StripInfo st = strips[blockIdx.x];
   const int f = blockIdx.y;
   int pitch;
   const uint8_t* base = level_base(frames, fstride, rstride, pyr, pstride, lv[st.level], st.level, f, &pitch);
   const int bh = st.h - 6;
-  const bool aligned = ((reinterpret_cast<uintptr_t>(base) | (uintptr_t)pitch) & 3) == 0;
-  const int xal = aligned ? (st.x & ~3) : st.x;
+  const uintptr_t alb = reinterpret_cast<uintptr_t>(base) | (uintptr_t)pitch;
+  const bool aligned = (alb & 3) == 0;
+  const bool aligned16 = (alb & 15) == 0;
+  const int xal = aligned16 ? (st.x & ~15) : aligned ? (st.x & ~3) : st.x;
   const int lead = st.x - xal;          // tile col of global st.x
   const int tw = lead + st.w;           // columns in use
-  const int nd = (tw + 3) >> 2;         // dwords per tile row
-  if (aligned) {
-    for (int i = tid; i < nd * st.h; i += 256) {
-      const int r = i / nd, c = i - r * nd;
-      const uint32_t* src = reinterpret_cast<const uint32_t*>(base + (size_t)(st.y + r) * pitch + xal);
-      reinterpret_cast<uint32_t*>(tile + r * tpitch)[c] = src[c];
-    }
-  } else {
-    for (int i = tid; i < tw * st.h; i += 256) {
-      const int r = i / tw, c = i - r * tw;
-      tile[r * tpitch + c] = base[(size_t)(st.y + r) * pitch + xal + c];
-    }
+  {
+    const uint8_t* s0 = base + (size_t)st.y * pitch + xal;
+    if (aligned16) stage_region<uint4, 4, 256>(tile, tpitch, s0, pitch, st.h, (tw + 15) >> 4, tid);
+    else if (aligned) stage_region<uint32_t, 12, 256>(tile, tpitch, s0, pitch, st.h, (tw + 3) >> 2, tid);
+    else stage_region<uint8_t, 16, 256>(tile, tpitch, s0, pitch, st.h, tw, tid);
   }
-  for (int i = tid; i < st.ncells * bh; i += 256) mask[i] = 0ull;
+  for (int i = tid; i < st.ncells * bh; i += 256) mask[i] = mask2[i] = 0ull;
   if (tid < st.ncells) cnt[tid] = 0;
   __syncthreads();
+  if (dbg == 1) return;
   // band columns [c0, c1) in tile coordinates, rows [3, 3+bh)
   const CellInfo lastc = cells[st.cell_begin + st.ncells - 1];
   const int c0 = lead + 3, c1 = lead + (lastc.x + lastc.w - st.x) - 3;
   const int t_lo = min(ini_th, min_th);
-  // pass 1 (per wave, no block barrier): cardinal-point pre-test on groups of
-  // 4 pixels (tile cols 4g..4g+3), zero-fill of the strength map, then the
-  // wave's own candidates get the full FAST strength.
+  // pass 1 (per wave, no block barrier).  Stage A: cardinal pre-test on a
+  // group of 4 pixels (tile cols 4g..4g+3) in packed 16-bit lanes + zero-fill
+  // of the strength map; survivors are appended to list L1.  Stage B: the
+  // even-point test, 64 L1 entries at a time, appends to L2.  Stage C: the
+  // full 16-point strength, 64 L2 entries at a time.  Lists are per wave, so
+  // only wave-level LDS ordering is needed.
   const int g0 = c0 >> 2, g1 = (c1 + 3) >> 2, ng = g1 - g0;
   const int ntask = ng * bh;
-  uint16_t* wl = wlist[wave];
-  for (int it0 = wave * 64; it0 < ntask; it0 += 256) {  // wave-uniform trip count
-    const int it = it0 + lane;
-    const int r = 3 + it / ng, g = g0 + it % ng;
-    int flags = 0;
-    if (it < ntask) {
-      const uint32_t* rowm = reinterpret_cast<const uint32_t*>(tile + (r - 3) * tpitch);
-      const uint32_t* row0 = reinterpret_cast<const uint32_t*>(tile + r * tpitch);
-      const uint32_t* rowp = reinterpret_cast<const uint32_t*>(tile + (r + 3) * tpitch);
-      uint32_t m0[3];
-      m0[0] = g > 0 ? row0[g - 1] : 0u;
-      m0[1] = row0[g];
-      m0[2] = row0[g + 1];
-      const uint32_t up = rowm[g], dn = rowp[g];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int c = 4 * g + j;
-        const int v = tbyte(m0, 4 + j);
-        const int I0 = (dn >> (8 * j)) & 0xFF, I8 = (up >> (8 * j)) & 0xFF;
-        const int I4 = tbyte(m0, 4 + j + 3), I12 = tbyte(m0, 4 + j - 3);
-        const int hi = v + t_lo, lo = v - t_lo;
-        const bool br = (I0 > hi || I8 > hi) && (I4 > hi || I12 > hi);
-        const bool dk = (I0 < lo || I8 < lo) && (I4 < lo || I12 < lo);
-        if ((br || dk) && c >= c0 && c < c1) flags |= 1 << j;
-      }
-      reinterpret_cast<uint32_t*>(amap + r * tpitch)[g] = 0u;
-    }
-    const int n = __popc(flags);
-    int incl = n;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      const int t = __shfl_up(incl, d, 64);
-      if (lane >= d) incl += t;
-    }
-    const int tot = __shfl(incl, 63, 64);
-    int pos = incl - n;
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-      if (flags & (1 << j)) wl[pos++] = (uint16_t)((r << 9) | (4 * g + j));
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    for (int q = lane; q < tot; q += 64) {
-      const int e = wl[q];
+  uint16_t* L1 = wlist1[wave];
+  uint16_t* L2 = wlist2[wave];
+  int n1 = 0, n2 = 0;  // wave-uniform list lengths
+  const unsigned long long lt = (1ull << lane) - 1ull;
+  auto strength_batch = [&](int e, bool act) {
+    if (act) {
       const int rr = e >> 9, cc = e & 511;
       const int a = fast_strength(tile + rr * tpitch + cc, tpitch);
       amap[rr * tpitch + cc] = (uint8_t)(a > t_lo ? a : 0);
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  }
-  __syncthreads();
-  // pass 2: NMS at iniThFAST over the (sparse) nonzero strength map
-  const int wcell = st.wcell;
-  for (int it = tid; it < ntask; it += 256) {
-    const int r = 3 + it / ng, g = g0 + it % ng;
-    const uint32_t w4 = reinterpret_cast<const uint32_t*>(amap + r * tpitch)[g];
-    if (!w4) continue;
+  };
+  auto even_batch = [&](int e, bool act) {
+    const bool keep = act && fast_even_test(tile + (e >> 9) * tpitch + (e & 511), tpitch, t_lo);
+    const unsigned long long bal = __ballot(keep);
+    if (keep) L2[n2 + __popcll(bal & lt)] = (uint16_t)e;
+    n2 += __popcll(bal);
+    if (n2 >= 64) {
+      wave_sync_lds();
+      n2 -= 64;
+      strength_batch(L2[n2 + lane], true);
+      wave_sync_lds();
+    }
+  };
+  {
+    const uint32_t tt = (uint32_t)t_lo * 0x00010001u;
+    const int it_first = wave * 64 + lane;
+    int r = 3 + it_first / ng, g = g0 + it_first % ng;
+    const int dr = 256 / ng, dg = 256 - dr * ng;
+    for (int it0 = wave * 64; it0 < ntask; it0 += 256) {  // wave-uniform trip count
+      const int it = it0 + lane;
+      uint32_t clo = 0, chi = 0;  // candidate words: pixels 0,2 / 1,3 (16-bit lanes)
+      if (it < ntask) {
+        const uint32_t* row0 = reinterpret_cast<const uint32_t*>(tile + r * tpitch);
+        const uint32_t w0 = g > 0 ? row0[g - 1] : 0u, w1 = row0[g], w2 = row0[g + 1];
+        const uint32_t up = reinterpret_cast<const uint32_t*>(tile + (r - 3) * tpitch)[g];
+        const uint32_t dn = reinterpret_cast<const uint32_t*>(tile + (r + 3) * tpitch)[g];
+        const uint32_t I4 = __builtin_amdgcn_alignbyte(w2, w1, 3);   // (x+3, y)
+        const uint32_t I12 = __builtin_amdgcn_alignbyte(w1, w0, 1);  // (x-3, y)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int a = (w4 >> (8 * j)) & 0xFF, c = 4 * g + j;
-      if (a <= ini_th || c < c0 || c >= c1) continue;
-      const int k = min((c - c0) / wcell, st.ncells - 1);
-      const int cb0 = c0 + k * wcell, cb1 = (k == st.ncells - 1) ? c1 : cb0 + wcell;
-      if (nms_keep_tile(amap, tpitch, r, c, a, ini_th, bh, cb0, cb1)) {
-        atomicOr(&mask[k * bh + (r - 3)], 1ull << (c - cb0));
-        atomicAdd(&cnt[k], 1);
+        for (int h = 0; h < 2; ++h) {
+          const uint32_t sel = h ? 0x0c030c01u : 0x0c020c00u;
+          const us2 v = as_us2(__builtin_amdgcn_perm(0u, w1, sel));
+          const us2 a0 = as_us2(__builtin_amdgcn_perm(0u, dn, sel));
+          const us2 a8 = as_us2(__builtin_amdgcn_perm(0u, up, sel));
+          const us2 a4 = as_us2(__builtin_amdgcn_perm(0u, I4, sel));
+          const us2 a12 = as_us2(__builtin_amdgcn_perm(0u, I12, sel));
+          const us2 t2 = as_us2(tt);
+          const us2 mb = __builtin_elementwise_min(__builtin_elementwise_max(a0, a8),
+                                                   __builtin_elementwise_max(a4, a12));
+          const us2 md = __builtin_elementwise_max(__builtin_elementwise_min(a0, a8),
+                                                   __builtin_elementwise_min(a4, a12));
+          const us2 db = __builtin_elementwise_sub_sat(mb, v + t2);       // > 0 iff brighter arc
+          const us2 dd = __builtin_elementwise_sub_sat(__builtin_elementwise_sub_sat(v, md), t2);
+          const uint32_t x = as_u32(db) | as_u32(dd);
+          if (h) chi = x; else clo = x;
+        }
+        reinterpret_cast<uint32_t*>(amap + r * tpitch)[g] = 0u;
       }
-    }
-  }
-  __syncthreads();
-  // pass 3: cells without a corner at iniThFAST retry at minThFAST (:293-296)
-  for (int it = tid; it < ntask; it += 256) {
-    const int r = 3 + it / ng, g = g0 + it % ng;
-    const uint32_t w4 = reinterpret_cast<const uint32_t*>(amap + r * tpitch)[g];
-    if (!w4) continue;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int a = (w4 >> (8 * j)) & 0xFF, c = 4 * g + j;
-      if (a <= min_th || c < c0 || c >= c1) continue;
-      const int k = min((c - c0) / wcell, st.ncells - 1);
-      if (cnt[k] != 0) continue;
-      const int cb0 = c0 + k * wcell, cb1 = (k == st.ncells - 1) ? c1 : cb0 + wcell;
-      if (nms_keep_tile(amap, tpitch, r, c, a, min_th, bh, cb0, cb1))
-        atomicOr(&mask[k * bh + (r - 3)], 1ull << (c - cb0));
+      for (int j = 0; j < 4; ++j) {
+        const int c = 4 * g + j;
+        const uint32_t x = (j & 1) ? chi : clo;
+        const bool k = ((j & 2) ? (x >> 16) : (x & 0xFFFFu)) != 0 && c >= c0 && c < c1;
+        const unsigned long long bal = __ballot(k);
+        if (k) L1[n1 + __popcll(bal & lt)] = (uint16_t)((r << 9) | c);
+        n1 += __popcll(bal);
+      }
+      if (n1 >= 64) {  // wave-uniform
+        wave_sync_lds();
+        while (n1 >= 64) {
+          n1 -= 64;
+          even_batch(L1[n1 + lane], true);
+        }
+        wave_sync_lds();
+      }
+      r += dr;
+      g += dg;
+      if (g >= g1) { g -= ng; ++r; }
+    }
+    wave_sync_lds();
+    if (n1 > 0) even_batch(lane < n1 ? (int)L1[lane] : 0, lane < n1);
+    wave_sync_lds();
+    if (n2 > 0) strength_batch(lane < n2 ? (int)L2[lane] : 0, lane < n2);
+  }
+  __syncthreads();
+  if (dbg == 2) return;
+  // pass 2: cv::FAST NMS over the (sparse) nonzero strength map at both
+  // thresholds in one scan: iniThFAST into mask (+ per-cell counts) and
+  // minThFAST into mask2, used for cells left empty at iniThFAST (:293-296)
+  const int wcell = st.wcell;
+  const int dr = 256 / ng, dg = 256 - dr * ng;
+  {
+    int r = 3 + tid / ng, g = g0 + tid % ng;
+    for (; r < 3 + bh;) {
+      const uint32_t w4 = reinterpret_cast<const uint32_t*>(amap + r * tpitch)[g];
+      if (w4) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int a = (w4 >> (8 * j)) & 0xFF, c = 4 * g + j;
+          if (a == 0 || c < c0 || c >= c1) continue;
+          const int k = min((c - c0) / wcell, st.ncells - 1);
+          const int cb0 = c0 + k * wcell, cb1 = (k == st.ncells - 1) ? c1 : cb0 + wcell;
+          // neighbour scores inside the cell band (0 outside)
+          int nbm = 0, nbi = 0;  // max neighbour score at min / ini threshold
+#pragma unroll
+          for (int dy = -1; dy <= 1; ++dy)
+#pragma unroll
+            for (int dx = -1; dx <= 1; ++dx) {
+              if (!dx && !dy) continue;
+              const int rr = r + dy, cc = c + dx;
+              int aq = 0;
+              if (rr >= 3 && rr < 3 + bh && cc >= cb0 && cc < cb1) aq = amap[rr * tpitch + cc];
+              nbm = max(nbm, aq > min_th ? aq - 1 : 0);
+              nbi = max(nbi, aq > ini_th ? aq - 1 : 0);
+            }
+          const unsigned long long bit = 1ull << (c - cb0);
+          if (a > ini_th && a - 1 > nbi) {
+            atomicOr(&mask[k * bh + (r - 3)], bit);
+            atomicAdd(&cnt[k], 1);
+          }
+          if (a > min_th && a - 1 > nbm) atomicOr(&mask2[k * bh + (r - 3)], bit);
+        }
+      }
+      r += dr;
+      g += dg;
+      if (g >= g1) { g -= ng; ++r; }
     }
   }
   __syncthreads();
+  if (dbg == 3 || dbg == 4) return;
   // pass 4: raster-order output per cell
   uint32_t* fslots = slots + (size_t)f * slot_stride;
   for (int i = tid; i < st.ncells * bh; i += 256) {
     const int k = i / bh, br = i - k * bh;
+    const unsigned long long* mk = (cnt[k] != 0 ? mask : mask2) + k * bh;
     int off = 0;
-    for (int t = 0; t < br; ++t) off += __popcll(mask[k * bh + t]);
-    unsigned long long m = mask[i];
+    for (int t = 0; t < br; ++t) off += __popcll(mk[t]);
+    unsigned long long m = mk[br];
     const CellInfo ci = cells[st.cell_begin + k];
     const int cb0 = c0 + k * wcell;
     const int gy = st.y + 3 + br - ORBX_MINB;
@@ -752,10 +858,8 @@ __global__ __launch_bounds__(256) void k_orient_brief(
   const bool inside = px0 >= 0 && px0 + KP_COLS <= UW && py0 >= 0 && py0 + KP_ROWS <= UH &&
                       ((reinterpret_cast<uintptr_t>(img) | (uintptr_t)pitch) & 3) == 0;
   if (inside) {
-    for (int q = lane; q < KP_ROWS * (KP_COLS / 4); q += 64) {
-      const int r = q / (KP_COLS / 4), c = q - r * (KP_COLS / 4);
-      P[r][c] = reinterpret_cast<const uint32_t*>(img + (size_t)(py0 + r) * pitch + px0)[c];
-    }
+    stage_region<uint32_t, 9, 64>(reinterpret_cast<uint8_t*>(P), KP_COLS,
+                                  img + (size_t)py0 * pitch + px0, pitch, KP_ROWS, KP_COLS / 4, lane);
   } else {
     uint8_t* P8 = reinterpret_cast<uint8_t*>(P);
     for (int q = lane; q < KP_ROWS * KP_COLS; q += 64) {

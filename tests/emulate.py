@@ -170,3 +170,22 @@ def quadtree(keys, N, Wr, Hr, max_passes=64):
         if b is None or keys[k, 2] > keys[b, 2]:
             best[n] = k
     return np.array([keys[best[i]] for i in range(len(rect))], np.int64).reshape(-1, 3)
+
+
+def prefilters(img, t):
+    """The GPU FAST kernel's two pre-tests (kernels_extract.hip k_fast_strips):
+    cardinal (points 0/8 and 4/12) and 4-of-8 even points cyclically
+    consecutive; both must hold wherever A > t."""
+    img = img.astype(np.int32)
+    h, w = img.shape
+    core = img[3:h - 3, 3:w - 3]
+    ring = [img[3 + dy:h - 3 + dy, 3 + dx:w - 3 + dx] for dx, dy in CIRCLE]
+    hi, lo = core + t, core - t
+    card = (((ring[0] > hi) | (ring[8] > hi)) & ((ring[4] > hi) | (ring[12] > hi))) | \
+           (((ring[0] < lo) | (ring[8] < lo)) & ((ring[4] < lo) | (ring[12] < lo)))
+    ev = np.zeros(core.shape, bool)
+    for bright in (True, False):
+        bits = [(ring[2 * k] > hi) if bright else (ring[2 * k] < lo) for k in range(8)]
+        for k in range(8):
+            ev |= bits[k] & bits[(k + 1) % 8] & bits[(k + 2) % 8] & bits[(k + 3) % 8]
+    return card, ev

@@ -67,3 +67,17 @@ def test_quadtree_small_n_and_portrait(oracle):
             ok = e.level_keys(l)
             refk = np.stack([ok["x"] - 16, ok["y"] - 16, ok["response"]], 1).astype(np.int64)
             assert np.array_equal(sel, refk.reshape(-1, 3)), (w, h, l)
+
+
+@pytest.mark.parametrize("kind,idx", [("rects", 0), ("noise", 1), ("rects", 2)])
+def test_fast_prefilters_are_necessary(kind, idx):
+    """Every corner (A > t) passes both pre-tests the GPU kernel applies
+    before the full 16-point strength, so no corner can be dropped."""
+    img = synth.frame(640, 480, idx, kind)
+    A = emulate.fast_strength(img)[3:-3, 3:-3]
+    for t in (0, 7, 20):
+        card, ev = emulate.prefilters(img, t)
+        corner = A > t
+        assert not np.any(corner & ~card), t
+        assert not np.any(corner & ~ev), t
+        assert ev.sum() <= card.sum() or t == 0

@@ -1,0 +1,7 @@
+# trace + traffic (FETCH/WRITE) + SQ counter passes for one tag; each GPU step bounded
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+TAG=${1:-run}
+bash tools/profile.sh $TAG || exit $?
+bash tools/pmc_sq.sh $TAG || exit $?
+python3 tools/pmc_traffic.py gpurun_out/prof_$TAG gpurun_out/prof_$TAG/traffic.json > /dev/null

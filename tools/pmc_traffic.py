@@ -15,6 +15,7 @@ from collections import defaultdict
 
 STAGE_OF = {
     "k_resize": "resize",
+    "k_pyramid": "resize",
     "k_fast_strips": "fast_cells",
     "k_quadtree": "quadtree",
     "k_orient_brief": "orient_brief",
