@@ -17,7 +17,7 @@ namespace orbx {
 __global__ void k_pyramid(const uint8_t*, size_t, size_t, uint8_t*, size_t, const PyrSeg,
                           const int4*, const int4*, const uint4*, const int*, int);
 __global__ void k_fast_strips(const uint8_t*, size_t, size_t, const uint8_t*, size_t,
-                              const LevelInfo*, const CellInfo*, const StripInfo*, uint32_t*,
+                              const LevelArgs, const CellInfo*, const StripInfo*, uint32_t*,
                               size_t, uint32_t*, int, int, int, int, int, int, int);
 __global__ void k_quadtree(const LevelInfo*, const CellInfo*, const uint32_t*, size_t,
                            const uint32_t*, int, uint32_t*, int32_t*, size_t, uint32_t*, size_t,
@@ -132,6 +132,7 @@ struct orbx_plan {
   size_t pyr_stride = 0, blur_stride = 0, slot_stride = 0, qk_stride = 0, qout_stride = 0;
   size_t qt_lds = 0;
   BriefArgs bargs;
+  LevelArgs largs;
   StageTimer timer;
   int dbg = 0; /* ORBX_DEBUG_STOP: kernel phase early-exit for profiling only */
 };
@@ -193,6 +194,12 @@ extern "C" int orbx_plan_create(const orbx_params* prm, int width, int height, i
   }
   p->ndisk = (int)disk.size() / 2;
   memset(&p->bargs, 0, sizeof(p->bargs));
+  memset(&p->largs, 0, sizeof(p->largs));
+  for (int l = 0; l < P.params.nlevels; ++l) {
+    const LevelInfo& u = P.levels[P.levels[l].unique];
+    p->largs.pyr_off[l] = u.pyr_off;
+    p->largs.pitch[l] = u.pitch;
+  }
   p->bargs.nlevels = P.params.nlevels;
   p->bargs.kcap = P.kcap;
   for (int l = 0; l < P.params.nlevels; ++l) {
@@ -300,7 +307,7 @@ extern "C" int orbx_plan_extract(orbx_plan* p, const uint8_t* frames, int nframe
   p->timer.begin(ORBX_STAGE_FAST, s);
   if (!P.strips.empty()) {
     hipLaunchKernelGGL(k_fast_strips, dim3((unsigned)P.strips.size(), n), dim3(256), p->fs_lds, s,
-                       frames, fstride, rstride, p->d_pyr, p->pyr_stride, p->d_lv, p->d_cells,
+                       frames, fstride, rstride, p->d_pyr, p->pyr_stride, p->largs, p->d_cells,
                        p->d_strips, p->d_slots, p->slot_stride, p->d_ccount, P.ncells, P.ini_th,
                        P.min_th, p->fs_tpitch, p->fs_tmaxh, p->fs_mcells, p->dbg);
   }

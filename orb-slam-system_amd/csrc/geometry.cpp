@@ -462,6 +462,7 @@ int plan_geometry(const orbx_params& p, int width, int height, Plan& P) {
         P.strip_max_w = std::max(P.strip_max_w, st.w);
         P.strip_max_h = std::max(P.strip_max_h, st.h);
         P.strip_max_cells = std::max(P.strip_max_cells, st.ncells);
+        if (st.ncells > ORBX_STRIP_MAXCELLS) return ORBX_ERR_UNSUPPORTED;
       }
     }
     lv.ncells = (int)P.cells.size() - lv.cell_begin;

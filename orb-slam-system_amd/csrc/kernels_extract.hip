@@ -328,6 +328,7 @@ __device__ __forceinline__ void wave_sync_lds() {
 
 #define FS_L1CAP 320 /* per-wave cardinal survivors: < 64 carried + <= 256 new */
 #define FS_L2CAP 128 /* per-wave even-test survivors: < 64 carried + <= 64 new */
+#define FS_CCAP 1024 /* per-strip corner list (overflow falls back to a map scan) */
 
 typedef unsigned short us2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ us2 as_us2(uint32_t x) { return __builtin_bit_cast(us2, x); }
@@ -335,7 +336,7 @@ __device__ __forceinline__ uint32_t as_u32(us2 x) { return __builtin_bit_cast(ui
 
 __global__ __launch_bounds__(256) void k_fast_strips(
     const uint8_t* __restrict__ frames, size_t fstride, size_t rstride,
-    const uint8_t* __restrict__ pyr, size_t pstride, const LevelInfo* __restrict__ lv,
+    const uint8_t* __restrict__ pyr, size_t pstride, const LevelArgs LA,
     const CellInfo* __restrict__ cells, const StripInfo* __restrict__ strips,
     uint32_t* __restrict__ slots, size_t slot_stride, uint32_t* __restrict__ ccount, int ncells,
     int ini_th, int min_th, int tpitch, int tmax_h, int mcells, int dbg) {
@@ -347,11 +348,16 @@ __global__ __launch_bounds__(256) void k_fast_strips(
   int* cnt = reinterpret_cast<int*>(mask2 + mcells * (tmax_h - 6));  // mcells
   __shared__ uint16_t wlist1[4][FS_L1CAP];
   __shared__ uint16_t wlist2[4][FS_L2CAP];
+  __shared__ uint16_t clist[FS_CCAP];  // corners at t_lo (A > t_lo), any order
+  __shared__ int cslot[ORBX_STRIP_MAXCELLS];
+  __shared__ int ncorner;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const StripInfo st = strips[blockIdx.x];
   const int f = blockIdx.y;
-  int pitch;
-  const uint8_t* base = level_base(frames, fstride, rstride, pyr, pstride, lv[st.level], st.level, f, &pitch);
+  const int pitch = st.level == 0 ? (int)rstride : LA.pitch[st.level];
+  const uint8_t* base = st.level == 0 ? frames + (size_t)f * fstride
+                                      : pyr + (size_t)f * pstride + LA.pyr_off[st.level];
+  const int slot_pref = tid < st.ncells ? cells[st.cell_begin + tid].slot_off : 0;  // in flight
   const int bh = st.h - 6;
   const uintptr_t alb = reinterpret_cast<uintptr_t>(base) | (uintptr_t)pitch;
   const bool aligned = (alb & 3) == 0;
@@ -366,12 +372,16 @@ __global__ __launch_bounds__(256) void k_fast_strips(
     else stage_region<uint8_t, 16, 256>(tile, tpitch, s0, pitch, st.h, tw, tid);
   }
   for (int i = tid; i < st.ncells * bh; i += 256) mask[i] = mask2[i] = 0ull;
-  if (tid < st.ncells) cnt[tid] = 0;
+  if (tid < st.ncells) {
+    cnt[tid] = 0;
+    cslot[tid] = slot_pref;
+  }
+  if (tid == 0) ncorner = 0;
   __syncthreads();
   if (dbg == 1) return;
-  // band columns [c0, c1) in tile coordinates, rows [3, 3+bh)
-  const CellInfo lastc = cells[st.cell_begin + st.ncells - 1];
-  const int c0 = lead + 3, c1 = lead + (lastc.x + lastc.w - st.x) - 3;
+  // band columns [c0, c1) in tile coordinates, rows [3, 3+bh); the strip's
+  // cells tile [st.x, st.x + st.w)
+  const int c0 = lead + 3, c1 = lead + st.w - 3;
   const int t_lo = min(ini_th, min_th);
   // pass 1 (per wave, no block barrier).  Stage A: cardinal pre-test on a
   // group of 4 pixels (tile cols 4g..4g+3) in packed 16-bit lanes + zero-fill
@@ -386,11 +396,19 @@ __global__ __launch_bounds__(256) void k_fast_strips(
   int n1 = 0, n2 = 0;  // wave-uniform list lengths
   const unsigned long long lt = (1ull << lane) - 1ull;
   auto strength_batch = [&](int e, bool act) {
+    bool corner = false;
     if (act) {
       const int rr = e >> 9, cc = e & 511;
       const int a = fast_strength(tile + rr * tpitch + cc, tpitch);
-      amap[rr * tpitch + cc] = (uint8_t)(a > t_lo ? a : 0);
+      corner = a > t_lo;
+      amap[rr * tpitch + cc] = (uint8_t)(corner ? a : 0);
     }
+    const unsigned long long bal = __ballot(corner);
+    int b = 0;
+    if (lane == 0 && bal) b = atomicAdd(&ncorner, __popcll(bal));
+    b = __shfl(b, 0, 64);
+    const int q = b + __popcll(bal & lt);
+    if (corner && q < FS_CCAP) clist[q] = (uint16_t)e;
   };
   auto even_batch = [&](int e, bool act) {
     const bool keep = act && fast_even_test(tile + (e >> 9) * tpitch + (e & 511), tpitch, t_lo);
@@ -471,8 +489,37 @@ __global__ __launch_bounds__(256) void k_fast_strips(
   // thresholds in one scan: iniThFAST into mask (+ per-cell counts) and
   // minThFAST into mask2, used for cells left empty at iniThFAST (:293-296)
   const int wcell = st.wcell;
-  const int dr = 256 / ng, dg = 256 - dr * ng;
-  {
+  auto nms_pixel = [&](int r, int c, int a) {
+    const int k = min((c - c0) / wcell, st.ncells - 1);
+    const int cb0 = c0 + k * wcell, cb1 = (k == st.ncells - 1) ? c1 : cb0 + wcell;
+    int nbm = 0, nbi = 0;  // max neighbour score at min / ini threshold (0 outside the band)
+#pragma unroll
+    for (int dy = -1; dy <= 1; ++dy)
+#pragma unroll
+      for (int dx = -1; dx <= 1; ++dx) {
+        if (!dx && !dy) continue;
+        const int rr = r + dy, cc = c + dx;
+        int aq = 0;
+        if (rr >= 3 && rr < 3 + bh && cc >= cb0 && cc < cb1) aq = amap[rr * tpitch + cc];
+        nbm = max(nbm, aq > min_th ? aq - 1 : 0);
+        nbi = max(nbi, aq > ini_th ? aq - 1 : 0);
+      }
+    const unsigned long long bit = 1ull << (c - cb0);
+    if (a > ini_th && a - 1 > nbi) {
+      atomicOr(&mask[k * bh + (r - 3)], bit);
+      atomicAdd(&cnt[k], 1);
+    }
+    if (a > min_th && a - 1 > nbm) atomicOr(&mask2[k * bh + (r - 3)], bit);
+  };
+  const int nc = ncorner;
+  if (nc <= FS_CCAP) {
+    for (int q = tid; q < nc; q += 256) {
+      const int e = clist[q];
+      const int r = e >> 9, c = e & 511;
+      nms_pixel(r, c, amap[r * tpitch + c]);
+    }
+  } else {  // list overflow: scan the strength map
+    const int dr = 256 / ng, dg = 256 - dr * ng;
     int r = 3 + tid / ng, g = g0 + tid % ng;
     for (; r < 3 + bh;) {
       const uint32_t w4 = reinterpret_cast<const uint32_t*>(amap + r * tpitch)[g];
@@ -481,27 +528,7 @@ __global__ __launch_bounds__(256) void k_fast_strips(
         for (int j = 0; j < 4; ++j) {
           const int a = (w4 >> (8 * j)) & 0xFF, c = 4 * g + j;
           if (a == 0 || c < c0 || c >= c1) continue;
-          const int k = min((c - c0) / wcell, st.ncells - 1);
-          const int cb0 = c0 + k * wcell, cb1 = (k == st.ncells - 1) ? c1 : cb0 + wcell;
-          // neighbour scores inside the cell band (0 outside)
-          int nbm = 0, nbi = 0;  // max neighbour score at min / ini threshold
-#pragma unroll
-          for (int dy = -1; dy <= 1; ++dy)
-#pragma unroll
-            for (int dx = -1; dx <= 1; ++dx) {
-              if (!dx && !dy) continue;
-              const int rr = r + dy, cc = c + dx;
-              int aq = 0;
-              if (rr >= 3 && rr < 3 + bh && cc >= cb0 && cc < cb1) aq = amap[rr * tpitch + cc];
-              nbm = max(nbm, aq > min_th ? aq - 1 : 0);
-              nbi = max(nbi, aq > ini_th ? aq - 1 : 0);
-            }
-          const unsigned long long bit = 1ull << (c - cb0);
-          if (a > ini_th && a - 1 > nbi) {
-            atomicOr(&mask[k * bh + (r - 3)], bit);
-            atomicAdd(&cnt[k], 1);
-          }
-          if (a > min_th && a - 1 > nbm) atomicOr(&mask2[k * bh + (r - 3)], bit);
+          nms_pixel(r, c, a);
         }
       }
       r += dr;
@@ -511,26 +538,30 @@ __global__ __launch_bounds__(256) void k_fast_strips(
   }
   __syncthreads();
   if (dbg == 3 || dbg == 4) return;
-  // pass 4: raster-order output per cell
+  // pass 4: raster-order output per cell: one wave per cell, lane = band row,
+  // row offsets by a wave prefix sum of the row popcounts
   uint32_t* fslots = slots + (size_t)f * slot_stride;
-  for (int i = tid; i < st.ncells * bh; i += 256) {
-    const int k = i / bh, br = i - k * bh;
+  for (int k = wave; k < st.ncells; k += 4) {
     const unsigned long long* mk = (cnt[k] != 0 ? mask : mask2) + k * bh;
-    int off = 0;
-    for (int t = 0; t < br; ++t) off += __popcll(mk[t]);
-    unsigned long long m = mk[br];
-    const CellInfo ci = cells[st.cell_begin + k];
-    const int cb0 = c0 + k * wcell;
-    const int gy = st.y + 3 + br - ORBX_MINB;
-    while (m) {
-      const int b = __ffsll(m) - 1;
-      m &= m - 1;
-      const int c = cb0 + b;
-      const int gx = xal + c - ORBX_MINB;
-      fslots[ci.slot_off + off++] =
-          orbx_pack_key((uint32_t)gx, (uint32_t)gy, (uint32_t)amap[(3 + br) * tpitch + c] - 1u);
+    const int cb0 = c0 + k * wcell, so = cslot[k];
+    int carry = 0;
+    for (int rb = 0; rb < bh; rb += 64) {
+      const int br = rb + lane;
+      unsigned long long m = br < bh ? mk[br] : 0ull;
+      int tot;
+      int off = carry + wave_excl_scan(__popcll(m), lane, &tot);
+      const int gy = st.y + 3 + br - ORBX_MINB;
+      while (m) {
+        const int b = __ffsll(m) - 1;
+        m &= m - 1;
+        const int c = cb0 + b;
+        const int gx = xal + c - ORBX_MINB;
+        fslots[so + off++] =
+            orbx_pack_key((uint32_t)gx, (uint32_t)gy, (uint32_t)amap[(3 + br) * tpitch + c] - 1u);
+      }
+      carry += tot;
     }
-    if (br == bh - 1) ccount[(size_t)f * ncells + st.cell_begin + k] = (uint32_t)off;
+    if (lane == 0) ccount[(size_t)f * ncells + st.cell_begin + k] = (uint32_t)carry;
   }
 }
 

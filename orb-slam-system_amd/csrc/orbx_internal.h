@@ -75,6 +75,14 @@ struct StripInfo {
   int wcell;
 };
 
+/* per-level storage of the pyramid, passed by value to kernels that only
+ * need to locate a level (no dependent LevelInfo loads) */
+struct LevelArgs {
+  long long pyr_off[ORBX_MAX_LEVELS];
+  int pitch[ORBX_MAX_LEVELS];
+};
+#define ORBX_STRIP_MAXCELLS 64 /* cells per FAST strip (>= 256 / min cell width) */
+
 /* per-level constants of k_orient_brief, passed by value (kernel arguments
  * live in SGPRs: no dependent global loads to find a keypoint's level) */
 struct BriefArgs {
