@@ -214,6 +214,8 @@ extern "C" int orbm_search_by_bow(const orbx_bow_frame* kf1, const orbx_bow_fram
     P.check_ori = check_ori ? 1 : 0;
     P.nnratio = nnratio;
     P.sequential = sequential;
+    P.dcap = orbm_dcap(nnratio);
+    P.pad = 0;
     MProblem* d_prob = B.upload(&P, 1, s);
     MNodePair* d_nps = B.upload(nps.data(), nps.size(), s);
     uint2* d_cand = B.alloc<uint2>((size_t)rows * ORBM_T);
@@ -311,7 +313,8 @@ __global__ void k_match_setup(MProblem* probs, MNodePair* nps, int npairs,
   P.check_ori = check_ori;
   P.nnratio = nnratio;
   P.sequential = 0;
-  P.pad[0] = P.pad[1] = 0;
+  P.dcap = orbm_dcap(nnratio);
+  P.pad = 0;
   probs[p] = P;
   MNodePair NP;
   NP.prob = p;

@@ -33,8 +33,22 @@ struct MProblem {
   int check_ori;
   float nnratio;
   int sequential;  /* 1: one wave walks all node pairs in order (malformed FeatureVectors) */
-  int pad[2];
+  int dcap;        /* candidate distance cap (orbm_dcap) */
+  int pad;
 };
+
+/* Smallest distance D >= TH_LOW with (float)(TH_LOW-1) < nnratio * (float)D,
+ * capped at 257.  Only candidates below D can change a SearchByBoW decision:
+ * a best match needs d < TH_LOW <= D, and a second-best >= D always passes
+ * the ratio test (ORBmatcher.cc:339-342), exactly like the true value. */
+#if defined(__HIPCC__)
+__host__ __device__
+#endif
+static inline int orbm_dcap(float nnratio) {
+  for (int D = ORBM_TH_LOW; D <= 256; ++D)
+    if ((float)(ORBM_TH_LOW - 1) < nnratio * (float)D) return D;
+  return 257;
+}
 
 struct MNodePair {
   int prob;
