@@ -276,8 +276,6 @@ __global__ __launch_bounds__(256) void k_match_cand_rows(
       atomicOr(&svalid[(i >> 1) >> 5], 1u << ((i >> 1) & 31));
   }
   __syncthreads();
-  int nvalid = 0;
-  for (int w = 0; w < ((n2 + 31) >> 5); ++w) nvalid += __popc(svalid[w]);
   const int a = a0 + tid;
   const bool act = a < NP.n1;
   const int r = NP.row_base + a;
@@ -290,34 +288,52 @@ __global__ __launch_bounds__(256) void k_match_cand_rows(
     q0 = reinterpret_cast<const uint4*>(P.desc1 + (size_t)idx1 * 32)[0];
     q1 = reinterpret_cast<const uint4*>(P.desc1 + (size_t)idx1 * 32)[1];
   }
+  // lists start full of sentinels at the distance cap: only d < dcap enters
+  const uint32_t sent = (uint32_t)P.dcap << 16;
   uint32_t L[ORBM_T];
 #pragma unroll
-  for (int t = 0; t < ORBM_T; ++t) L[t] = 0xFFFFFFFFu;
-  for (int j0 = 0; j0 < n2; j0 += 4) {
-    uint32_t kk[4];
+  for (int t = 0; t < ORBM_T; ++t) L[t] = sent;
+  auto dist = [&](int j) {
+    const uint4 b0 = sdesc[2 * j], b1 = sdesc[2 * j + 1];
+    return __popc(q0.x ^ b0.x) + __popc(q0.y ^ b0.y) + __popc(q0.z ^ b0.z) +
+           __popc(q0.w ^ b0.w) + __popc(q1.x ^ b1.x) + __popc(q1.y ^ b1.y) +
+           __popc(q1.z ^ b1.z) + __popc(q1.w ^ b1.w);
+  };
+  auto insert = [&](uint32_t k) {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int j = min(j0 + q, n2 - 1);
-      const uint4 b0 = sdesc[2 * j], b1 = sdesc[2 * j + 1];
-      const bool ok = (j0 + q < n2) && ((svalid[j >> 5] >> (j & 31)) & 1u);
-      const uint32_t d = __popc(q0.x ^ b0.x) + __popc(q0.y ^ b0.y) + __popc(q0.z ^ b0.z) +
-                         __popc(q0.w ^ b0.w) + __popc(q1.x ^ b1.x) + __popc(q1.y ^ b1.y) +
-                         __popc(q1.z ^ b1.z) + __popc(q1.w ^ b1.w);
-      kk[q] = ok ? ((d << 16) | (uint32_t)j) : 0xFFFFFFFFu;
+    for (int t = 0; t < ORBM_T; ++t) {
+      const uint32_t lo = min(L[t], k);
+      k = max(L[t], k);
+      L[t] = lo;
     }
+  };
+  const int n8 = n2 & ~7;
+  for (int j0 = 0; j0 < n8; j0 += 8) {
+    // validity of these 8 positions: one wave-uniform word
+    const uint32_t vw = __builtin_amdgcn_readfirstlane(svalid[j0 >> 5]) >> (j0 & 31);
+    uint32_t kk[8];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      uint32_t k = kk[q];
-      if (__ballot(k < L[ORBM_T - 1])) {
+    for (int q = 0; q < 8; ++q)
+      kk[q] = ((vw >> q) & 1u) ? (((uint32_t)dist(j0 + q) << 16) | (uint32_t)(j0 + q)) : 0xFFFFFFFFu;
+    uint32_t kmin = kk[0];
 #pragma unroll
-        for (int t = 0; t < ORBM_T; ++t) {
-          const uint32_t lo = min(L[t], k);
-          k = max(L[t], k);
-          L[t] = lo;
-        }
-      }
+    for (int q = 1; q < 8; ++q) kmin = min(kmin, kk[q]);
+    if (__ballot(kmin < L[ORBM_T - 1])) {
+#pragma unroll
+      for (int q = 0; q < 8; ++q)
+        if (__ballot(kk[q] < L[ORBM_T - 1])) insert(kk[q]);
     }
   }
+  for (int j = n8; j < n2; ++j) {
+    const bool ok = (svalid[j >> 5] >> (j & 31)) & 1u;
+    const uint32_t k = ok ? (((uint32_t)dist(j) << 16) | (uint32_t)j) : 0xFFFFFFFFu;
+    if (__ballot(k < L[ORBM_T - 1])) insert(k);
+  }
+  // a full list (no sentinel left) may have more candidates below the cap
+  const bool full = L[ORBM_T - 1] < sent;
+#pragma unroll
+  for (int t = 0; t < ORBM_T; ++t)
+    if (L[t] >= sent) L[t] = 0xFFFFFFFFu;
   if (!act) return;
   ev[r] = make_int2(-1, 0);
   if (!v1) {
@@ -325,7 +341,8 @@ __global__ __launch_bounds__(256) void k_match_cand_rows(
     return;
   }
   const int minD = L[0] != 0xFFFFFFFFu ? (int)(L[0] >> 16) : (1 << 20);
-  rowinfo[r] = make_int4(1, nvalid, minD, idx1);
+  // .y > ORBM_T: the list may be incomplete (resolve rescans when exhausted)
+  rowinfo[r] = make_int4(1, full ? ORBM_T + 1 : 0, minD, idx1);
   if (minD >= ORBM_TH_LOW) return;
   uint4* out = reinterpret_cast<uint4*>(cand + (size_t)r * ORBM_T);
 #pragma unroll
@@ -483,25 +500,33 @@ __global__ __launch_bounds__(64) void k_match_resolve_spec(
   __builtin_amdgcn_wave_barrier();
   const float factor = 1.0f / ORBM_HISTO;
   const uint64_t below = (1ull << lane) - 1ull;
+  // the next chunk's row info and candidate lists are loaded while the
+  // current chunk resolves (rows that are not feasible never read theirs)
+  int4 inf_n = make_int4(0, 0, 0, 0);
+  uint4 cv_n[ORBM_T / 2];
+  auto fetch = [&](int base) {
+    const int r = NP.row_base + base + lane;
+    inf_n = make_int4(0, 0, 0, 0);
+    if (base + lane < NP.n1) inf_n = rowinfo[r];
+    const uint4* src = reinterpret_cast<const uint4*>(cand + (size_t)r * ORBM_T);
+#pragma unroll
+    for (int t = 0; t < ORBM_T / 2; ++t)
+      cv_n[t] = (base + lane < NP.n1) ? src[t] : make_uint4(0xFFFFFFFFu, 0u, 0xFFFFFFFFu, 0u);
+  };
+  fetch(0);
   for (int base = 0; base < NP.n1; base += 64) {
     const int r = NP.row_base + base + lane;
-    int4 inf = make_int4(0, 0, 0, 0);
-    if (base + lane < NP.n1) inf = rowinfo[r];
+    const int4 inf = inf_n;
     const bool feas = inf.x != 0 && inf.z < ORBM_TH_LOW;
-    uint64_t pend = __ballot(feas);
-    if (!pend) continue;
     uint2 c[ORBM_T];
 #pragma unroll
-    for (int t = 0; t < ORBM_T; ++t) c[t] = make_uint2(0xFFFFFFFFu, 0u);
-    if (feas) {
-      const uint4* src = reinterpret_cast<const uint4*>(cand + (size_t)r * ORBM_T);
-#pragma unroll
-      for (int t = 0; t < ORBM_T / 2; ++t) {
-        const uint4 v = src[t];
-        c[2 * t] = make_uint2(v.x, v.y);
-        c[2 * t + 1] = make_uint2(v.z, v.w);
-      }
+    for (int t = 0; t < ORBM_T / 2; ++t) {
+      c[2 * t] = feas ? make_uint2(cv_n[t].x, cv_n[t].y) : make_uint2(0xFFFFFFFFu, 0u);
+      c[2 * t + 1] = feas ? make_uint2(cv_n[t].z, cv_n[t].w) : make_uint2(0xFFFFFFFFu, 0u);
     }
+    if (base + 64 < NP.n1) fetch(base + 64);
+    uint64_t pend = __ballot(feas);
+    if (!pend) continue;
     while (pend) {
       const bool mine = (pend >> lane) & 1ull;
       int k1 = INT_MAX, k2 = INT_MAX, id1 = -1, nun = 0, plen = ORBM_T;
