@@ -24,7 +24,7 @@ __global__ void k_quadtree(const LevelInfo*, const CellInfo*, const uint32_t*, s
                            int*, int, int, int, int*);
 __global__ void k_orient_brief(const uint8_t*, size_t, size_t, const uint8_t*, size_t,
                                const BriefArgs, const uint32_t*, size_t, const int*,
-                               const int16_t*, int, orbx_keypoint*, uint8_t*, int*);
+                               orbx_keypoint*, uint8_t*, int*);
 __global__ void k_synth(uint8_t*, int, int, size_t, int, int);
 }  // namespace orbx
 
@@ -123,8 +123,7 @@ struct orbx_plan {
   int32_t *d_xofs = nullptr, *d_xofs1 = nullptr, *d_yofs = nullptr;
   int32_t *d_pyr_xs = nullptr, *d_pyr_ys = nullptr, *d_pyr_bo = nullptr;
   uint32_t* d_pyr_blob = nullptr;
-  int16_t *d_alpha = nullptr, *d_beta = nullptr, *d_disk = nullptr;
-  int ndisk = 0;
+  int16_t *d_alpha = nullptr, *d_beta = nullptr;
   uint8_t *d_pyr = nullptr, *d_blur = nullptr;
   uint32_t *d_slots = nullptr, *d_ccount = nullptr, *d_qkeys = nullptr, *d_qout = nullptr;
   int32_t* d_qnode = nullptr;
@@ -143,7 +142,7 @@ static void plan_free(orbx_plan* p) {
   if (!p) return;
   hipSetDevice(p->device);
   void* bufs[] = {p->d_lv, p->d_cells, p->d_strips, p->d_xofs, p->d_xofs1, p->d_yofs, p->d_alpha, p->d_beta,
-                  p->d_disk, p->d_pyr, p->d_blur, p->d_slots, p->d_ccount, p->d_qkeys, p->d_qout,
+                  p->d_pyr, p->d_blur, p->d_slots, p->d_ccount, p->d_qkeys, p->d_qout,
                   p->d_qnode, p->d_lcount, p->d_err, p->d_pyr_xs, p->d_pyr_ys, p->d_pyr_bo, p->d_pyr_blob};
   for (void* b : bufs)
     if (b) hipFree(b);
@@ -186,14 +185,13 @@ extern "C" int orbx_plan_create(const orbx_params* prm, int width, int height, i
   if (hipFuncSetAttribute((const void*)k_quadtree, hipFuncAttributeMaxDynamicSharedMemorySize,
                           (int)p->qt_lds) != hipSuccess) { plan_free(p); return ORBX_ERR_HIP; }
   if (hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking) != hipSuccess) { plan_free(p); return ORBX_ERR_HIP; }
-  // disk offsets of IC_Angle (ORBextractor.cc:28-45), umax from the tables
-  std::vector<int16_t> disk;
-  for (int v = -15; v <= 15; ++v) {
-    const int um = (v == 0) ? 15 : P.tables.umax[v < 0 ? -v : v];
-    for (int u = -um; u <= um; ++u) { disk.push_back((int16_t)u); disk.push_back((int16_t)v); }
-  }
-  p->ndisk = (int)disk.size() / 2;
   memset(&p->bargs, 0, sizeof(p->bargs));
+  // IC_Angle row extents (ORBextractor.cc:28-45): the centre row spans
+  // [-15, 15], row v spans [-umax[|v|], umax[|v|]]
+  for (int v = 0; v < 16; ++v) {
+    const uint32_t um = (v == 0) ? 15u : (uint32_t)P.tables.umax[v];
+    p->bargs.umaxw[v >> 2] |= um << (8 * (v & 3));
+  }
   memset(&p->largs, 0, sizeof(p->largs));
   for (int l = 0; l < P.params.nlevels; ++l) {
     const LevelInfo& u = P.levels[P.levels[l].unique];
@@ -229,7 +227,7 @@ extern "C" int orbx_plan_create(const orbx_params* prm, int width, int height, i
   if (upload(&p->d_lv, P.levels) || upload(&p->d_cells, P.cells) || upload(&p->d_strips, P.strips) ||
       upload(&p->d_xofs, P.xofs) ||
       upload(&p->d_xofs1, P.xofs1) || upload(&p->d_yofs, P.yofs) || upload(&p->d_alpha, P.alpha) ||
-      upload(&p->d_beta, P.beta) || upload(&p->d_disk, disk) ||
+      upload(&p->d_beta, P.beta) ||
       upload(&p->d_pyr_xs, P.pyr_xs) || upload(&p->d_pyr_ys, P.pyr_ys) ||
       upload(&p->d_pyr_bo, P.pyr_bo) || upload(&p->d_pyr_blob, P.pyr_blob)) {
     plan_free(p);
@@ -322,9 +320,11 @@ extern "C" int orbx_plan_extract(orbx_plan* p, const uint8_t* frames, int nframe
   p->timer.end(ORBX_STAGE_QUADTREE, s);
   // K4+K5+K6+K7 orientation, blur-at-sample descriptors, assembly
   p->timer.begin(ORBX_STAGE_BRIEF, s);
-  hipLaunchKernelGGL(k_orient_brief, dim3((P.kcap + 3) / 4 > 0 ? (P.kcap + 3) / 4 : 1, n),
+  // waves stride over each frame's keypoints (about nfeatures of them)
+  const int ob_waves = std::max(4, std::min(P.kcap, P.params.nfeatures + 256));
+  hipLaunchKernelGGL(k_orient_brief, dim3((ob_waves + 3) / 4, n),
                      dim3(256), 0, s, frames, fstride, rstride, p->d_pyr, p->pyr_stride, p->bargs,
-                     p->d_qout, p->qout_stride, p->d_lcount, p->d_disk, p->ndisk, kps, desc,
+                     p->d_qout, p->qout_stride, p->d_lcount, kps, desc,
                      counts);
   p->timer.end(ORBX_STAGE_BRIEF, s);
   if (hipGetLastError() != hipSuccess) return ORBX_ERR_HIP;

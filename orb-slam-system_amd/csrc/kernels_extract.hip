@@ -852,8 +852,7 @@ __global__ __launch_bounds__(256) void k_orient_brief(
     const uint8_t* __restrict__ frames, size_t fstride, size_t rstride,
     const uint8_t* __restrict__ pyr, size_t pstride, const BriefArgs A,
     const uint32_t* __restrict__ qout, size_t qout_stride, const int* __restrict__ lcount,
-    const int16_t* __restrict__ disk, int ndisk, orbx_keypoint* __restrict__ kps,
-    uint8_t* __restrict__ desc, int* __restrict__ counts) {
+    orbx_keypoint* __restrict__ kps, uint8_t* __restrict__ desc, int* __restrict__ counts) {
   __shared__ uint32_t patch[4][KP_ROWS][KP_COLS / 4];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int f = blockIdx.y;
@@ -869,13 +868,12 @@ __global__ __launch_bounds__(256) void k_orient_brief(
   }
   const int total = __shfl(incl, 63, 64);  // all lanes active here
   if (blockIdx.x == 0 && threadIdx.x == 0) counts[f] = total;
-  if (g >= kcap) return;
-  int l = 0;
-  while (l < nlevels && !(g >= A.kout_off[l] && g < A.kout_off[l] + A.lcap[l])) ++l;
-  if (l >= nlevels) return;
-  const int i = g - A.kout_off[l];
-  if (i >= __shfl(lcv, l, 64)) return;
-  const int o = i + __shfl(incl - lcv, l, 64);
+  // output position o (levels concatenated, :455-494); waves stride over
+  // the frame's keypoints, so the grid is sized by nfeatures, not capacity
+  const int stride = (int)gridDim.x * 4;
+  for (int o = g; o < total; o += stride) {  // wave-uniform
+  const int l = __popcll(__ballot(lane < nlevels && incl <= o));
+  const int i = o - __shfl(incl - lcv, l, 64);
   const uint32_t key = qout[(size_t)f * qout_stride + A.kout_off[l] + i];
   const int x = (int)(key >> 20) + ORBX_MINB, y = (int)((key >> 8) & 0xFFF) + ORBX_MINB;
   const int score = (int)(key & 0xFF);
@@ -903,20 +901,31 @@ __global__ __launch_bounds__(256) void k_orient_brief(
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   const uint8_t* P8 = reinterpret_cast<const uint8_t*>(P);
-  // IC_Angle (:21-48) on the unblurred level
+  // IC_Angle (:21-48) on the unblurred level: lane = patch row v + 15,
+  // u in [-umax[|v|], umax[|v|]] (integer sums: order-free)
   const int cc = x - px0, cr = KP_R;
   int m10 = 0, m01 = 0;
-  for (int j = lane; j < ndisk; j += 64) {
-    const int du = disk[2 * j], dv = disk[2 * j + 1];
-    const int I = P8[(cr + dv) * KP_COLS + cc + du];
-    m10 += du * I;
-    m01 += dv * I;
+  if (lane < 31) {
+    const int v = lane - 15, av = v < 0 ? -v : v;
+    const uint32_t uw = (av >> 2) == 0 ? A.umaxw[0] : (av >> 2) == 1 ? A.umaxw[1]
+                      : (av >> 2) == 2 ? A.umaxw[2] : A.umaxw[3];
+    const int um = (int)((uw >> (8 * (av & 3))) & 0xFFu);
+    const uint8_t* rowp = P8 + (cr + v) * KP_COLS + cc;
+    int sum = 0;
+    for (int uu = -um; uu <= um; ++uu) {
+      const int I = rowp[uu];
+      sum += I;
+      m10 += uu * I;
+    }
+    m01 = v * sum;
   }
 #pragma unroll
   for (int d = 32; d >= 1; d >>= 1) {
     m10 += __shfl_xor(m10, d, 64);
     m01 += __shfl_xor(m01, d, 64);
   }
+  m10 = __builtin_amdgcn_readfirstlane(m10);  // uniform: scalar angle / sincos table
+  m01 = __builtin_amdgcn_readfirstlane(m01);
   const float angle = fast_atan2((float)m01, (float)m10);
   const float factorPI = (float)(3.1415926535897932384626433832795 / 180.f);
   float sn, cs;
@@ -969,6 +978,7 @@ __global__ __launch_bounds__(256) void k_orient_brief(
     kp.octave = l;
     kp.class_id = -1;
     kps[(size_t)f * kcap + o] = kp;
+  }
   }
 }
 

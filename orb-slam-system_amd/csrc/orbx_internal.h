@@ -92,6 +92,7 @@ struct BriefArgs {
   long long pyr_off[ORBX_MAX_LEVELS];
   float scale[ORBX_MAX_LEVELS];
   int patch[ORBX_MAX_LEVELS];
+  uint32_t umaxw[4]; /* IC_Angle umax[0..15], one byte each */
 };
 
 /* fused pyramid segment: destination levels lev[1..nl] computed in one
