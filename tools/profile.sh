@@ -4,7 +4,7 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 TAG=${1:-run}
-ARGS="--steps 3 --warmup 1 --batch 64 --no-cpu-baseline"
+ARGS="--steps 3 --warmup 1 --batch ${BATCH:-256} --no-cpu-baseline"
 export TMPDIR=/tmp
 OUT=$GRAFT_REPO_ROOT/gpurun_out/prof_$TAG
 mkdir -p $OUT
