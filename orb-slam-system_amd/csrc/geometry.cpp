@@ -7,6 +7,7 @@
 #include "geometry.h"
 
 #include <math.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -303,14 +304,17 @@ static int plan_pyramid(Plan& P) {
   std::vector<int> uniq;
   for (int l = 0; l < (int)P.levels.size(); ++l)
     if (P.levels[l].unique == l) uniq.push_back(l);
-  static const int tiles[][2] = {{64, 32}, {64, 16}, {32, 32}, {32, 16}, {16, 16}, {16, 8}, {8, 8}};
+  static const int tiles[][2] = {{64, 16}, {128, 16}, {128, 8}, {64, 8}, {64, 32}, {32, 16},
+                                 {16, 16}, {16, 8}, {8, 8}};
+  int k0 = 0; /* ORBX_DEBUG_PYR_TILE=k: start the tile search at tiles[k] (profiling only) */
+  if (const char* e = getenv("ORBX_DEBUG_PYR_TILE")) k0 = std::min(std::max(atoi(e), 0), 8);
   size_t i = 1;
   while (i < uniq.size()) {
     bool done = false;
     for (size_t j = uniq.size(); j > i && !done; --j) {
       std::vector<int> lev(uniq.begin() + (i - 1), uniq.begin() + j);
-      const int ntile = (j == i + 1) ? 7 : 4;
-      for (int k = 0; k < ntile && !done; ++k) {
+      const int ntile = (j == i + 1) ? 9 : 6;
+      for (int k = std::min(k0, ntile - 1); k < ntile && !done; ++k) {
         PyrSeg g;
         std::vector<Iv> xs, ys;
         if (!try_segment(P, lev, tiles[k][0], tiles[k][1], g, xs, ys)) continue;

@@ -78,6 +78,8 @@ __device__ __forceinline__ void stage_region(uint8_t* __restrict__ lds, int lpit
 // is written once and the intermediate levels are never re-read from HBM.
 // Thread = 4 consecutive columns (dword in LDS and HBM) of a row.
 // ---------------------------------------------------------------------------
+#define PYR_U 1 /* rows in flight per thread (more measured slower) */
+
 __global__ __launch_bounds__(256) void k_pyramid(const uint8_t* __restrict__ frames, size_t fstride,
                                                  size_t rstride, uint8_t* __restrict__ pyr,
                                                  size_t pstride, const PyrSeg S,
@@ -158,29 +160,42 @@ __global__ __launch_bounds__(256) void k_pyramid(const uint8_t* __restrict__ fra
         const bool any_x = gx0 + 4 > X.z && gx0 < X.w;
         uint8_t* gdst = pyr + (size_t)f * pstride + S.off[s];
         const int gp = S.pitch[s];
-        for (int r = r0; r < nrows; r += R) {
-          const int y = Y.x + r;
-          const uint2 e = yl[yo + r];
-          const int b0 = (int)(int16_t)(e.y & 0xFFFF), b1 = (int)e.y >> 16;
-          const uint8_t* R0 = cur + (int)(e.x & 0xFFFF) * cpitch;
-          const uint8_t* R1 = cur + (int)(e.x >> 16) * cpitch;
-          uint32_t packed = 0;
+        // PYR_U rows per iteration: every LDS read of the group is issued
+        // before the first store (cur/nxt alias as far as the compiler knows)
+        for (int rb = r0; rb < nrows; rb += PYR_U * R) {
+          uint32_t packed[PYR_U];
 #pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            const int d0 = R0[sx[k]] * a0[k] + R0[sx1[k]] * a1[k];
-            const int d1 = R1[sx[k]] * a0[k] + R1[sx1[k]] * a1[k];
-            const int v = (((b0 * (d0 >> 4)) >> 16) + ((b1 * (d1 >> 4)) >> 16) + 2) >> 2;
-            packed |= (uint32_t)(v & 0xFF) << (8 * k);
+          for (int u = 0; u < PYR_U; ++u) {
+            const int r = min(rb + u * R, nrows - 1);
+            const uint2 e = yl[yo + r];
+            const int b0 = (int)(int16_t)(e.y & 0xFFFF), b1 = (int)e.y >> 16;
+            const uint8_t* R0 = cur + (int)(e.x & 0xFFFF) * cpitch;
+            const uint8_t* R1 = cur + (int)(e.x >> 16) * cpitch;
+            uint32_t pk = 0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+              const int d0 = R0[sx[k]] * a0[k] + R0[sx1[k]] * a1[k];
+              const int d1 = R1[sx[k]] * a0[k] + R1[sx1[k]] * a1[k];
+              const int v = (((b0 * (d0 >> 4)) >> 16) + ((b1 * (d1 >> 4)) >> 16) + 2) >> 2;
+              pk |= (uint32_t)(v & 0xFF) << (8 * k);
+            }
+            packed[u] = pk;
           }
-          *reinterpret_cast<uint32_t*>(nxt + r * dpitch + 4 * cg) = packed;
-          if (y >= Y.z && y < Y.w && any_x) {
-            uint8_t* o = gdst + (size_t)y * gp + gx0;
-            if (in_x) {
-              *reinterpret_cast<uint32_t*>(o) = packed;  // pyr offsets/pitches are 16-B multiples
-            } else {
 #pragma unroll
-              for (int k = 0; k < 4; ++k)
-                if (gx0 + k >= X.z && gx0 + k < X.w) o[k] = (uint8_t)(packed >> (8 * k));
+          for (int u = 0; u < PYR_U; ++u) {
+            const int r = rb + u * R;
+            if (r >= nrows) break;
+            const int y = Y.x + r;
+            *reinterpret_cast<uint32_t*>(nxt + r * dpitch + 4 * cg) = packed[u];
+            if (y >= Y.z && y < Y.w && any_x) {
+              uint8_t* o = gdst + (size_t)y * gp + gx0;
+              if (in_x) {
+                *reinterpret_cast<uint32_t*>(o) = packed[u];  // pyr offsets/pitches are 16-B multiples
+              } else {
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                  if (gx0 + k >= X.z && gx0 + k < X.w) o[k] = (uint8_t)(packed[u] >> (8 * k));
+              }
             }
           }
         }

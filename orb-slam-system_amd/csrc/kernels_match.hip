@@ -309,12 +309,23 @@ __global__ __launch_bounds__(256) void k_match_cand_rows(
   };
   const int n8 = n2 & ~7;
   for (int j0 = 0; j0 < n8; j0 += 8) {
-    // validity of these 8 positions: one wave-uniform word
+    // validity of these 8 positions: one wave-uniform word; an invalid
+    // position's key is forced to ~0 with a scalar OR mask (no branches, so
+    // all 16 LDS reads of the group stay in flight together)
     const uint32_t vw = __builtin_amdgcn_readfirstlane(svalid[j0 >> 5]) >> (j0 & 31);
+    uint4 bd[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) bd[q] = sdesc[2 * j0 + q];  // all 16 reads in flight
     uint32_t kk[8];
 #pragma unroll
-    for (int q = 0; q < 8; ++q)
-      kk[q] = ((vw >> q) & 1u) ? (((uint32_t)dist(j0 + q) << 16) | (uint32_t)(j0 + q)) : 0xFFFFFFFFu;
+    for (int q = 0; q < 8; ++q) {
+      const uint4 b0 = bd[2 * q], b1 = bd[2 * q + 1];
+      const uint32_t d = __popc(q0.x ^ b0.x) + __popc(q0.y ^ b0.y) + __popc(q0.z ^ b0.z) +
+                         __popc(q0.w ^ b0.w) + __popc(q1.x ^ b1.x) + __popc(q1.y ^ b1.y) +
+                         __popc(q1.z ^ b1.z) + __popc(q1.w ^ b1.w);
+      const uint32_t inval = ((vw >> q) & 1u) - 1u;  // 0 or 0xFFFFFFFF (uniform)
+      kk[q] = ((d << 16) | (uint32_t)(j0 + q)) | inval;
+    }
     uint32_t kmin = kk[0];
 #pragma unroll
     for (int q = 1; q < 8; ++q) kmin = min(kmin, kk[q]);
