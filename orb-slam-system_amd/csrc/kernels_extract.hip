@@ -25,6 +25,10 @@ namespace orbx {
 
 __device__ __forceinline__ int lane_id() { return __lane_id(); }
 
+// 16-B chunk as a native LLVM vector: HIP's uint4 class defeats SROA when it
+// is held in a local array (stage_region's loads would bounce through scratch).
+typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+
 __device__ __forceinline__ const uint8_t* level_base(const uint8_t* frames, size_t fstride,
                                                      size_t rstride, const uint8_t* pyr,
                                                      size_t pstride, const LevelInfo& U, int u,
@@ -123,7 +127,7 @@ __global__ __launch_bounds__(256) void k_pyramid(const uint8_t* __restrict__ fra
     const uintptr_t al = reinterpret_cast<uintptr_t>(src) | (uintptr_t)sp;
     const uint8_t* s0 = src + (size_t)cay * sp;
     if ((al & 15) == 0) {
-      stage_region<uint4, 4, 256>(cur, cpitch, s0 + cax, sp, nr, cpitch >> 4, tid);
+      stage_region<v4u, 4, 256>(cur, cpitch, s0 + cax, sp, nr, cpitch >> 4, tid);
     } else if ((al & 3) == 0) {
       const int d0 = (X.x & ~3) - cax, nd = (((X.y + 3) & ~3) - (X.x & ~3)) >> 2;
       stage_region<uint32_t, 8, 256>(cur + d0, cpitch, s0 + cax + d0, sp, nr, nd, tid);
@@ -382,7 +386,7 @@ __global__ __launch_bounds__(256) void k_fast_strips(
   const int tw = lead + st.w;           // columns in use
   {
     const uint8_t* s0 = base + (size_t)st.y * pitch + xal;
-    if (aligned16) stage_region<uint4, 4, 256>(tile, tpitch, s0, pitch, st.h, (tw + 15) >> 4, tid);
+    if (aligned16) stage_region<v4u, 4, 256>(tile, tpitch, s0, pitch, st.h, (tw + 15) >> 4, tid);
     else if (aligned) stage_region<uint32_t, 12, 256>(tile, tpitch, s0, pitch, st.h, (tw + 3) >> 2, tid);
     else stage_region<uint8_t, 16, 256>(tile, tpitch, s0, pitch, st.h, tw, tid);
   }
