@@ -204,6 +204,42 @@ int orbm_plan_match_frames(orbm_plan* mp, int npairs, const orbx_keypoint* d_kps
 int orbm_plan_set_timing(orbm_plan* mp, int enable);
 int orbm_plan_stage_times(orbm_plan* mp, double* ms, int* launches, int nstages);
 
+/* ---------------------------------------------------------------------------
+ * Stereo matcher: Frame::ComputeStereoMatches (src/Frame.cc:446-620), the
+ * consumer of the extractors' mvImagePyramid.
+ * ------------------------------------------------------------------------- */
+/* Drop-in on host keypoints: kps_l/desc_l (mvKeys / mDescriptors) and
+ * kps_r/desc_r (mvKeysRight / mDescriptorsRight) of a rectified pair whose
+ * images were the last orbx_extract of `left` and `right` (their pyramids are
+ * read on the device).  mb = baseline, mbf = baseline * fx (the reference
+ * reads the member mb before assigning it at Frame.cc:94; callers pass
+ * mbf / fx).  Outputs uright[nl] (mvuRight) and depth[nl] (mvDepth), -1 =
+ * no match; *nmatches = stereo matches kept by the median filter.
+ * ORBX_ERR_ARG where the reference would index out of range or throw. */
+int orbx_stereo_match(orbx_extractor* left, orbx_extractor* right, const orbx_keypoint* kps_l,
+                      const uint8_t* desc_l, int nl, const orbx_keypoint* kps_r,
+                      const uint8_t* desc_r, int nr, float mb, float mbf, float* uright,
+                      float* depth, int* nmatches);
+
+/* Batched device path: nframes rectified pairs.  `left` / `right` are the
+ * plans whose last orbx_plan_extract consumed d_frames_l / d_frames_r (their
+ * device pyramids are read); keypoint arrays are the orbx_plan_extract
+ * outputs ([nframes][kcap], counts [nframes]).  d_uright / d_depth are
+ * [nframes][kcap], d_nmatches [nframes].  Asynchronous on `stream`;
+ * orbs_plan_check() synchronises and reports latched range errors. */
+typedef struct orbs_plan orbs_plan;
+int orbs_plan_create(const orbx_plan* geometry, int max_batch, orbs_plan** out);
+int orbs_plan_destroy(orbs_plan* sp);
+int orbs_plan_match(orbs_plan* sp, int nframes, const orbx_plan* left, const orbx_plan* right,
+                    const uint8_t* d_frames_l, const uint8_t* d_frames_r, size_t frame_stride,
+                    size_t row_stride, const orbx_keypoint* d_kps_l, const uint8_t* d_desc_l,
+                    const int* d_count_l, const orbx_keypoint* d_kps_r, const uint8_t* d_desc_r,
+                    const int* d_count_r, float mb, float mbf, float* d_uright, float* d_depth,
+                    int* d_nmatches, void* stream);
+int orbs_plan_check(orbs_plan* sp, void* stream);
+int orbs_plan_set_timing(orbs_plan* sp, int enable);
+int orbs_plan_stage_times(orbs_plan* sp, double* ms, int* launches, int nstages);
+
 #ifdef __cplusplus
 }
 #endif

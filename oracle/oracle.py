@@ -55,6 +55,8 @@ def lib():
         L.oo_brief_descriptor.argtypes = [P, i, i, i, f, P]
         L.oo_descriptor_distance.argtypes = [P, P]
         L.oo_search_by_bow.argtypes = [i, P, P, P, i, P, P, P, i, P, P, P, i, P, P, P, f, i, P]
+        L.oo_compute_stereo_matches.argtypes = [i, P, P, i, P, P, i, P, P, P, P, P, P, P, f, f,
+                                                P, P]
         _lib = L
     return _lib
 
@@ -191,3 +193,34 @@ def search_by_bow(kf1, kf2, nnratio=0.6, check_ori=True):
                                 len(d2), _p(d2), _p(a2), _p(v2), len(n2), _p(n2), _p(o2), _p(f2),
                                 float(nnratio), 1 if check_ori else 0, _p(m))
     return m, nm
+
+
+def compute_stereo_matches(kl, dl, kr, dr, scale, inv_scale, lpyr, rpyr, mb, mbf):
+    """Frame::ComputeStereoMatches (src/Frame.cc:446-620) on one rectified pair.
+    lpyr / rpyr: lists of uint8 level images (mvImagePyramid of the left /
+    right extractor).  Returns (uRight, depth, nkept); raises OracleError
+    where the reference would index out of range or throw."""
+    kl = np.ascontiguousarray(kl, KEYPOINT_DTYPE)
+    kr = np.ascontiguousarray(kr, KEYPOINT_DTYPE)
+    dl = np.ascontiguousarray(dl, np.uint8).reshape(-1, 32)
+    dr = np.ascontiguousarray(dr, np.uint8).reshape(-1, 32)
+    scale = np.ascontiguousarray(scale, np.float32)
+    inv_scale = np.ascontiguousarray(inv_scale, np.float32)
+    L = len(lpyr)
+    lp = [np.ascontiguousarray(a, np.uint8) for a in lpyr]
+    rp = [np.ascontiguousarray(a, np.uint8) for a in rpyr]
+    for a, b in zip(lp, rp):
+        assert a.shape == b.shape
+    lptr = (ctypes.c_void_p * L)(*[a.ctypes.data for a in lp])
+    rptr = (ctypes.c_void_p * L)(*[a.ctypes.data for a in rp])
+    lw = np.array([a.shape[1] for a in lp], np.int32)
+    lh = np.array([a.shape[0] for a in lp], np.int32)
+    ur = np.zeros(len(kl), np.float32)
+    dep = np.zeros(len(kl), np.float32)
+    rc = lib().oo_compute_stereo_matches(len(kl), _p(kl), _p(dl), len(kr), _p(kr), _p(dr), L,
+                                         _p(scale), _p(inv_scale), ctypes.cast(lptr, ctypes.c_void_p),
+                                         ctypes.cast(rptr, ctypes.c_void_p), _p(lw), _p(lh), _p(lw),
+                                         float(mb), float(mbf), _p(ur), _p(dep))
+    if rc < 0:
+        raise OracleError(rc)
+    return ur, dep, rc

@@ -930,3 +930,163 @@ int oo_search_by_bow(int n1, const uint8_t* desc1, const float* angle1, const ui
   free(histbin);
   return nmatches;
 }
+
+/* ---------- Frame::ComputeStereoMatches (src/Frame.cc:446-620) ------------ */
+#define TH_HIGH 100
+
+typedef struct {
+  int first, second;
+} oo_pair;
+
+static int pair_cmp(const void* a, const void* b) { /* std::pair operator< */
+  const oo_pair* x = (const oo_pair*)a;
+  const oo_pair* y = (const oo_pair*)b;
+  if (x->first != y->first) return x->first < y->first ? -1 : 1;
+  return (x->second > y->second) - (x->second < y->second);
+}
+
+int oo_compute_stereo_matches(int nl, const oo_keypoint* kl, const uint8_t* dl, int nr,
+                              const oo_keypoint* kr, const uint8_t* dr, int nlevels,
+                              const float* scale, const float* inv_scale,
+                              const uint8_t* const* lpyr, const uint8_t* const* rpyr,
+                              const int* lw, const int* lh, const int* lstride, float mb,
+                              float mbf, float* uright, float* depth) {
+  /* :448-449 */
+  for (int i = 0; i < nl; ++i) uright[i] = depth[i] = -1.0f;
+  const int thOrbDist = (TH_HIGH + TH_LOW) / 2; /* :451 */
+  const int nRows = lh[0];                      /* :453 mvImagePyramid[0].rows */
+  /* :456-473 vRowIndices: right keypoint iR is listed in rows
+   * floor(y - r) .. ceil(y + r), r = 2 * mvScaleFactors[octave], in iR order */
+  int* rcount = (int*)calloc((size_t)nRows + 1, sizeof(int));
+  for (int iR = 0; iR < nr; ++iR) {
+    const float kpY = kr[iR].y;
+    const float r = 2.0f * scale[kr[iR].octave];
+    const int maxr = (int)ceilf(kpY + r), minr = (int)floorf(kpY - r);
+    if (minr < 0 || maxr >= nRows) { free(rcount); return OO_ERR_ARG; } /* out-of-range vector index */
+    for (int yi = minr; yi <= maxr; ++yi) rcount[yi + 1]++;
+  }
+  for (int y = 0; y < nRows; ++y) rcount[y + 1] += rcount[y];
+  int* rows = (int*)malloc(sizeof(int) * (size_t)(rcount[nRows] > 0 ? rcount[nRows] : 1));
+  int* fill = (int*)calloc((size_t)nRows, sizeof(int));
+  for (int iR = 0; iR < nr; ++iR) {
+    const float kpY = kr[iR].y;
+    const float r = 2.0f * scale[kr[iR].octave];
+    const int maxr = (int)ceilf(kpY + r), minr = (int)floorf(kpY - r);
+    for (int yi = minr; yi <= maxr; ++yi) rows[rcount[yi] + fill[yi]++] = iR;
+  }
+  free(fill);
+  /* :476-478 */
+  const float minZ = mb;
+  const float minD = 0;
+  const float maxD = mbf / minZ;
+  oo_pair* vDistIdx = (oo_pair*)malloc(sizeof(oo_pair) * (size_t)(nl > 0 ? nl : 1));
+  int nd = 0, rc = OO_OK;
+  for (int iL = 0; iL < nl; ++iL) { /* :484-606 */
+    const oo_keypoint* kpL = &kl[iL];
+    const int levelL = kpL->octave;
+    const float vL = kpL->y, uL = kpL->x;
+    const size_t row = (size_t)vL; /* vRowIndices[vL]: float -> size_t */
+    if (row >= (size_t)nRows) { rc = OO_ERR_ARG; break; }
+    const int cb = rcount[row], ce = rcount[row + 1];
+    if (cb == ce) continue;
+    const float minU = uL - maxD, maxU = uL - minD;
+    if (maxU < 0) continue;
+    int bestDist = TH_HIGH;
+    size_t bestIdxR = 0;
+    const uint8_t* dL = dl + (size_t)iL * 32;
+    for (int c = cb; c < ce; ++c) { /* :507-529 */
+      const int iR = rows[c];
+      const oo_keypoint* kpR = &kr[iR];
+      if (kpR->octave < levelL - 1 || kpR->octave > levelL + 1) continue;
+      const float uR = kpR->x;
+      if (uR >= minU && uR <= maxU) {
+        const int dist = oo_descriptor_distance(dL, dr + (size_t)iR * 32);
+        if (dist < bestDist) {
+          bestDist = dist;
+          bestIdxR = (size_t)iR;
+        }
+      }
+    }
+    if (bestDist < thOrbDist) { /* :532-605 */
+      const float uR0 = kr[bestIdxR].x;
+      const float scaleFactor = inv_scale[kpL->octave];
+      const float scaleduL = roundf(kpL->x * scaleFactor);
+      const float scaledvL = roundf(kpL->y * scaleFactor);
+      const float scaleduR0 = roundf(uR0 * scaleFactor);
+      const int w = 5, L = 5;
+      const int o = kpL->octave;
+      if (o < 0 || o >= nlevels) { rc = OO_ERR_ARG; break; }
+      const int W = lw[o], H = lh[o], st = lstride[o];
+      const int y0 = (int)scaledvL - w, xl0 = (int)scaleduL - w;
+      /* IL = rowRange(y0, y0+11).colRange(xl0, xl0+11): cv asserts in range */
+      if (y0 < 0 || y0 + 2 * w + 1 > H || xl0 < 0 || xl0 + 2 * w + 1 > W) { rc = OO_ERR_ARG; break; }
+      const uint8_t* IL = lpyr[o] + (size_t)y0 * st + xl0;
+      const int cL = IL[w * st + w];
+      int bestSad = INT_MAX; /* :552 int bestDist = INT_MAX */
+      int bestincR = 0;
+      float vDists[2 * 5 + 1];
+      const float iniu = scaleduR0 + L - w;
+      const float endu = scaleduR0 + L + w + 1;
+      if (iniu < 0 || endu >= W) continue; /* :562-563 (right level has the same size) */
+      const int xr_lo = (int)scaleduR0 - L - w, xr_hi = (int)scaleduR0 + L + w + 1;
+      if (xr_lo < 0 || xr_hi > W) { rc = OO_ERR_ARG; break; } /* colRange assertion */
+      for (int incR = -L; incR <= L; ++incR) { /* :565-578 */
+        const uint8_t* IR = rpyr[o] + (size_t)y0 * st + ((int)scaleduR0 + incR - w);
+        const int cR = IR[w * st + w];
+        int sad = 0; /* cv::norm(IL, IR, NORM_L1) of the centred float patches: exact */
+        for (int yy = 0; yy < 2 * w + 1; ++yy)
+          for (int xx = 0; xx < 2 * w + 1; ++xx) {
+            const int d = (IL[yy * st + xx] - cL) - (IR[yy * st + xx] - cR);
+            sad += d < 0 ? -d : d;
+          }
+        const float dist = (float)sad;
+        if (dist < (float)bestSad) {
+          bestSad = (int)dist;
+          bestincR = incR;
+        }
+        vDists[L + incR] = dist;
+      }
+      if (bestincR == -L || bestincR == L) continue; /* :580-581 */
+      const float dist1 = vDists[L + bestincR - 1]; /* :584-588 */
+      const float dist2 = vDists[L + bestincR];
+      const float dist3 = vDists[L + bestincR + 1];
+      const float deltaR = (dist1 - dist3) / (2.0f * (dist1 + dist3 - 2.0f * dist2));
+      if (deltaR < -1 || deltaR > 1) continue;
+      float bestuR = scale[kpL->octave] * ((float)scaleduR0 + (float)bestincR + deltaR); /* :594 */
+      float disparity = (uL - bestuR);
+      if (disparity >= minD && disparity < maxD) { /* :598-611 */
+        if (disparity <= 0) {
+          disparity = 0.01;
+          bestuR = uL - 0.01; /* double arithmetic, stored as float */
+        }
+        depth[iL] = mbf / disparity;
+        uright[iL] = bestuR;
+        vDistIdx[nd].first = bestSad;
+        vDistIdx[nd].second = iL;
+        nd++;
+      }
+    }
+  }
+  free(rows);
+  free(rcount);
+  if (rc != OO_OK) {
+    free(vDistIdx);
+    return rc;
+  }
+  /* :615-631 median filter; an empty vDistIdx reads past the end in the
+   * reference but then removes nothing -- the same as skipping */
+  int nvalid = nd;
+  if (nd > 0) {
+    qsort(vDistIdx, (size_t)nd, sizeof(oo_pair), pair_cmp);
+    const float median = (float)vDistIdx[nd / 2].first;
+    const float thDist = 1.5f * 1.4f * median;
+    for (int i = nd - 1; i >= 0; i--) {
+      if ((float)vDistIdx[i].first < thDist) break;
+      uright[vDistIdx[i].second] = -1;
+      depth[vDistIdx[i].second] = -1;
+      nvalid--;
+    }
+  }
+  free(vDistIdx);
+  return nvalid;
+}

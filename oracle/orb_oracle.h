@@ -92,6 +92,21 @@ int oo_search_by_bow(int n1, const uint8_t* desc1, const float* angle1, const ui
                      const uint32_t* off2, const uint32_t* feat2, float nnratio, int check_ori,
                      int32_t* match12);
 
+/* Frame::ComputeStereoMatches (src/Frame.cc:446-620).  Left/right keypoints
+ * and descriptors of one rectified pair; lpyr/rpyr[l] = mvImagePyramid[l] of
+ * the left/right extractor (both of size lw[l] x lh[l], rows lstride[l]);
+ * scale/inv_scale = mvScaleFactors / mvInvScaleFactors; mb and mbf as the
+ * Frame members (the reference reads mb before assigning it, Frame.cc:70 vs
+ * :94 -- callers pass mbf/fx).  Outputs mvuRight/mvDepth (-1 = none).
+ * Returns the number of stereo matches kept, or OO_ERR_ARG where the
+ * reference would index out of range or throw (cv::Mat range asserts). */
+int oo_compute_stereo_matches(int nl, const oo_keypoint* kl, const uint8_t* dl, int nr,
+                              const oo_keypoint* kr, const uint8_t* dr, int nlevels,
+                              const float* scale, const float* inv_scale,
+                              const uint8_t* const* lpyr, const uint8_t* const* rpyr,
+                              const int* lw, const int* lh, const int* lstride, float mb,
+                              float mbf, float* uright, float* depth);
+
 #ifdef __cplusplus
 }
 #endif

@@ -23,6 +23,9 @@ enum {
   ORBX_STAGE_MCAND,
   ORBX_STAGE_MRESOLVE,
   ORBX_STAGE_MFINAL,
+  ORBX_STAGE_SROWS,
+  ORBX_STAGE_SMATCH,
+  ORBX_STAGE_SFILTER,
   ORBX_NSTAGES
 };
 

@@ -12,6 +12,7 @@
 #include "../../include/orbx.h"
 #include "api_common.h"
 #include "geometry.h"
+#include "plan_internal.h"
 
 namespace orbx {
 __global__ void k_pyramid(const uint8_t*, size_t, size_t, uint8_t*, size_t, const PyrSeg,
@@ -32,7 +33,8 @@ using namespace orbx;
 
 static const char* kStageNames[ORBX_NSTAGES] = {
     "resize", "fast_cells", "quadtree", "blur", "orient_brief",
-    "match_select", "match_candidates", "match_resolve", "match_finalize"};
+    "match_select", "match_candidates", "match_resolve", "match_finalize",
+    "stereo_rows", "stereo_match", "stereo_filter"};
 
 extern "C" int orbx_abi_version(void) { return ORBX_ABI_VERSION; }
 
@@ -111,30 +113,6 @@ extern "C" int orbx_resize_tables(const orbx_params* p, int width, int height, i
 // ---------------------------------------------------------------------------
 // orbx_plan
 // ---------------------------------------------------------------------------
-struct orbx_plan {
-  Plan P;
-  int device = 0, max_batch = 0;
-  hipStream_t stream = nullptr;
-  LevelInfo* d_lv = nullptr;
-  CellInfo* d_cells = nullptr;
-  StripInfo* d_strips = nullptr;
-  int fs_tpitch = 0, fs_tmaxh = 0, fs_qcap = 0, fs_mcells = 0;
-  size_t fs_lds = 0;
-  int32_t *d_xofs = nullptr, *d_xofs1 = nullptr, *d_yofs = nullptr;
-  int32_t *d_pyr_xs = nullptr, *d_pyr_ys = nullptr, *d_pyr_bo = nullptr;
-  uint32_t* d_pyr_blob = nullptr;
-  int16_t *d_alpha = nullptr, *d_beta = nullptr;
-  uint8_t *d_pyr = nullptr, *d_blur = nullptr;
-  uint32_t *d_slots = nullptr, *d_ccount = nullptr, *d_qkeys = nullptr, *d_qout = nullptr;
-  int32_t* d_qnode = nullptr;
-  int *d_lcount = nullptr, *d_err = nullptr;
-  size_t pyr_stride = 0, blur_stride = 0, slot_stride = 0, qk_stride = 0, qout_stride = 0;
-  size_t qt_lds = 0;
-  BriefArgs bargs;
-  LevelArgs largs;
-  StageTimer timer;
-  int dbg = 0; /* ORBX_DEBUG_STOP: kernel phase early-exit for profiling only */
-};
 
 static size_t round_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 
@@ -361,20 +339,10 @@ extern "C" int orbx_synth_frames(uint8_t* d_frames, int W, int H, size_t fstride
 // ---------------------------------------------------------------------------
 // orbx_extractor: the ORBextractor::operator() drop-in (host buffers).
 // ---------------------------------------------------------------------------
-struct orbx_extractor {
-  orbx_params params;
-  int device = 0;
-  orbx_plan* plan = nullptr;
-  int W = 0, H = 0;
-  uint8_t* d_img = nullptr;
-  orbx_keypoint* d_kps = nullptr;
-  uint8_t* d_desc = nullptr;
-  int* d_count = nullptr;
-  bool have_frame = false;
-};
 
 static void extractor_release_plan(orbx_extractor* e) {
   hipSetDevice(e->device);
+  orbx_stereo_release(e);
   if (e->plan) orbx_plan_destroy(e->plan);
   if (e->d_img) hipFree(e->d_img);
   if (e->d_kps) hipFree(e->d_kps);

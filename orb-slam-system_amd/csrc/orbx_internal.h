@@ -83,6 +83,19 @@ struct LevelArgs {
 };
 #define ORBX_STRIP_MAXCELLS 64 /* cells per FAST strip (>= 256 / min cell width) */
 
+/* per-level constants of the stereo matcher (Frame::ComputeStereoMatches),
+ * passed by value.  Left and right plans share the geometry: the storage of
+ * level l is the caller's frame when off[l] < 0, else pyr + off[l]. */
+struct StereoArgs {
+  int nlevels, nrows, kcap, rcap; /* nrows = level-0 height; rcap = row-list entries per frame */
+  long long off[ORBX_MAX_LEVELS];
+  int pitch[ORBX_MAX_LEVELS], w[ORBX_MAX_LEVELS], h[ORBX_MAX_LEVELS];
+  float scale[ORBX_MAX_LEVELS], inv_scale[ORBX_MAX_LEVELS];
+  float mb, mbf;
+};
+#define ORBX_DEVERR_STEREO 4 /* the reference would index out of range / throw */
+#define ORBX_STEREO_MAXROWS 8192
+
 /* per-level constants of k_orient_brief, passed by value (kernel arguments
  * live in SGPRs: no dependent global loads to find a keypoint's level) */
 struct BriefArgs {

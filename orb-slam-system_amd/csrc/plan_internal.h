@@ -1,0 +1,54 @@
+// plan_internal.h -- host-side state of an extraction plan and of the
+// ORBextractor drop-in, shared by the C-ABI translation units (the stereo
+// matcher reads the device pyramid the extractor left behind).
+#ifndef ORBX_PLAN_INTERNAL_H
+#define ORBX_PLAN_INTERNAL_H
+
+#include <hip/hip_runtime.h>
+
+#include "../../include/orbx.h"
+#include "api_common.h"
+#include "geometry.h"
+
+struct orbx_plan {
+  orbx::Plan P;
+  int device = 0, max_batch = 0;
+  hipStream_t stream = nullptr;
+  LevelInfo* d_lv = nullptr;
+  CellInfo* d_cells = nullptr;
+  StripInfo* d_strips = nullptr;
+  int fs_tpitch = 0, fs_tmaxh = 0, fs_qcap = 0, fs_mcells = 0;
+  size_t fs_lds = 0;
+  int32_t *d_xofs = nullptr, *d_xofs1 = nullptr, *d_yofs = nullptr;
+  int32_t *d_pyr_xs = nullptr, *d_pyr_ys = nullptr, *d_pyr_bo = nullptr;
+  uint32_t* d_pyr_blob = nullptr;
+  int16_t *d_alpha = nullptr, *d_beta = nullptr;
+  uint8_t *d_pyr = nullptr, *d_blur = nullptr;
+  uint32_t *d_slots = nullptr, *d_ccount = nullptr, *d_qkeys = nullptr, *d_qout = nullptr;
+  int32_t* d_qnode = nullptr;
+  int *d_lcount = nullptr, *d_err = nullptr;
+  size_t pyr_stride = 0, blur_stride = 0, slot_stride = 0, qk_stride = 0, qout_stride = 0;
+  size_t qt_lds = 0;
+  BriefArgs bargs;
+  LevelArgs largs;
+  orbx::StageTimer timer;
+  int dbg = 0; /* ORBX_DEBUG_STOP: kernel phase early-exit for profiling only */
+};
+
+struct orbx_extractor {
+  orbx_params params;
+  int device = 0;
+  orbx_plan* plan = nullptr;
+  int W = 0, H = 0;
+  uint8_t* d_img = nullptr;
+  orbx_keypoint* d_kps = nullptr;
+  uint8_t* d_desc = nullptr;
+  int* d_count = nullptr;
+  bool have_frame = false;
+  void* stereo = nullptr; /* orbs_plan of orbx_stereo_match (api_stereo.hip) */
+};
+
+/* frees the stereo scratch an extractor owns (api_stereo.hip) */
+void orbx_stereo_release(orbx_extractor* e);
+
+#endif

@@ -5,6 +5,7 @@ reference interfaces for tests and the benchmark:
 
   Extractor      ORB_SLAM2::ORBextractor  (/root/reference/include/ORBextractor.h:25-91)
   search_by_bow  ORBmatcher::SearchByBoW(KF, KF) (/root/reference/src/ORBmatcher.cc:278-366)
+  compute_stereo_matches  Frame::ComputeStereoMatches (/root/reference/src/Frame.cc:446-620)
   descriptor_distance_batch  ORBmatcher::DescriptorDistance (ORBmatcher.cc:896-908)
   Plan / MatchPlan  batched device-resident throughput path (bench.py)
 
@@ -48,6 +49,8 @@ EXPORTED = [
     "orbx_plan_stage_times", "orbx_synth_frames", "orbm_search_by_bow",
     "orbm_descriptor_distance_batch", "orbm_plan_create", "orbm_plan_destroy",
     "orbm_plan_match_frames", "orbm_plan_set_timing", "orbm_plan_stage_times",
+    "orbx_stereo_match", "orbs_plan_create", "orbs_plan_destroy", "orbs_plan_match",
+    "orbs_plan_check", "orbs_plan_set_timing", "orbs_plan_stage_times",
 ]
 
 
@@ -108,6 +111,13 @@ _sig = {
     "orbm_plan_match_frames": (I, [P, I, P, P, P, P, P, P, F, I, P, P, P]),
     "orbm_plan_set_timing": (I, [P, I]),
     "orbm_plan_stage_times": (I, [P, P, P, I]),
+    "orbx_stereo_match": (I, [P, P, P, P, I, P, P, I, F, F, P, P, P]),
+    "orbs_plan_create": (I, [P, I, P]),
+    "orbs_plan_destroy": (I, [P]),
+    "orbs_plan_match": (I, [P, I, P, P, P, P, SZ, SZ, P, P, P, P, P, P, F, F, P, P, P, P]),
+    "orbs_plan_check": (I, [P, P]),
+    "orbs_plan_set_timing": (I, [P, I]),
+    "orbs_plan_stage_times": (I, [P, P, P, I]),
 }
 for _n, (_r, _a) in _sig.items():
     _f = getattr(_lib, _n)
@@ -234,6 +244,24 @@ class Extractor:
         out = np.zeros((h.value, w.value), np.uint8)
         _check(_lib.orbx_extractor_level(self._h, l, _p(out), w.value, None, None))
         return out
+
+
+# --------------------------------------------------------------------------- stereo
+def compute_stereo_matches(left, right, kps_l, desc_l, kps_r, desc_r, mb, mbf):
+    """Frame::ComputeStereoMatches (Frame.cc:446-620) for the pair whose images
+    were the last extract() of Extractor `left` and `right` (their pyramids
+    stay on the device).  Returns (mvuRight f32[N], mvDepth f32[N], nmatches)."""
+    kl = np.ascontiguousarray(kps_l, KEYPOINT_DTYPE)
+    kr = np.ascontiguousarray(kps_r, KEYPOINT_DTYPE)
+    dl = np.ascontiguousarray(desc_l, np.uint8).reshape(-1, 32)
+    dr = np.ascontiguousarray(desc_r, np.uint8).reshape(-1, 32)
+    ur = np.full(max(len(kl), 1), -1, np.float32)
+    dep = np.full(max(len(kl), 1), -1, np.float32)
+    nm = ctypes.c_int(0)
+    _check(_lib.orbx_stereo_match(left._h, right._h, _p(kl), _p(dl), len(kl), _p(kr), _p(dr),
+                                  len(kr), float(mb), float(mbf), _p(ur), _p(dep),
+                                  ctypes.byref(nm)), "orbx_stereo_match")
+    return ur[:len(kl)].copy(), dep[:len(kl)].copy(), nm.value
 
 
 # --------------------------------------------------------------------------- ORBmatcher
@@ -376,6 +404,53 @@ class MatchPlan:
         ms = np.zeros(n, np.float64)
         cnt = np.zeros(n, np.int32)
         _check(_lib.orbm_plan_stage_times(self._h, _p(ms), _p(cnt), n))
+        return {name: (ms[i], int(cnt[i])) for i, name in enumerate(stage_names())}
+
+
+class StereoPlan:
+    """Batched device stereo matcher (Frame::ComputeStereoMatches) over the
+    outputs and pyramids of a left and a right Plan of the same geometry."""
+
+    def __init__(self, plan, max_batch=None, device=0):
+        import torch
+        max_batch = max_batch or plan.max_batch
+        h = ctypes.c_void_p()
+        _check(_lib.orbs_plan_create(plan._h, max_batch, ctypes.byref(h)), "orbs_plan_create")
+        self._h, self.kcap, self.max_batch = h, plan.kcap, max_batch
+        dev = torch.device("cuda", device)
+        self.uright = torch.empty((max_batch, max(self.kcap, 1)), dtype=torch.float32, device=dev)
+        self.depth = torch.empty((max_batch, max(self.kcap, 1)), dtype=torch.float32, device=dev)
+        self.nmatches = torch.zeros(max_batch, dtype=torch.int32, device=dev)
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            _lib.orbs_plan_destroy(self._h)
+            self._h = None
+
+    def match(self, left, right, frames_l, frames_r, mb, mbf, left_out=None, right_out=None,
+              stream=None):
+        """frames_*: the cuda [B, H, W] tensors the plans last extracted.  Async."""
+        B = frames_l.shape[0]
+        kl, dl, cl = left_out if left_out is not None else (left.kps, left.desc, left.counts)
+        kr, dr, cr = right_out if right_out is not None else (right.kps, right.desc, right.counts)
+        _check(_lib.orbs_plan_match(self._h, B, left._h, right._h, frames_l.data_ptr(),
+                                    frames_r.data_ptr(), left.W * left.H, left.W, kl.data_ptr(),
+                                    dl.data_ptr(), cl.data_ptr(), kr.data_ptr(), dr.data_ptr(),
+                                    cr.data_ptr(), float(mb), float(mbf), self.uright.data_ptr(),
+                                    self.depth.data_ptr(), self.nmatches.data_ptr(),
+                                    _stream_handle(stream)), "orbs_plan_match")
+
+    def check(self, stream=None):
+        _check(_lib.orbs_plan_check(self._h, _stream_handle(stream)), "orbs_plan_check")
+
+    def set_timing(self, enable):
+        _check(_lib.orbs_plan_set_timing(self._h, 1 if enable else 0))
+
+    def stage_times(self):
+        n = _lib.orbx_stage_count()
+        ms = np.zeros(n, np.float64)
+        cnt = np.zeros(n, np.int32)
+        _check(_lib.orbs_plan_stage_times(self._h, _p(ms), _p(cnt), n))
         return {name: (ms[i], int(cnt[i])) for i, name in enumerate(stage_names())}
 
 

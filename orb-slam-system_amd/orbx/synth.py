@@ -58,5 +58,36 @@ def frame(w, h, frame_idx, kind="rects"):
     return np.clip(img + noise, 0, 255).astype(np.uint8)
 
 
+def stereo_pair(w, h, frame_idx, max_disp=64):
+    """Rectified synthetic stereo pair (left, right) for the stereo matcher.
+
+    Same scene model as ``frame(kind="rects")`` with a disparity per object:
+    rectangle r (stream elements 5r..5r+4 as in rects) is seen at x - d_r in
+    the right image, d_r = element 480 + r mod max_disp; the background
+    gradient has disparity 2.  Noise: left element 576 + y*W + x, right
+    element 576 + W*H + y*W + x (mod 13, minus 6), independent per image.
+    """
+    seed = SEED_BASE + frame_idx
+    x = np.arange(w, dtype=np.int64)
+    bgl = 64 + (128 * x) // max(w - 1, 1)
+    bgr = 64 + (128 * (x + 2)) // max(w - 1, 1)
+    L = np.broadcast_to(bgl, (h, w)).astype(np.int32).copy()
+    R = np.broadcast_to(bgr, (h, w)).astype(np.int32).copy()
+    r = stream(seed, 0, 5 * 96).reshape(96, 5)
+    disp = stream(seed, 480, 96) % np.uint64(max_disp)
+    for (x0, x1, y0, y1, v), d in zip(r, disp):
+        x0, x1 = int(x0 % np.uint64(w)), int(x1 % np.uint64(w))
+        y0, y1 = int(y0 % np.uint64(h)), int(y1 % np.uint64(h))
+        xa, xb, ya, yb, d = min(x0, x1), max(x0, x1), min(y0, y1), max(y0, y1), int(d)
+        val = int(v % np.uint64(256))
+        L[ya:yb + 1, xa:xb + 1] = val
+        ra, rb = max(xa - d, 0), xb - d
+        if rb >= 0:
+            R[ya:yb + 1, ra:rb + 1] = val
+    nl = (stream(seed, 576, w * h) % np.uint64(13)).astype(np.int32).reshape(h, w) - 6
+    nr = (stream(seed, 576 + w * h, w * h) % np.uint64(13)).astype(np.int32).reshape(h, w) - 6
+    return (np.clip(L + nl, 0, 255).astype(np.uint8), np.clip(R + nr, 0, 255).astype(np.uint8))
+
+
 def frames(w, h, first_idx, count, kind="rects"):
     return np.stack([frame(w, h, first_idx + i, kind) for i in range(count)])

@@ -86,5 +86,28 @@ def main():
     print("search_by_bow", {k: int(v[0]) for k, v in res.items() if k.startswith("n_")})
 
 
+def stereo():
+    """Frame::ComputeStereoMatches on a KITTI-shaped synthetic pair (config 5)."""
+    O.build()
+    w, h, nf, idx = 1241, 376, 2000, 300
+    fx, mbf = 718.856, 386.1448
+    L, R = synth.stereo_pair(w, h, idx)
+    el, er = O.Extractor(nf, 1.2, 8, 20, 7), O.Extractor(nf, 1.2, 8, 20, 7)
+    kl, dl = el.extract(L)
+    kr, dr = er.extract(R)
+    t = el.tables()
+    ur, dep, n = O.compute_stereo_matches(kl, dl, kr, dr, t["scale"], t["inv_scale"],
+                                          [el.level(l) for l in range(8)],
+                                          [er.level(l) for l in range(8)], mbf / fx, mbf)
+    np.savez_compressed(os.path.join(OUT, "stereo_c5_1241x376.npz"), kl=kl.view(np.uint8),
+                        uright=ur, depth=dep, n=np.array(n), mb=np.float32(mbf / fx),
+                        mbf=np.float32(mbf), spec=np.array([w, h, nf, idx], np.int64))
+    print("stereo", len(kl), len(kr), n)
+
+
 if __name__ == "__main__":
-    main()
+    if len(sys.argv) > 1 and sys.argv[1] == "stereo":
+        stereo()
+    else:
+        main()
+        stereo()
