@@ -3,6 +3,7 @@
 //
 //   orbx::ORBextractor  <->  ORB_SLAM2::ORBextractor  (reference include/ORBextractor.h:25-91)
 //   orbx::ORBmatcher    <->  ORB_SLAM2::ORBmatcher    (reference include/ORBmatcher.h:16-81)
+//   orbx::ComputeStereoMatches <-> Frame::ComputeStereoMatches (reference src/Frame.cc:446-620)
 //
 // Same constructor arguments, same getters, same operator() contract
 // (keypoints cleared and refilled level-major; untouched when no keypoint
@@ -119,6 +120,8 @@ class ORBextractor {
     return im;
   }
 
+  orbx_extractor* handle() const { return h_; }
+
  private:
   orbx_params prm_;
   orbx_extractor* h_ = nullptr;
@@ -214,6 +217,29 @@ class ORBmatcher {
   bool mbCheckOrientation;
   int device_;
 };
+
+// Frame::ComputeStereoMatches (src/Frame.cc:446-620) for a rectified pair
+// whose images were the last operator() calls of `left` and `right` (the
+// pyramids they left on the device are read there).  mb = baseline,
+// mbf = baseline * fx.  Fills mvuRight / mvDepth (-1 = no match) and returns
+// the number of stereo matches the median filter kept.
+inline int ComputeStereoMatches(ORBextractor& left, ORBextractor& right,
+                                const std::vector<KeyPoint>& keysL,
+                                const std::vector<uint8_t>& descL,
+                                const std::vector<KeyPoint>& keysR,
+                                const std::vector<uint8_t>& descR, float mb, float mbf,
+                                std::vector<float>& uRight, std::vector<float>& depth) {
+  uRight.assign(keysL.size(), -1.0f);  // :448-449
+  depth.assign(keysL.size(), -1.0f);
+  int n = 0;
+  check(orbx_stereo_match(left.handle(), right.handle(),
+                          reinterpret_cast<const orbx_keypoint*>(keysL.data()), descL.data(),
+                          (int)keysL.size(), reinterpret_cast<const orbx_keypoint*>(keysR.data()),
+                          descR.data(), (int)keysR.size(), mb, mbf, uRight.data(), depth.data(),
+                          &n),
+        "ComputeStereoMatches");
+  return n;
+}
 
 }  // namespace orbx
 

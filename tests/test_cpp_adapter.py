@@ -53,3 +53,43 @@ def test_cpp_adapter_matches_oracle(gpu, oracle, tmp_path):
     rm, rnm = oracle.search_by_bow(one(rk1, rd1), one(rk2, rd2), 0.75, True)
     assert nm == rnm and np.array_equal(m12, rm)
     assert d01 == oracle.descriptor_distance(rd1[0], rd2[0])
+
+
+def _build_stereo(tmp_path):
+    exe = tmp_path / "stereo_main"
+    subprocess.check_call(["g++", "-O2", "-std=c++17", "-I", os.path.join(PKG, "cpp"),
+                           os.path.join(ROOT, "tests", "cpp", "stereo_main.cpp"), "-o", str(exe),
+                           "-L", PKG, "-lorbx", "-Wl,-rpath," + PKG])
+    return exe
+
+
+def test_cpp_stereo_adapter_compiles(tmp_path):
+    assert _build_stereo(tmp_path).exists()
+
+
+@pytest.mark.gpu
+def test_cpp_stereo_adapter_matches_oracle(gpu, oracle, tmp_path):
+    exe = _build_stereo(tmp_path)
+    W, H, nf, fx, bf = 1241, 376, 2000, 718.856, 386.1448
+    L, R = synth.stereo_pair(W, H, 60)
+    (tmp_path / "l.raw").write_bytes(L.tobytes())
+    (tmp_path / "r.raw").write_bytes(R.tobytes())
+    out = tmp_path / "out.bin"
+    subprocess.check_call([str(exe), str(tmp_path / "l.raw"), str(tmp_path / "r.raw"), str(W),
+                           str(H), str(nf), repr(fx), repr(bf), str(out)])
+    raw = out.read_bytes()
+    nl, nr, n = np.frombuffer(raw[:12], np.int32).tolist()
+    ur = np.frombuffer(raw[12:12 + 4 * nl], np.float32)
+    dep = np.frombuffer(raw[12 + 4 * nl:12 + 8 * nl], np.float32)
+    el, er = oracle.Extractor(nf, 1.2, 8, 20, 7), oracle.Extractor(nf, 1.2, 8, 20, 7)
+    kl, dl = el.extract(L)
+    kr, dr = er.extract(R)
+    assert (nl, nr) == (len(kl), len(kr))
+    t = el.tables()
+    mb = np.float32(np.float32(bf) / np.float32(fx))
+    ur0, dep0, n0 = oracle.compute_stereo_matches(kl, dl, kr, dr, t["scale"], t["inv_scale"],
+                                                  [el.level(l) for l in range(8)],
+                                                  [er.level(l) for l in range(8)], mb, np.float32(bf))
+    assert n == n0
+    assert np.array_equal(ur.view(np.uint32), ur0.view(np.uint32))
+    assert np.array_equal(dep.view(np.uint32), dep0.view(np.uint32))
