@@ -240,6 +240,49 @@ int orbs_plan_check(orbs_plan* sp, void* stream);
 int orbs_plan_set_timing(orbs_plan* sp, int enable);
 int orbs_plan_stage_times(orbs_plan* sp, double* ms, int* launches, int nstages);
 
+/* ---------------------------------------------------------------------------
+ * DBoW2 vocabulary transform: the producer of the
+ * FeatureVectors SearchByBoW consumes (Frame::ComputeBoW / KeyFrame::ComputeBoW,
+ * src/Frame.cc:375-382, src/KeyFrame.cc:39-48, levelsup = 4).
+ *   TemplatedVocabulary<FORB::TDescriptor, FORB>
+ *     loadFromTextFile     Thirdparty/DBoW2/DBoW2/TemplatedVocabulary.h:1338-1424
+ *     transform(features, BowVector&, FeatureVector&, levelsup)          :1126-1191
+ *     transform(feature, word, weight, nid, levelsup)                    :1222-1259
+ * ------------------------------------------------------------------------- */
+typedef struct orbv_vocab orbv_vocab;
+/* Text vocabulary (ORBvoc.txt format): "k L scoring weighting" then one node
+ * per line "parent isLeaf d0..d31 weight".  ORBX_ERR_ARG for a rejected
+ * header (:1356-1360) or a parent that does not precede its child. */
+int orbv_vocab_load_text(const char* path, int device, orbv_vocab** out);
+/* The same from node records (record r = node r+1 in file order). */
+int orbv_vocab_create(int k, int L, int scoring, int weighting, int nrec, const int32_t* parent,
+                      const int32_t* is_leaf, const uint8_t* desc, const double* weight,
+                      int device, orbv_vocab** out);
+int orbv_vocab_destroy(orbv_vocab* v);
+int orbv_vocab_info(const orbv_vocab* v, int* k, int* L, int* scoring, int* weighting,
+                    int* nnodes, int* nwords);
+/* transform(features, BowVector&, FeatureVector&, levelsup) on host
+ * descriptors desc[n][32].  BowVector: bow_word[nbow] ascending with
+ * bow_value[nbow] (WordValue = double, normalised as the scoring requires);
+ * FeatureVector (DBoW2::FeatureVector, FeatureVector.h:21-22) as CSR:
+ * fv_node[nfv] ascending, features fv_feat[fv_off[j] .. fv_off[j+1]) in
+ * ascending index order -- exactly the orbx_bow_frame layout.  Outputs hold
+ * n entries (fv_off n + 1).  ORBX_ERR_ARG where the reference would read an
+ * uninitialised NodeId (a leaf above the levelsup level); at most 8192
+ * descriptors per call (ORBX_ERR_UNSUPPORTED beyond). */
+int orbv_transform(orbv_vocab* v, const uint8_t* desc, int n, int levelsup, uint32_t* bow_word,
+                   double* bow_value, int* nbow, uint32_t* fv_node, uint32_t* fv_off,
+                   uint32_t* fv_feat, int* nfv);
+/* Batched device form over orbx_plan_extract outputs: d_desc [nframes][kcap][32],
+ * d_counts [nframes]; outputs [nframes][kcap] (d_fv_off [nframes][kcap+1]) and
+ * counts [nframes].  Asynchronous on `stream`; orbv_check() synchronises and
+ * reports the latched unset-NodeId error. */
+int orbv_transform_batch(orbv_vocab* v, int nframes, const uint8_t* d_desc, const int* d_counts,
+                         int kcap, int levelsup, uint32_t* d_bow_word, double* d_bow_value,
+                         int* d_nbow, uint32_t* d_fv_node, uint32_t* d_fv_off, uint32_t* d_fv_feat,
+                         int* d_nfv, void* stream);
+int orbv_check(orbv_vocab* v, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -55,6 +55,11 @@ def lib():
         L.oo_brief_descriptor.argtypes = [P, i, i, i, f, P]
         L.oo_descriptor_distance.argtypes = [P, P]
         L.oo_search_by_bow.argtypes = [i, P, P, P, i, P, P, P, i, P, P, P, i, P, P, P, f, i, P]
+        L.oo_vocab_from_records.restype = P
+        L.oo_vocab_from_records.argtypes = [i, i, i, i, i, P, P, P, P]
+        L.oo_vocab_destroy.argtypes = [P]
+        L.oo_vocab_info.argtypes = [P, P, P, P, P, P, P]
+        L.oo_vocab_transform.argtypes = [P, P, i, i, P, P, P, P, P, P, P]
         L.oo_compute_stereo_matches.argtypes = [i, P, P, i, P, P, i, P, P, P, P, P, P, P, f, f,
                                                 P, P]
         _lib = L
@@ -82,8 +87,11 @@ class Extractor:
             raise ValueError("bad extractor parameters")
 
     def __del__(self):
-        if getattr(self, "_h", None):
-            lib().oo_destroy(self._h)
+        if getattr(self, "_h", None) and _lib is not None:
+            try:
+                lib().oo_destroy(self._h)
+            except TypeError:  # interpreter teardown
+                pass
             self._h = None
 
     def tables(self):
@@ -224,3 +232,92 @@ def compute_stereo_matches(kl, dl, kr, dr, scale, inv_scale, lpyr, rpyr, mb, mbf
     if rc < 0:
         raise OracleError(rc)
     return ur, dep, rc
+
+
+def parse_vocabulary_text(path):
+    """TemplatedVocabulary::loadFromTextFile (TemplatedVocabulary.h:1338-1424)
+    on the text: header "k L scoring weighting", node records "parent isLeaf
+    d0..d31 weight".  Failed extractions give 0 (C++11 operator>>); blank
+    lines are skipped (the reference turns a trailing one into a phantom root
+    child with an uninitialised descriptor -- see DESIGN.md)."""
+    with open(path) as f:
+        lines = f.read().split("\n")
+
+    def num(tok, cast):
+        try:
+            return cast(tok), True
+        except (ValueError, IndexError):
+            return cast(0), False
+
+    hdr = lines[0].split()
+    head = []
+    for j in range(4):
+        v, ok = num(hdr[j] if j < len(hdr) else "", int)
+        head.append(v)
+    parent, leaf, desc, weight = [], [], [], []
+    for ln in lines[1:]:
+        t = ln.split()
+        if not t:
+            continue
+        vals, ok = [], True
+        for j in range(34):
+            if ok:
+                v, ok = num(t[j] if j < len(t) else "", int)
+            else:
+                v = 0
+            vals.append(v)
+        w = 0.0
+        if ok and len(t) > 34:
+            w, _ = num(t[34], float)
+        parent.append(vals[0])
+        leaf.append(vals[1])
+        desc.append([x & 0xFF for x in vals[2:34]])
+        weight.append(w)
+    return dict(k=head[0], L=head[1], scoring=head[2], weighting=head[3],
+                parent=np.array(parent, np.int32), is_leaf=np.array(leaf, np.int32),
+                desc=np.array(desc, np.uint8).reshape(-1, 32), weight=np.array(weight, np.float64))
+
+
+class Vocabulary:
+    """CPU restatement of DBoW2::TemplatedVocabulary<FORB> (load + transform)."""
+
+    def __init__(self, voc, scoring=0, weighting=0):
+        self.voc = voc
+        parent = np.ascontiguousarray(voc["parent"], np.int32)
+        leaf = np.ascontiguousarray(voc["is_leaf"], np.int32)
+        desc = np.ascontiguousarray(voc["desc"], np.uint8)
+        w = np.ascontiguousarray(voc["weight"], np.float64)
+        self._keep = (parent, leaf, desc, w)
+        self._h = lib().oo_vocab_from_records(voc["k"], voc["L"], scoring, weighting, len(parent),
+                                              _p(parent), _p(leaf), _p(desc), _p(w))
+        if not self._h:
+            raise OracleError(OO_ERR_ARG)
+
+    @classmethod
+    def load_text(cls, path):
+        v = parse_vocabulary_text(path)
+        return cls(v, v["scoring"], v["weighting"])
+
+    def __del__(self):
+        if getattr(self, "_h", None) and _lib is not None:
+            try:
+                lib().oo_vocab_destroy(self._h)
+            except TypeError:  # interpreter teardown
+                pass
+            self._h = None
+
+    def transform(self, desc, levelsup=4):
+        d = np.ascontiguousarray(desc, np.uint8).reshape(-1, 32)
+        n = len(d)
+        m = max(n, 1)
+        bw, bv = np.zeros(m, np.uint32), np.zeros(m, np.float64)
+        fn, fo, ff = np.zeros(m, np.uint32), np.zeros(m + 1, np.uint32), np.zeros(m, np.uint32)
+        nb, nf = ctypes.c_int(), ctypes.c_int()
+        rc = lib().oo_vocab_transform(self._h, _p(d), n, levelsup, _p(bw), _p(bv), ctypes.byref(nb),
+                                      _p(fn), _p(fo), _p(ff), ctypes.byref(nf))
+        if rc != OO_OK:
+            raise OracleError(rc)
+        nfe = int(fo[nf.value])
+        return ((bw[:nb.value].copy(), bv[:nb.value].copy()),
+                dict(node_id=fn[:nf.value].copy(), off=fo[:nf.value + 1].copy(),
+                     feat=ff[:nfe].copy()))

@@ -1090,3 +1090,181 @@ int oo_compute_stereo_matches(int nl, const oo_keypoint* kl, const uint8_t* dl, 
   free(vDistIdx);
   return nvalid;
 }
+
+/* ---------- DBoW2 vocabulary (Thirdparty/DBoW2/DBoW2) -------------------- */
+struct oo_vocab {
+  int k, L, scoring, weighting;
+  int nnodes;          /* including the root (node 0) */
+  int* parent;
+  int* cbeg;           /* children of node i: cid[cbeg[i] .. cbeg[i+1]) in push order */
+  int* cid;
+  uint8_t* desc;       /* [nnodes][32] */
+  double* weight;
+  uint32_t* word_id;
+  int nwords;
+};
+
+static void vocab_free(oo_vocab* v) {
+  if (!v) return;
+  free(v->parent); free(v->cbeg); free(v->cid); free(v->desc); free(v->weight); free(v->word_id);
+  free(v);
+}
+
+void oo_vocab_destroy(oo_vocab* v) { vocab_free(v); }
+
+/* build from the node records in file order (node i = record i-1, i >= 1):
+ * TemplatedVocabulary::loadFromTextFile (TemplatedVocabulary.h:1338-1424) */
+oo_vocab* oo_vocab_from_records(int k, int L, int scoring, int weighting, int nrec,
+                                const int* parent, const int* is_leaf, const uint8_t* desc,
+                                const double* weight) {
+  if (k < 0 || k > 20 || L < 1 || L > 10 || scoring < 0 || scoring > 5 || weighting < 0 ||
+      weighting > 3 || nrec < 0) /* :1356-1360 */
+    return NULL;
+  oo_vocab* v = (oo_vocab*)calloc(1, sizeof(oo_vocab));
+  v->k = k; v->L = L; v->scoring = scoring; v->weighting = weighting;
+  const int n = nrec + 1;
+  v->nnodes = n;
+  v->parent = (int*)calloc((size_t)n, sizeof(int));
+  v->cbeg = (int*)calloc((size_t)n + 1, sizeof(int));
+  v->cid = (int*)calloc((size_t)(nrec > 0 ? nrec : 1), sizeof(int));
+  v->desc = (uint8_t*)calloc((size_t)n * 32, 1);
+  v->weight = (double*)calloc((size_t)n, sizeof(double));  /* Node(): weight(0), word_id(0) */
+  v->word_id = (uint32_t*)calloc((size_t)n, sizeof(uint32_t));
+  for (int i = 1; i < n; ++i) {
+    const int pid = parent[i - 1];
+    if (pid < 0 || pid >= i) { vocab_free(v); return NULL; } /* m_nodes[pid] must exist */
+    v->parent[i] = pid;
+    v->cbeg[pid + 1]++;
+    memcpy(v->desc + (size_t)i * 32, desc + (size_t)(i - 1) * 32, 32);
+    v->weight[i] = weight[i - 1];
+    if (is_leaf[i - 1] > 0) v->word_id[i] = (uint32_t)v->nwords++; /* :1412-1418 */
+  }
+  for (int i = 0; i < n; ++i) v->cbeg[i + 1] += v->cbeg[i];
+  int* fill = (int*)calloc((size_t)n, sizeof(int));
+  for (int i = 1; i < n; ++i) { /* m_nodes[pid].children.push_back(nid), file order */
+    const int pid = v->parent[i];
+    v->cid[v->cbeg[pid] + fill[pid]++] = i;
+  }
+  free(fill);
+  return v;
+}
+
+int oo_vocab_info(const oo_vocab* v, int* k, int* L, int* scoring, int* weighting, int* nnodes,
+                  int* nwords) {
+  if (k) *k = v->k;
+  if (L) *L = v->L;
+  if (scoring) *scoring = v->scoring;
+  if (weighting) *weighting = v->weighting;
+  if (nnodes) *nnodes = v->nnodes;
+  if (nwords) *nwords = v->nwords;
+  return OO_OK;
+}
+
+/* TemplatedVocabulary::transform(feature, word_id, weight, nid, levelsup)
+ * (:1222-1259).  Returns 0 or OO_ERR_ARG when the reference would read an
+ * unset NodeId (a leaf above nid_level). */
+static int vocab_transform1(const oo_vocab* v, const uint8_t* f, int levelsup, uint32_t* word,
+                            double* w, uint32_t* nid, int* nid_set) {
+  const int nid_level = v->L - levelsup;
+  *nid_set = 0;
+  if (nid_level <= 0) { *nid = 0; *nid_set = 1; }
+  int final_id = 0, level = 0;
+  do {
+    ++level;
+    const int b = v->cbeg[final_id], e = v->cbeg[final_id + 1];
+    final_id = v->cid[b];
+    double best_d = (double)oo_descriptor_distance(f, v->desc + (size_t)final_id * 32);
+    for (int c = b + 1; c < e; ++c) {
+      const int id = v->cid[c];
+      const double d = (double)oo_descriptor_distance(f, v->desc + (size_t)id * 32);
+      if (d < best_d) { best_d = d; final_id = id; }
+    }
+    if (level == nid_level) { *nid = (uint32_t)final_id; *nid_set = 1; }
+  } while (v->cbeg[final_id] != v->cbeg[final_id + 1]); /* !isLeaf(): children non-empty */
+  *word = v->word_id[final_id];
+  *w = v->weight[final_id];
+  return 0;
+}
+
+typedef struct { uint32_t key; uint32_t i; } oo_kv;
+static int kv_cmp(const void* a, const void* b) {
+  const oo_kv* x = (const oo_kv*)a;
+  const oo_kv* y = (const oo_kv*)b;
+  if (x->key != y->key) return x->key < y->key ? -1 : 1;
+  return (x->i > y->i) - (x->i < y->i);
+}
+
+/* transform(features, BowVector&, FeatureVector&, levelsup) (:1126-1191).
+ * BowVector: bow_word[nbow] ascending, bow_value[nbow]; FeatureVector CSR:
+ * fv_node[nfv] ascending, fv_off[nfv+1], fv_feat (ascending per node).
+ * Outputs need n entries (n + 1 for fv_off).  Returns OO_OK / OO_ERR_ARG. */
+int oo_vocab_transform(const oo_vocab* v, const uint8_t* desc, int n, int levelsup,
+                       uint32_t* bow_word, double* bow_value, int* nbow, uint32_t* fv_node,
+                       uint32_t* fv_off, uint32_t* fv_feat, int* nfv) {
+  *nbow = 0;
+  *nfv = 0;
+  fv_off[0] = 0;
+  if (v->nwords == 0) return OO_OK; /* if(empty()) return; (:1133) */
+  const int tf = v->weighting == 0 || v->weighting == 1; /* TF_IDF || TF */
+  int must = v->scoring != 5, l2 = v->scoring == 1;       /* mustNormalize (ScoringObject.h:74-89) */
+  oo_kv* bw = (oo_kv*)malloc(sizeof(oo_kv) * (size_t)(n > 0 ? n : 1));
+  oo_kv* fw = (oo_kv*)malloc(sizeof(oo_kv) * (size_t)(n > 0 ? n : 1));
+  double* wv = (double*)malloc(sizeof(double) * (size_t)(n > 0 ? n : 1));
+  int nb = 0, nf = 0;
+  for (int i = 0; i < n; ++i) {
+    uint32_t word, nid = 0;
+    double w;
+    int set;
+    vocab_transform1(v, desc + (size_t)i * 32, levelsup, &word, &w, &nid, &set);
+    if (w > 0) { /* not stopped */
+      if (!set) { free(bw); free(fw); free(wv); return OO_ERR_ARG; }
+      bw[nb].key = word; bw[nb].i = (uint32_t)i; wv[i] = w; nb++;
+      fw[nf].key = nid; fw[nf].i = (uint32_t)i; nf++;
+    }
+  }
+  /* std::map order: ascending key; ties keep feature order (push order) */
+  qsort(bw, (size_t)nb, sizeof(oo_kv), kv_cmp);
+  qsort(fw, (size_t)nf, sizeof(oo_kv), kv_cmp);
+  int m = 0;
+  for (int a = 0; a < nb;) {
+    int e = a;
+    double s = wv[bw[a].i];
+    while (++e < nb && bw[e].key == bw[a].key)
+      if (tf) s += wv[bw[e].i]; /* addWeight: +=; addIfNotExist keeps the first */
+    bow_word[m] = bw[a].key;
+    bow_value[m] = s;
+    m++;
+    a = e;
+  }
+  *nbow = m;
+  if (tf && m > 0 && !must) { /* :1164-1170 */
+    const double nd = (double)m;
+    for (int j = 0; j < m; ++j) bow_value[j] /= nd;
+  }
+  if (must) { /* BowVector::normalize (BowVector.cpp:61-83) */
+    double norm = 0.0;
+    if (!l2) {
+      for (int j = 0; j < m; ++j) norm += fabs(bow_value[j]);
+    } else {
+      /* BowVector.cpp is built with -O3 -march=native (Thirdparty/DBoW2/
+       * CMakeLists.txt:4-5): GCC contracts the square-accumulate into an
+       * FMA on FMA hosts (inferred from the flags; no DBoW2 object ships) */
+      for (int j = 0; j < m; ++j) norm = fma(bow_value[j], bow_value[j], norm);
+      norm = sqrt(norm);
+    }
+    if (norm > 0.0)
+      for (int j = 0; j < m; ++j) bow_value[j] /= norm;
+  }
+  int q = 0;
+  for (int a = 0; a < nf;) {
+    int e = a;
+    fv_node[q] = fw[a].key;
+    while (e < nf && fw[e].key == fw[a].key) { fv_feat[e] = fw[e].i; e++; }
+    fv_off[q + 1] = (uint32_t)e;
+    q++;
+    a = e;
+  }
+  *nfv = q;
+  free(bw); free(fw); free(wv);
+  return OO_OK;
+}

@@ -107,6 +107,22 @@ int oo_compute_stereo_matches(int nl, const oo_keypoint* kl, const uint8_t* dl, 
                               const int* lw, const int* lh, const int* lstride, float mb,
                               float mbf, float* uright, float* depth);
 
+/* DBoW2 vocabulary (Thirdparty/DBoW2/DBoW2/TemplatedVocabulary.h).  Node
+ * records in loadFromTextFile order (:1378-1422): record r is node r+1 with
+ * parent[r], is_leaf[r] (nIsLeaf), desc[r] (32 B), weight[r].  NULL if the
+ * header is rejected (:1356-1360) or a parent does not exist yet. */
+typedef struct oo_vocab oo_vocab;
+oo_vocab* oo_vocab_from_records(int k, int L, int scoring, int weighting, int nrec,
+                                const int* parent, const int* is_leaf, const uint8_t* desc,
+                                const double* weight);
+void oo_vocab_destroy(oo_vocab* v);
+int oo_vocab_info(const oo_vocab* v, int* k, int* L, int* scoring, int* weighting, int* nnodes,
+                  int* nwords);
+/* transform(features, BowVector&, FeatureVector&, levelsup) (:1126-1191) */
+int oo_vocab_transform(const oo_vocab* v, const uint8_t* desc, int n, int levelsup,
+                       uint32_t* bow_word, double* bow_value, int* nbow, uint32_t* fv_node,
+                       uint32_t* fv_off, uint32_t* fv_feat, int* nfv);
+
 #ifdef __cplusplus
 }
 #endif

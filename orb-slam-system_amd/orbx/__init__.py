@@ -51,6 +51,8 @@ EXPORTED = [
     "orbm_plan_match_frames", "orbm_plan_set_timing", "orbm_plan_stage_times",
     "orbx_stereo_match", "orbs_plan_create", "orbs_plan_destroy", "orbs_plan_match",
     "orbs_plan_check", "orbs_plan_set_timing", "orbs_plan_stage_times",
+    "orbv_vocab_load_text", "orbv_vocab_create", "orbv_vocab_destroy", "orbv_vocab_info",
+    "orbv_transform", "orbv_transform_batch", "orbv_check",
 ]
 
 
@@ -118,6 +120,13 @@ _sig = {
     "orbs_plan_check": (I, [P, P]),
     "orbs_plan_set_timing": (I, [P, I]),
     "orbs_plan_stage_times": (I, [P, P, P, I]),
+    "orbv_vocab_load_text": (I, [ctypes.c_char_p, I, P]),
+    "orbv_vocab_create": (I, [I, I, I, I, I, P, P, P, P, I, P]),
+    "orbv_vocab_destroy": (I, [P]),
+    "orbv_vocab_info": (I, [P, P, P, P, P, P, P]),
+    "orbv_transform": (I, [P, P, I, I, P, P, P, P, P, P, P]),
+    "orbv_transform_batch": (I, [P, I, P, P, I, I, P, P, P, P, P, P, P, P]),
+    "orbv_check": (I, [P, P]),
 }
 for _n, (_r, _a) in _sig.items():
     _f = getattr(_lib, _n)
@@ -262,6 +271,85 @@ def compute_stereo_matches(left, right, kps_l, desc_l, kps_r, desc_r, mb, mbf):
                                   len(kr), float(mb), float(mbf), _p(ur), _p(dep),
                                   ctypes.byref(nm)), "orbx_stereo_match")
     return ur[:len(kl)].copy(), dep[:len(kl)].copy(), nm.value
+
+
+# --------------------------------------------------------------------------- DBoW2 vocabulary
+class Vocabulary:
+    """DBoW2::TemplatedVocabulary<FORB::TDescriptor, FORB> (ORBVocabulary) on
+    the device: loadFromTextFile + transform (TemplatedVocabulary.h:1126-1424)."""
+
+    def __init__(self, handle):
+        self._h = handle
+
+    @classmethod
+    def load_text(cls, path, device=0):
+        h = ctypes.c_void_p()
+        _check(_lib.orbv_vocab_load_text(os.fsencode(path), device, ctypes.byref(h)),
+               "orbv_vocab_load_text")
+        return cls(h)
+
+    @classmethod
+    def from_records(cls, voc, scoring=0, weighting=0, device=0):
+        parent = np.ascontiguousarray(voc["parent"], np.int32)
+        leaf = np.ascontiguousarray(voc["is_leaf"], np.int32)
+        desc = np.ascontiguousarray(voc["desc"], np.uint8)
+        w = np.ascontiguousarray(voc["weight"], np.float64)
+        h = ctypes.c_void_p()
+        _check(_lib.orbv_vocab_create(voc["k"], voc["L"], scoring, weighting, len(parent),
+                                      _p(parent), _p(leaf), _p(desc), _p(w), device,
+                                      ctypes.byref(h)), "orbv_vocab_create")
+        return cls(h)
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            _lib.orbv_vocab_destroy(self._h)
+            self._h = None
+
+    def info(self):
+        v = [ctypes.c_int() for _ in range(6)]
+        _check(_lib.orbv_vocab_info(self._h, *[ctypes.byref(x) for x in v]))
+        return dict(zip(("k", "L", "scoring", "weighting", "nnodes", "nwords"),
+                        [x.value for x in v]))
+
+    def transform(self, desc, levelsup=4):
+        """-> (BowVector (word ids u32, values f64), FeatureVector dict(node_id, off, feat))"""
+        d = np.ascontiguousarray(desc, np.uint8).reshape(-1, 32)
+        n = len(d)
+        m = max(n, 1)
+        bw, bv = np.zeros(m, np.uint32), np.zeros(m, np.float64)
+        fn, fo, ff = np.zeros(m, np.uint32), np.zeros(m + 1, np.uint32), np.zeros(m, np.uint32)
+        nb, nf = ctypes.c_int(), ctypes.c_int()
+        _check(_lib.orbv_transform(self._h, _p(d), n, levelsup, _p(bw), _p(bv), ctypes.byref(nb),
+                                   _p(fn), _p(fo), _p(ff), ctypes.byref(nf)), "orbv_transform")
+        nfe = int(fo[nf.value])
+        return ((bw[:nb.value].copy(), bv[:nb.value].copy()),
+                dict(node_id=fn[:nf.value].copy(), off=fo[:nf.value + 1].copy(),
+                     feat=ff[:nfe].copy()))
+
+    def transform_batch(self, desc, counts, levelsup=4, stream=None):
+        """Device form over Plan outputs: desc cuda u8 [B, kcap, 32], counts i32 [B].
+        Async; returns dict of cuda tensors (bow_word, bow_value, nbow, fv_node,
+        fv_off, fv_feat, nfv), rows per frame as in orbv_transform."""
+        import torch
+        B, kcap = desc.shape[0], desc.shape[1]
+        dev = desc.device
+        o = dict(bow_word=torch.empty((B, kcap), dtype=torch.int32, device=dev),
+                 bow_value=torch.empty((B, kcap), dtype=torch.float64, device=dev),
+                 nbow=torch.empty(B, dtype=torch.int32, device=dev),
+                 fv_node=torch.empty((B, kcap), dtype=torch.int32, device=dev),
+                 fv_off=torch.empty((B, kcap + 1), dtype=torch.int32, device=dev),
+                 fv_feat=torch.empty((B, kcap), dtype=torch.int32, device=dev),
+                 nfv=torch.empty(B, dtype=torch.int32, device=dev))
+        _check(_lib.orbv_transform_batch(self._h, B, desc.data_ptr(), counts.data_ptr(), kcap,
+                                         levelsup, o["bow_word"].data_ptr(),
+                                         o["bow_value"].data_ptr(), o["nbow"].data_ptr(),
+                                         o["fv_node"].data_ptr(), o["fv_off"].data_ptr(),
+                                         o["fv_feat"].data_ptr(), o["nfv"].data_ptr(),
+                                         _stream_handle(stream)), "orbv_transform_batch")
+        return o
+
+    def check(self, stream=None):
+        _check(_lib.orbv_check(self._h, _stream_handle(stream)), "orbv_check")
 
 
 # --------------------------------------------------------------------------- ORBmatcher

@@ -91,3 +91,56 @@ def stereo_pair(w, h, frame_idx, max_disp=64):
 
 def frames(w, h, first_idx, count, kind="rects"):
     return np.stack([frame(w, h, first_idx + i, kind) for i in range(count)])
+
+
+def vocabulary(k=10, L=6, seed=1, flip=0.2, stop_frac=0.03, prune=0.0):
+    """Synthetic DBoW2 vocabulary tree (the reference's ORBvoc.txt is not in
+    the tree).  Nodes in breadth-first order (children of a node contiguous,
+    parents before children, as loadFromTextFile requires); root children
+    are random 32-B descriptors, a child is its parent with each bit flipped
+    with probability round(256 * flip) / 256.  Leaves carry idf-like weights in (0.1, 8),
+    `stop_frac` of them 0 (stopped words); inner nodes weight 0.  `prune`:
+    probability that a node below level 1 gets no children (shallow leaves).
+    Returns dict(k, L, parent, is_leaf, desc, weight) of node records."""
+    rng = np.random.default_rng(seed)
+    parents, descs = [], []
+    f_ids = np.zeros(1, np.int64)           # frontier node ids
+    f_desc = None                           # frontier descriptors (None = root)
+    next_id = 1
+    for level in range(1, L + 1):
+        if level > 2 and prune > 0:
+            keep = rng.uniform(size=len(f_ids)) >= prune
+            f_ids, f_desc = f_ids[keep], f_desc[keep]
+        n = len(f_ids) * k
+        if n == 0:
+            break
+        par = np.repeat(f_ids, k)
+        if f_desc is None:
+            cd = rng.integers(0, 256, (n, 32), dtype=np.uint8)
+        else:
+            bits = rng.integers(0, 256, (n, 256), dtype=np.uint8) < int(round(flip * 256))
+            cd = np.repeat(f_desc, k, axis=0) ^ np.packbits(bits, axis=1)
+        parents.append(par)
+        descs.append(cd)
+        f_ids = np.arange(next_id, next_id + n, dtype=np.int64)
+        f_desc = cd
+        next_id += n
+    parent = np.concatenate(parents).astype(np.int32)
+    desc = np.concatenate(descs)
+    nrec = len(parent)
+    has_child = np.zeros(nrec + 1, bool)
+    has_child[parent] = True
+    is_leaf = (~has_child[1:]).astype(np.int32)
+    w = rng.uniform(0.1, 8.0, nrec)
+    w[rng.uniform(size=nrec) < stop_frac] = 0.0
+    weight = np.where(is_leaf == 1, w, 0.0)
+    return dict(k=k, L=L, parent=parent, is_leaf=is_leaf, desc=desc.reshape(nrec, 32),
+                weight=weight.astype(np.float64))
+
+
+def write_vocabulary_text(path, voc, scoring=0, weighting=0):
+    """TemplatedVocabulary::saveToTextFile format (TemplatedVocabulary.h:1430-1455)."""
+    with open(path, "w") as f:
+        f.write("%d %d %d %d\n" % (voc["k"], voc["L"], scoring, weighting))
+        for p, l, d, w in zip(voc["parent"], voc["is_leaf"], voc["desc"], voc["weight"]):
+            f.write("%d %d %s %s\n" % (p, l, " ".join(str(int(x)) for x in d), repr(float(w))))

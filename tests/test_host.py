@@ -17,7 +17,7 @@ HEADER = os.path.join(ROOT, "include", "orbx.h")
 
 def test_library_exports_every_header_function(orbx_mod):
     txt = open(HEADER).read()
-    decl = set(re.findall(r"^\w[\w\s\*]*?\b(orb[xms]_\w+)\s*\(", txt, re.M))
+    decl = set(re.findall(r"^\w[\w\s\*]*?\b(orb[xmsv]_\w+)\s*\(", txt, re.M))
     assert len(decl) >= 25
     missing = [n for n in decl if not hasattr(orbx_mod.lib(), n)]
     assert not missing, missing
