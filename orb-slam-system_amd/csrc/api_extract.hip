@@ -25,7 +25,7 @@ __global__ void k_quadtree(const LevelInfo*, const CellInfo*, const uint32_t*, s
                            int*, int, int, int, int*);
 __global__ void k_orient_brief(const uint8_t*, size_t, size_t, const uint8_t*, size_t,
                                const BriefArgs, const uint32_t*, size_t, const int*,
-                               orbx_keypoint*, uint8_t*, int*);
+                               orbx_keypoint*, uint8_t*, int*, int);
 __global__ void k_synth(uint8_t*, int, int, size_t, int, int);
 }  // namespace orbx
 
@@ -288,7 +288,7 @@ extern "C" int orbx_plan_extract(orbx_plan* p, const uint8_t* frames, int nframe
                        P.min_th, p->fs_tpitch, p->fs_tmaxh, p->fs_mcells, p->dbg);
   }
   p->timer.end(ORBX_STAGE_FAST, s);
-  if (p->dbg) return ORBX_OK; /* phase probe: later stages would read partial results */
+  if (p->dbg && p->dbg < 20) return ORBX_OK; /* phase probe: later stages would read partial results */
   // K3 DistributeOctTree
   p->timer.begin(ORBX_STAGE_QUADTREE, s);
   hipLaunchKernelGGL(k_quadtree, dim3(L, n), dim3(256), p->qt_lds, s, p->d_lv, p->d_cells,
@@ -303,7 +303,7 @@ extern "C" int orbx_plan_extract(orbx_plan* p, const uint8_t* frames, int nframe
   hipLaunchKernelGGL(k_orient_brief, dim3((ob_waves + 3) / 4, n),
                      dim3(256), 0, s, frames, fstride, rstride, p->d_pyr, p->pyr_stride, p->bargs,
                      p->d_qout, p->qout_stride, p->d_lcount, kps, desc,
-                     counts);
+                     counts, p->dbg);
   p->timer.end(ORBX_STAGE_BRIEF, s);
   if (hipGetLastError() != hipSuccess) return ORBX_ERR_HIP;
   return ORBX_OK;

@@ -867,11 +867,77 @@ __device__ __forceinline__ void brief_sincos(float x, float* s, float* c) {
 #define KP_ROWS 43
 #define KP_COLS 48
 
+// One keypoint of the frame's level-major output list: where its level
+// lives and where its patch starts (all wave-uniform).
+struct BriefKp {
+  int l, x, y, score, patch_size;
+  float scale;
+  const uint8_t* img;
+  int pitch, UW, UH, px0, py0;
+  bool inside;   // the whole patch lies in the level
+  bool aligned;  // level base and pitch are dword aligned (register path usable)
+};
+
+// the patch is 43 rows x 12 dwords: lane (< 60) owns column lane % 12 of
+// rows lane / 12 + 5u, u = 0..8 (row 43+ clamped).  The nine loads are issued
+// together from one uniform base (saddr) + a 32-bit lane offset and held in
+// registers (scalars in a struct: never spilled to scratch).
+struct BriefRegs {
+  uint32_t r[9];
+};
+
+__device__ __forceinline__ void brief_issue(const BriefKp& k, BriefRegs& R, int lane) {
+  const int ln = min(lane, 59);
+  const uint32_t c4 = (uint32_t)(ln % 12) * 4u, r0 = (uint32_t)(ln / 12);
+  if (k.inside) {
+    const uint8_t* b = k.img + (size_t)k.py0 * k.pitch + k.px0;  // wave-uniform
+#pragma unroll
+    for (int u = 0; u < 9; ++u) {
+      const uint32_t row = min(r0 + 5u * u, (uint32_t)(KP_ROWS - 1));
+      R.r[u] = *reinterpret_cast<const uint32_t*>(b + (row * (uint32_t)k.pitch + c4));
+    }
+  } else {
+    // patch crosses the level border: reflect-101 rows, dword loads where the
+    // four columns are inside, reflected bytes at the left/right edge only
+    const int cx = k.px0 + (int)c4;
+    const bool cin = cx >= 0 && cx + 4 <= k.UW;
+#pragma unroll
+    for (int u = 0; u < 9; ++u) {
+      const int r = min((int)r0 + 5 * u, KP_ROWS - 1);
+      const int gy = reflect101(min(max(k.py0 + r, -3), k.UH + 2), k.UH);
+      const uint8_t* rowp = k.img + (size_t)gy * k.pitch;
+      if (cin) {
+        R.r[u] = *reinterpret_cast<const uint32_t*>(rowp + cx);
+      } else {
+        uint32_t w = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int gx = reflect101(min(max(cx + j, -3), k.UW + 2), k.UW);
+          w |= (uint32_t)rowp[gx] << (8 * j);
+        }
+        R.r[u] = w;
+      }
+    }
+  }
+}
+
+__device__ __forceinline__ void brief_commit(const BriefRegs& R, uint32_t* P, int lane) {
+  if (lane < 60) {
+    const int c = lane % 12, r0 = lane / 12;
+#pragma unroll
+    for (int u = 0; u < 9; ++u) {
+      const int row = r0 + 5 * u;
+      if (row < KP_ROWS) P[row * (KP_COLS / 4) + c] = R.r[u];
+    }
+  }
+}
+
 __global__ __launch_bounds__(256) void k_orient_brief(
     const uint8_t* __restrict__ frames, size_t fstride, size_t rstride,
     const uint8_t* __restrict__ pyr, size_t pstride, const BriefArgs A,
     const uint32_t* __restrict__ qout, size_t qout_stride, const int* __restrict__ lcount,
-    orbx_keypoint* __restrict__ kps, uint8_t* __restrict__ desc, int* __restrict__ counts) {
+    orbx_keypoint* __restrict__ kps, uint8_t* __restrict__ desc, int* __restrict__ counts,
+    int dbg) {
   __shared__ uint32_t patch[4][KP_ROWS][KP_COLS / 4];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int f = blockIdx.y;
@@ -887,38 +953,71 @@ __global__ __launch_bounds__(256) void k_orient_brief(
   }
   const int total = __shfl(incl, 63, 64);  // all lanes active here
   if (blockIdx.x == 0 && threadIdx.x == 0) counts[f] = total;
-  // output position o (levels concatenated, :455-494); waves stride over
-  // the frame's keypoints, so the grid is sized by nfeatures, not capacity
-  const int stride = (int)gridDim.x * 4;
-  for (int o = g; o < total; o += stride) {  // wave-uniform
-  const int l = __popcll(__ballot(lane < nlevels && incl <= o));
-  const int i = o - __shfl(incl - lcv, l, 64);
-  const uint32_t key = qout[(size_t)f * qout_stride + A.kout_off[l] + i];
-  const int x = (int)(key >> 20) + ORBX_MINB, y = (int)((key >> 8) & 0xFFF) + ORBX_MINB;
-  const int score = (int)(key & 0xFF);
-  const int u = A.unique[l];
-  const int pitch = u == 0 ? (int)rstride : A.pitch[u];
-  const uint8_t* img = u == 0 ? frames + (size_t)f * fstride : pyr + (size_t)f * pstride + A.pyr_off[u];
-  const int UW = A.w[u], UH = A.h[u];
-  // stage the patch (unblurred level), reflect-101 outside the image
-  const int px0 = (x - KP_R) & ~3, py0 = y - KP_R;
+  const int excl = incl - lcv;
+  const uint32_t* Q = qout + (size_t)f * qout_stride;
   uint32_t(*P)[KP_COLS / 4] = patch[wave];
-  const bool inside = px0 >= 0 && px0 + KP_COLS <= UW && py0 >= 0 && py0 + KP_ROWS <= UH &&
-                      ((reinterpret_cast<uintptr_t>(img) | (uintptr_t)pitch) & 3) == 0;
-  if (inside) {
-    stage_region<uint32_t, 9, 64>(reinterpret_cast<uint8_t*>(P), KP_COLS,
-                                  img + (size_t)py0 * pitch + px0, pitch, KP_ROWS, KP_COLS / 4, lane);
+  // the 256 test pairs {x0, y0, x1, y1} in LDS (ds_read, not a vector load
+  // that would wait behind the patch prefetch)
+  __shared__ uint32_t spat[256];
+  spat[threadIdx.x] = *reinterpret_cast<const uint32_t*>(ORBX_BRIEF_PATTERN[threadIdx.x]);
+  __syncthreads();
+  // output position o -> keypoint.  Everything is wave-uniform and forced
+  // scalar (readfirstlane): the key and the level tables are s_loads, so the
+  // only vector loads in flight while a keypoint is computed are the next
+  // keypoint's patch (vmcnt stays exact; nothing waits on it early).
+  auto locate = [&](int o) {
+    const int l = __builtin_amdgcn_readfirstlane(__popcll(__ballot(lane < nlevels && incl <= o)));
+    const int i = o - __builtin_amdgcn_readfirstlane(__shfl(excl, l, 64));
+    const uint32_t key = __builtin_amdgcn_readfirstlane(Q[A.kout_off[l] + i]);
+    BriefKp k;
+    k.l = l;
+    k.x = (int)(key >> 20) + ORBX_MINB;
+    k.y = (int)((key >> 8) & 0xFFF) + ORBX_MINB;
+    k.score = (int)(key & 0xFF);
+    k.scale = A.scale[l];
+    k.patch_size = A.patch[l];
+    const int u = A.unique[l];
+    k.pitch = u == 0 ? (int)rstride : A.pitch[u];
+    k.img = u == 0 ? frames + (size_t)f * fstride : pyr + (size_t)f * pstride + A.pyr_off[u];
+    k.UW = A.w[u];
+    k.UH = A.h[u];
+    k.px0 = (k.x - KP_R) & ~3;
+    k.py0 = k.y - KP_R;
+    k.inside = k.px0 >= 0 && k.px0 + KP_COLS <= k.UW && k.py0 >= 0 && k.py0 + KP_ROWS <= k.UH;
+    k.aligned = ((reinterpret_cast<uintptr_t>(k.img) | (uintptr_t)k.pitch) & 3) == 0;
+    return k;
+  };
+  // output position o (levels concatenated, :455-494); waves stride over
+  // the frame's keypoints, so the grid is sized by nfeatures, not capacity.
+  // Software pipeline: keypoint o is computed while the patch of o+stride
+  // is loading into registers.
+  const int stride = (int)gridDim.x * 4;
+  int o = g;
+  if (o >= total) return;
+  BriefKp cur = locate(o);
+  BriefRegs R;
+  if (cur.aligned) brief_issue(cur, R, lane);
+  for (; o < total; o += stride) {  // wave-uniform
+  // ---- stage this keypoint's patch (unblurred level), reflect-101 outside ----
+  if (cur.aligned) {
+    brief_commit(R, &P[0][0], lane);
   } else {
-    uint8_t* P8 = reinterpret_cast<uint8_t*>(P);
+    uint8_t* P8w = reinterpret_cast<uint8_t*>(P);
     for (int q = lane; q < KP_ROWS * KP_COLS; q += 64) {
       const int r = q / KP_COLS, c = q - r * KP_COLS;
-      const int gy = reflect101(min(max(py0 + r, -3), UH + 2), UH);
-      const int gx = reflect101(min(max(px0 + c, -3), UW + 2), UW);
-      P8[q] = img[(size_t)gy * pitch + gx];
+      const int gy = reflect101(min(max(cur.py0 + r, -3), cur.UH + 2), cur.UH);
+      const int gx = reflect101(min(max(cur.px0 + c, -3), cur.UW + 2), cur.UW);
+      P8w[q] = cur.img[(size_t)gy * cur.pitch + gx];
     }
   }
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  const BriefKp me = cur;
+  if (o + stride < total) {  // next keypoint: its patch loads stay in flight
+    cur = locate(o + stride);
+    if (cur.aligned) brief_issue(cur, R, lane);
+  }
+  const int l = me.l, x = me.x, score = me.score, px0 = me.px0;
   const uint8_t* P8 = reinterpret_cast<const uint8_t*>(P);
   // IC_Angle (:21-48) on the unblurred level: lane = patch row v + 15,
   // u in [-umax[|v|], umax[|v|]] (integer sums: order-free)
@@ -952,15 +1051,16 @@ __global__ __launch_bounds__(256) void k_orient_brief(
   // BRIEF (:57-73) on GaussianBlur(7x7, sigma 2) evaluated at each sample:
   // out = (sum_j k_j * (sum_i k_i p) + 32768) >> 16, rows via v_dot4_u32_u8
   const uint32_t K0 = 18u | (34u << 8) | (48u << 16) | (56u << 24), K1 = 48u | (34u << 8) | (18u << 16);
-  uint64_t words[4];
+  constexpr uint32_t GK[7] = {18, 34, 48, 56, 48, 34, 18};
+  uint64_t words[4] = {0, 0, 0, 0};
 #pragma unroll
   for (int rr = 0; rr < 4; ++rr) {
-    const int p = lane + 64 * rr;
+    const uint32_t pw = spat[lane + 64 * rr];
     int t[2];
 #pragma unroll
     for (int e = 0; e < 2; ++e) {
-      const float fx = (float)ORBX_BRIEF_PATTERN[p][2 * e];
-      const float fy = (float)ORBX_BRIEF_PATTERN[p][2 * e + 1];
+      const float fx = (float)(int)(int8_t)(pw >> (16 * e));
+      const float fy = (float)(int)(int8_t)(pw >> (16 * e + 8));
       const float ya = fy * cs, yb = fy * sn;
       const int row = (int)__builtin_rintf(__builtin_fmaf(fx, sn, ya));
       const int col = (int)__builtin_rintf(__builtin_fmaf(fx, cs, -yb));
@@ -973,7 +1073,7 @@ __global__ __launch_bounds__(256) void k_orient_brief(
         const uint32_t lo4 = __builtin_amdgcn_alignbyte(w1, w0, sh);
         const uint32_t hi4 = __builtin_amdgcn_alignbyte(w2, w1, sh);
         const uint32_t h = __builtin_amdgcn_udot4(hi4, K1, __builtin_amdgcn_udot4(lo4, K0, 0u, false), false);
-        acc += (uint32_t)c_gk[jj] * h;
+        acc += GK[jj] * h;
       }
       t[e] = (int)min((acc + 32768u) >> 16, 255u);
     }
@@ -986,12 +1086,12 @@ __global__ __launch_bounds__(256) void k_orient_brief(
   if (lane == 0) {
     orbx_keypoint kp;
     kp.x = (float)x;
-    kp.y = (float)y;
+    kp.y = (float)me.y;
     if (l != 0) {
-      kp.x *= A.scale[l];
-      kp.y *= A.scale[l];
+      kp.x *= me.scale;
+      kp.y *= me.scale;
     }
-    kp.size = (float)A.patch[l];
+    kp.size = (float)me.patch_size;
     kp.angle = angle;
     kp.response = (float)score;
     kp.octave = l;
