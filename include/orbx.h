@@ -283,6 +283,48 @@ int orbv_transform_batch(orbv_vocab* v, int nframes, const uint8_t* d_desc, cons
                          int* d_nfv, void* stream);
 int orbv_check(orbv_vocab* v, void* stream);
 
+/* ---------------------------------------------------------------------------
+ * Projection matchers: the frame grid
+ * (Frame::AssignFeaturesToGrid / PosInGrid / GetFeaturesInArea,
+ * src/Frame.cc:210-225,307-371, 64 x 48 cells) and the windowed Hamming
+ * search of ORBmatcher::SearchByProjection.  Query form: the caller projects
+ * (the cv::Mat pose arithmetic and MapPoint::PredictScale stay with the
+ * caller) and passes per query the arguments the reference hands to
+ * GetFeaturesInArea plus the gates' inputs.
+ * ------------------------------------------------------------------------- */
+typedef struct {
+  float x, y;                    /* mTrackProjX/Y (mode 1) or the projection u, v       */
+  float radius;                  /* the r argument of GetFeaturesInArea (already scaled)  */
+  int32_t min_level, max_level;  /* its level bounds (-1 = the defaults)                 */
+  float xr;                      /* mode 1: mTrackProjXR (stereo gate, :39-43)           */
+  float angle;                   /* modes 2/3: angle of the source keypoint             */
+} orbx_query_proj;
+
+typedef struct {
+  int n;
+  const orbx_keypoint* keys;  /* mvKeysUn                                              */
+  const uint8_t* desc;        /* mDescriptors, n x 32                                   */
+  const float* uright;        /* mvuRight (mode 1 stereo gate), NULL = monocular        */
+  const uint8_t* occupied;    /* mode 1: mvpMapPoints[i] && Observations() > 0;
+                                 modes 2/3: mvpMapPoints[i] != NULL; NULL = none        */
+  float min_x, min_y;         /* mnMinX, mnMinY                                         */
+  float grid_w_inv, grid_h_inv; /* mfGridElementWidthInv / HeightInv                    */
+} orbx_proj_frame;
+
+/* mode 1: SearchByProjection(Frame&, const vector<MapPoint*>&, th) (src/ORBmatcher.cc:19-61):
+ *         best/second over unoccupied candidates, accept best <= TH_HIGH and
+ *         best <= nnratio * second (th_dist and check_ori unused).
+ * mode 2: SearchByProjection(Frame& Current, const Frame& Last, th, bMono) (:732-818):
+ *         accept best <= th_dist (TH_HIGH); rotation check if check_ori.
+ * mode 3: SearchByProjection(Frame&, KeyFrame*, set<MapPoint*>&, th, ORBdist) (:820-894):
+ *         accept best <= th_dist (ORBdist); rotation check if check_ori.
+ * Queries are walked in order (each takes its best unoccupied candidate,
+ * later queries skip it).  match[i] = the query that took feature i, or -1.
+ * At most 8192 features.  Synchronous; host buffers. */
+int orbm_search_by_projection(int mode, const orbx_proj_frame* frame, const orbx_query_proj* q,
+                              const uint8_t* qdesc, int nq, float nnratio, int th_dist,
+                              int check_ori, int device, int32_t* match, int* nmatches);
+
 #ifdef __cplusplus
 }
 #endif

@@ -60,6 +60,8 @@ def lib():
         L.oo_vocab_destroy.argtypes = [P]
         L.oo_vocab_info.argtypes = [P, P, P, P, P, P, P]
         L.oo_vocab_transform.argtypes = [P, P, i, i, P, P, P, P, P, P, P]
+        L.oo_features_in_area.argtypes = [i, P, f, f, f, f, f, f, f, i, i, P]
+        L.oo_search_by_projection.argtypes = [i, i, P, P, P, P, f, f, f, f, i, P, P, f, i, i, P]
         L.oo_compute_stereo_matches.argtypes = [i, P, P, i, P, P, i, P, P, P, P, P, P, P, f, f,
                                                 P, P]
         _lib = L
@@ -321,3 +323,33 @@ class Vocabulary:
         return ((bw[:nb.value].copy(), bv[:nb.value].copy()),
                 dict(node_id=fn[:nf.value].copy(), off=fo[:nf.value + 1].copy(),
                      feat=ff[:nfe].copy()))
+
+
+PROJ_QUERY_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("radius", "<f4"), ("min_level", "<i4"),
+                             ("max_level", "<i4"), ("xr", "<f4"), ("angle", "<f4")])
+
+
+def features_in_area(frame, x, y, r, min_level=-1, max_level=-1):
+    """Frame::GetFeaturesInArea (src/Frame.cc:307-358), in visiting order."""
+    keys = np.ascontiguousarray(frame["keys"], KEYPOINT_DTYPE)
+    out = np.zeros(max(len(keys), 1), np.int32)
+    n = lib().oo_features_in_area(len(keys), _p(keys), frame["min_x"], frame["min_y"],
+                                  frame["grid_w_inv"], frame["grid_h_inv"], float(x), float(y),
+                                  float(r), int(min_level), int(max_level), _p(out))
+    return out[:n].copy()
+
+
+def search_by_projection(mode, frame, queries, qdesc, nnratio=0.6, th_dist=100, check_ori=True):
+    """ORBmatcher::SearchByProjection, query form (modes 1-3, see orb_oracle.h)."""
+    keys = np.ascontiguousarray(frame["keys"], KEYPOINT_DTYPE)
+    desc = np.ascontiguousarray(frame["desc"], np.uint8).reshape(-1, 32)
+    ur = None if frame.get("uright") is None else np.ascontiguousarray(frame["uright"], np.float32)
+    occ = None if frame.get("occupied") is None else np.ascontiguousarray(frame["occupied"], np.uint8)
+    q = np.ascontiguousarray(queries, PROJ_QUERY_DTYPE)
+    qd = np.ascontiguousarray(qdesc, np.uint8).reshape(-1, 32)
+    m = np.full(max(len(keys), 1), -1, np.int32)
+    nm = lib().oo_search_by_projection(mode, len(keys), _p(keys), _p(desc), _p(ur), _p(occ),
+                                       frame["min_x"], frame["min_y"], frame["grid_w_inv"],
+                                       frame["grid_h_inv"], len(q), _p(q), _p(qd), float(nnratio),
+                                       int(th_dist), 1 if check_ori else 0, _p(m))
+    return m[:len(keys)].copy(), nm

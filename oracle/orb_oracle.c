@@ -1268,3 +1268,175 @@ int oo_vocab_transform(const oo_vocab* v, const uint8_t* desc, int n, int levels
   free(bw); free(fw); free(wv);
   return OO_OK;
 }
+
+/* ---------- Frame grid + ORBmatcher::SearchByProjection ------------------ */
+#define GRID_COLS 64 /* FRAME_GRID_COLS (include/Frame.h:18) */
+#define GRID_ROWS 48 /* FRAME_GRID_ROWS (include/Frame.h:17) */
+
+typedef struct {
+  int n;
+  const oo_keypoint* keys; /* mvKeysUn */
+  float minX, minY, wInv, hInv;
+  int* cell_off; /* [COLS*ROWS+1], cell c = ix*ROWS + iy */
+  int* cell_feat;
+} oo_grid;
+
+/* Frame::PosInGrid (src/Frame.cc:361-371) */
+static int pos_in_grid(const oo_grid* g, const oo_keypoint* kp, int* px, int* py) {
+  *px = (int)roundf((kp->x - g->minX) * g->wInv);
+  *py = (int)roundf((kp->y - g->minY) * g->hInv);
+  return !(*px < 0 || *px >= GRID_COLS || *py < 0 || *py >= GRID_ROWS);
+}
+
+/* Frame::AssignFeaturesToGrid (src/Frame.cc:210-225): cells keep index order */
+static void grid_build(oo_grid* g) {
+  g->cell_off = (int*)calloc(GRID_COLS * GRID_ROWS + 1, sizeof(int));
+  g->cell_feat = (int*)malloc(sizeof(int) * (size_t)(g->n > 0 ? g->n : 1));
+  int* cell = (int*)malloc(sizeof(int) * (size_t)(g->n > 0 ? g->n : 1));
+  for (int i = 0; i < g->n; ++i) {
+    int px, py;
+    cell[i] = pos_in_grid(g, &g->keys[i], &px, &py) ? px * GRID_ROWS + py : -1;
+    if (cell[i] >= 0) g->cell_off[cell[i] + 1]++;
+  }
+  for (int c = 0; c < GRID_COLS * GRID_ROWS; ++c) g->cell_off[c + 1] += g->cell_off[c];
+  int* fill = (int*)calloc(GRID_COLS * GRID_ROWS, sizeof(int));
+  for (int i = 0; i < g->n; ++i)
+    if (cell[i] >= 0) g->cell_feat[g->cell_off[cell[i]] + fill[cell[i]]++] = i;
+  free(fill);
+  free(cell);
+}
+
+static void grid_free(oo_grid* g) {
+  free(g->cell_off);
+  free(g->cell_feat);
+}
+
+/* Frame::GetFeaturesInArea (src/Frame.cc:307-358): candidate indices in the
+ * reference's visiting order (ix, iy, cell order).  Returns the count. */
+static int features_in_area(const oo_grid* g, float x, float y, float r, int minLevel,
+                            int maxLevel, int* out) {
+  int n = 0;
+  const int mincx = (int)floorf((x - g->minX - r) * g->wInv);
+  const int nMinX = mincx > 0 ? mincx : 0;
+  if (nMinX >= GRID_COLS) return 0;
+  const int maxcx = (int)ceilf((x - g->minX + r) * g->wInv);
+  const int nMaxX = maxcx < GRID_COLS - 1 ? maxcx : GRID_COLS - 1;
+  if (nMaxX < 0) return 0;
+  const int mincy = (int)floorf((y - g->minY - r) * g->hInv);
+  const int nMinY = mincy > 0 ? mincy : 0;
+  if (nMinY >= GRID_ROWS) return 0;
+  const int maxcy = (int)ceilf((y - g->minY + r) * g->hInv);
+  const int nMaxY = maxcy < GRID_ROWS - 1 ? maxcy : GRID_ROWS - 1;
+  if (nMaxY < 0) return 0;
+  const int bCheckLevels = (minLevel > 0) || (maxLevel >= 0);
+  for (int ix = nMinX; ix <= nMaxX; ix++)
+    for (int iy = nMinY; iy <= nMaxY; iy++) {
+      const int c = ix * GRID_ROWS + iy;
+      for (int j = g->cell_off[c]; j < g->cell_off[c + 1]; ++j) {
+        const int idx = g->cell_feat[j];
+        const oo_keypoint* kp = &g->keys[idx];
+        if (bCheckLevels) {
+          if (kp->octave < minLevel) continue;
+          if (maxLevel >= 0 && kp->octave > maxLevel) continue;
+        }
+        const float distx = kp->x - x, disty = kp->y - y;
+        if (fabsf(distx) < r && fabsf(disty) < r) out[n++] = idx;
+      }
+    }
+  return n;
+}
+
+int oo_features_in_area(int n, const oo_keypoint* keys, float minX, float minY, float wInv,
+                        float hInv, float x, float y, float r, int minLevel, int maxLevel,
+                        int* out) {
+  oo_grid g = {n, keys, minX, minY, wInv, hInv, NULL, NULL};
+  grid_build(&g);
+  const int m = features_in_area(&g, x, y, r, minLevel, maxLevel, out);
+  grid_free(&g);
+  return m;
+}
+
+/* ORBmatcher::SearchByProjection, query form (the caller projects):
+ *   mode 1: (Frame&, vector<MapPoint*>, th)       src/ORBmatcher.cc:19-61
+ *   mode 2: (Frame& Current, const Frame& Last)   src/ORBmatcher.cc:732-818
+ *   mode 3: (Frame& Current, KeyFrame*, set, ...) src/ORBmatcher.cc:820-894
+ * occupied[idx]: mode 1 mvpMapPoints[idx] && Observations() > 0; modes 2/3
+ * mvpMapPoints[idx] != NULL.  match[idx]: -1 or the query that took it. */
+int oo_search_by_projection(int mode, int n, const oo_keypoint* keys, const uint8_t* desc,
+                            const float* uright, const uint8_t* occupied, float minX, float minY,
+                            float wInv, float hInv, int nq, const oo_proj_query* q,
+                            const uint8_t* qdesc, float nnratio, int th_dist, int check_ori,
+                            int32_t* match) {
+  oo_grid g = {n, keys, minX, minY, wInv, hInv, NULL, NULL};
+  grid_build(&g);
+  uint8_t* taken = (uint8_t*)calloc((size_t)(n > 0 ? n : 1), 1);
+  int* cand = (int*)malloc(sizeof(int) * (size_t)(n > 0 ? n : 1));
+  int* hbin = (int*)malloc(sizeof(int) * (size_t)(n > 0 ? n : 1)); /* rotHist as (idx, bin) */
+  int* hidx = (int*)malloc(sizeof(int) * (size_t)(n > 0 ? n : 1));
+  int nh = 0, nmatches = 0;
+  for (int i = 0; i < n; ++i) {
+    match[i] = -1;
+    taken[i] = occupied ? occupied[i] : 0;
+  }
+  const float factor = 1.0f / HISTO_LENGTH;
+  for (int k = 0; k < nq; ++k) {
+    const oo_proj_query* Q = &q[k];
+    const int nc = features_in_area(&g, Q->x, Q->y, Q->radius, Q->min_level, Q->max_level, cand);
+    if (nc == 0) continue;
+    const uint8_t* dq = qdesc + (size_t)k * 32;
+    int bestDist = INT_MAX, bestIdx = -1, secondBestDist = INT_MAX;
+    for (int c = 0; c < nc; ++c) {
+      const int idx = cand[c];
+      if (taken[idx]) continue;
+      if (mode == 1 && uright && uright[idx] > 0) { /* :39-43 */
+        const float er = fabsf(Q->xr - uright[idx]);
+        if (er > Q->radius) continue;
+      }
+      const int dist = oo_descriptor_distance(dq, desc + (size_t)idx * 32);
+      if (dist < bestDist) {
+        secondBestDist = bestDist;
+        bestDist = dist;
+        bestIdx = idx;
+      } else if (dist < secondBestDist) {
+        secondBestDist = dist;
+      }
+    }
+    int ok;
+    if (mode == 1)
+      ok = bestDist <= TH_HIGH && ((float)bestDist <= nnratio * (float)secondBestDist); /* :55 */
+    else
+      ok = bestDist <= th_dist; /* :790 TH_HIGH, :869 ORBdist */
+    if (!ok) continue;
+    match[bestIdx] = k;
+    taken[bestIdx] = 1;
+    nmatches++;
+    if (mode != 1 && check_ori) {
+      float rot = Q->angle - keys[bestIdx].angle;
+      /* mode 3 wraps (:874); mode 2's reference omits it (:796) and indexes
+       * rotHist with a negative bin (UB): upstream ORB-SLAM2's wrap is used */
+      if (rot < 0) rot += 360.0f;
+      const int bin = (int)roundf(rot * factor) % HISTO_LENGTH;
+      hidx[nh] = bestIdx;
+      hbin[nh] = bin;
+      nh++;
+    }
+  }
+  if (mode != 1 && check_ori) {
+    int sizes[HISTO_LENGTH];
+    memset(sizes, 0, sizeof(sizes));
+    for (int i = 0; i < nh; ++i) sizes[hbin[i]]++;
+    int ind1 = -1, ind2 = -1, ind3 = -1;
+    compute_three_maxima(sizes, HISTO_LENGTH, &ind1, &ind2, &ind3);
+    for (int i = 0; i < nh; ++i)
+      if (hbin[i] != ind1 && hbin[i] != ind2 && hbin[i] != ind3) {
+        match[hidx[i]] = -1;
+        nmatches--;
+      }
+  }
+  free(taken);
+  free(cand);
+  free(hbin);
+  free(hidx);
+  grid_free(&g);
+  return nmatches;
+}

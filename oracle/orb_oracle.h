@@ -123,6 +123,26 @@ int oo_vocab_transform(const oo_vocab* v, const uint8_t* desc, int n, int levels
                        uint32_t* bow_word, double* bow_value, int* nbow, uint32_t* fv_node,
                        uint32_t* fv_off, uint32_t* fv_feat, int* nfv);
 
+/* Frame grid (src/Frame.cc:210-225,307-371, 64 x 48 cells) and
+ * ORBmatcher::SearchByProjection in query form: the caller projects (pose
+ * math on cv::Mat) and passes per query the position, the radius handed to
+ * GetFeaturesInArea, its level bounds, mTrackProjXR (mode 1 stereo gate)
+ * and the source keypoint angle (modes 2/3 rotation check). */
+typedef struct {
+  float x, y, radius;
+  int min_level, max_level;
+  float xr;
+  float angle;
+} oo_proj_query;
+int oo_features_in_area(int n, const oo_keypoint* keys, float minX, float minY, float wInv,
+                        float hInv, float x, float y, float r, int minLevel, int maxLevel,
+                        int* out);
+int oo_search_by_projection(int mode, int n, const oo_keypoint* keys, const uint8_t* desc,
+                            const float* uright, const uint8_t* occupied, float minX, float minY,
+                            float wInv, float hInv, int nq, const oo_proj_query* q,
+                            const uint8_t* qdesc, float nnratio, int th_dist, int check_ori,
+                            int32_t* match);
+
 #ifdef __cplusplus
 }
 #endif

@@ -52,7 +52,7 @@ EXPORTED = [
     "orbx_stereo_match", "orbs_plan_create", "orbs_plan_destroy", "orbs_plan_match",
     "orbs_plan_check", "orbs_plan_set_timing", "orbs_plan_stage_times",
     "orbv_vocab_load_text", "orbv_vocab_create", "orbv_vocab_destroy", "orbv_vocab_info",
-    "orbv_transform", "orbv_transform_batch", "orbv_check",
+    "orbv_transform", "orbv_transform_batch", "orbv_check", "orbm_search_by_projection",
 ]
 
 
@@ -75,6 +75,23 @@ class Geometry(ctypes.Structure):
 
     def level(self, name):
         return list(getattr(self, name))[:self.nlevels]
+
+
+class ProjQuery(ctypes.Structure):
+    _fields_ = [("x", ctypes.c_float), ("y", ctypes.c_float), ("radius", ctypes.c_float),
+                ("min_level", ctypes.c_int32), ("max_level", ctypes.c_int32),
+                ("xr", ctypes.c_float), ("angle", ctypes.c_float)]
+
+
+PROJ_QUERY_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("radius", "<f4"), ("min_level", "<i4"),
+                             ("max_level", "<i4"), ("xr", "<f4"), ("angle", "<f4")])
+
+
+class ProjFrame(ctypes.Structure):
+    _fields_ = [("n", ctypes.c_int), ("keys", ctypes.c_void_p), ("desc", ctypes.c_void_p),
+                ("uright", ctypes.c_void_p), ("occupied", ctypes.c_void_p),
+                ("min_x", ctypes.c_float), ("min_y", ctypes.c_float),
+                ("grid_w_inv", ctypes.c_float), ("grid_h_inv", ctypes.c_float)]
 
 
 class BowFrame(ctypes.Structure):
@@ -127,6 +144,7 @@ _sig = {
     "orbv_transform": (I, [P, P, I, I, P, P, P, P, P, P, P]),
     "orbv_transform_batch": (I, [P, I, P, P, I, I, P, P, P, P, P, P, P, P]),
     "orbv_check": (I, [P, P]),
+    "orbm_search_by_projection": (I, [I, P, P, P, I, F, I, I, I, P, P]),
 }
 for _n, (_r, _a) in _sig.items():
     _f = getattr(_lib, _n)
@@ -385,6 +403,28 @@ def descriptor_distance_batch(a, b, ia, ib, device=0):
     _check(_lib.orbm_descriptor_distance_batch(_p(a), len(a), _p(b), len(b), _p(ia), _p(ib),
                                                len(ia), device, _p(out)))
     return out
+
+
+def search_by_projection(mode, frame, queries, qdesc, nnratio=0.6, th_dist=100, check_ori=True,
+                         device=0):
+    """ORBmatcher::SearchByProjection in query form (orbm_search_by_projection).
+    frame = dict(keys, desc, uright|None, occupied|None, min_x, min_y, grid_w_inv,
+    grid_h_inv); queries = PROJ_QUERY_DTYPE array.  Returns (match int32[n], nmatches)."""
+    keys = np.ascontiguousarray(frame["keys"], KEYPOINT_DTYPE)
+    desc = np.ascontiguousarray(frame["desc"], np.uint8).reshape(-1, 32)
+    ur = None if frame.get("uright") is None else np.ascontiguousarray(frame["uright"], np.float32)
+    occ = None if frame.get("occupied") is None else np.ascontiguousarray(frame["occupied"], np.uint8)
+    q = np.ascontiguousarray(queries, PROJ_QUERY_DTYPE)
+    qd = np.ascontiguousarray(qdesc, np.uint8).reshape(-1, 32)
+    F = ProjFrame(len(keys), _p(keys), _p(desc), _p(ur), _p(occ), frame["min_x"], frame["min_y"],
+                  frame["grid_w_inv"], frame["grid_h_inv"])
+    m = np.full(max(len(keys), 1), -1, np.int32)
+    nm = ctypes.c_int(0)
+    _check(_lib.orbm_search_by_projection(mode, ctypes.byref(F), _p(q), _p(qd), len(q),
+                                          float(nnratio), int(th_dist), 1 if check_ori else 0,
+                                          device, _p(m), ctypes.byref(nm)),
+           "orbm_search_by_projection")
+    return m[:len(keys)].copy(), nm.value
 
 
 # --------------------------------------------------------------------------- batched device path
