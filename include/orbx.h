@@ -325,6 +325,23 @@ int orbm_search_by_projection(int mode, const orbx_proj_frame* frame, const orbx
                               const uint8_t* qdesc, int nq, float nnratio, int th_dist,
                               int check_ori, int device, int32_t* match, int* nmatches);
 
+/* ---------------------------------------------------------------------------
+ * SURVEY.md §8f rank 4.
+ * ------------------------------------------------------------------------- */
+/* MapPoint::ComputeDistinctiveDescriptors (src/MapPoint.cc:222-271), batched
+ * over map points: map point m's observation descriptors (mObservations order,
+ * non-bad keyframes) are rows off[m] .. off[m+1]) of desc; best[m] = the row
+ * (relative to off[m]) with the smallest median distance, the first on ties,
+ * -1 for no observation. */
+int orbm_compute_distinctive_descriptors(const uint8_t* desc, const int32_t* off, int nmp,
+                                         int device, int32_t* best);
+/* Frame::UndistortKeyPoints (src/Frame.cc:384-414): K = mK (3x3 row-major,
+ * CV_32F), dist = mDistCoef (ndist = 4 or 5: k1 k2 p1 p2 [k3]).  k1 == 0
+ * copies the keypoints (:386-390); otherwise cv::undistortPoints(.., K, D,
+ * noArray(), K) (OpenCV 3.4: double, 5 iterations).  out may equal kps. */
+int orbx_undistort_keypoints(const orbx_keypoint* kps, int n, const float* K, const float* dist,
+                             int ndist, int device, orbx_keypoint* out);
+
 #ifdef __cplusplus
 }
 #endif

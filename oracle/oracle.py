@@ -62,6 +62,8 @@ def lib():
         L.oo_vocab_transform.argtypes = [P, P, i, i, P, P, P, P, P, P, P]
         L.oo_features_in_area.argtypes = [i, P, f, f, f, f, f, f, f, i, i, P]
         L.oo_search_by_projection.argtypes = [i, i, P, P, P, P, f, f, f, f, i, P, P, f, i, i, P]
+        L.oo_distinctive_descriptor.argtypes = [P, i]
+        L.oo_undistort_keypoints.argtypes = [P, i, P, P, i, P]
         L.oo_compute_stereo_matches.argtypes = [i, P, P, i, P, P, i, P, P, P, P, P, P, P, f, f,
                                                 P, P]
         _lib = L
@@ -353,3 +355,19 @@ def search_by_projection(mode, frame, queries, qdesc, nnratio=0.6, th_dist=100, 
                                        frame["grid_h_inv"], len(q), _p(q), _p(qd), float(nnratio),
                                        int(th_dist), 1 if check_ori else 0, _p(m))
     return m[:len(keys)].copy(), nm
+
+
+def distinctive_descriptor(desc):
+    """MapPoint::ComputeDistinctiveDescriptors: index of the chosen row (-1 if none)."""
+    d = np.ascontiguousarray(desc, np.uint8).reshape(-1, 32)
+    return lib().oo_distinctive_descriptor(_p(d), len(d))
+
+
+def undistort_keypoints(kps, K, dist):
+    """Frame::UndistortKeyPoints (cv::undistortPoints restatement)."""
+    k = np.ascontiguousarray(kps, KEYPOINT_DTYPE)
+    K9 = np.ascontiguousarray(K, np.float32).reshape(9)
+    D = np.ascontiguousarray(dist, np.float32).reshape(-1)
+    out = np.zeros_like(k)
+    lib().oo_undistort_keypoints(_p(k), len(k), _p(K9), _p(D), len(D), _p(out))
+    return out

@@ -1440,3 +1440,70 @@ int oo_search_by_projection(int mode, int n, const oo_keypoint* keys, const uint
   grid_free(&g);
   return nmatches;
 }
+
+/* ---------- MapPoint::ComputeDistinctiveDescriptors (src/MapPoint.cc:222-271) */
+/* desc: the N observation descriptors in mObservations order (std::map over
+ * KeyFrame*, non-bad keyframes).  Returns the index of the descriptor with the
+ * smallest median distance to all (itself included: distances[i][i] = 0), the
+ * first one on ties; -1 if N == 0 (no change). */
+static int cmp_int(const void* a, const void* b) {
+  const int x = *(const int*)a, y = *(const int*)b;
+  return (x > y) - (x < y);
+}
+
+int oo_distinctive_descriptor(const uint8_t* desc, int N) {
+  if (N <= 0) return -1;
+  int* row = (int*)malloc(sizeof(int) * (size_t)N);
+  int bestMedian = INT_MAX, bestIndex = 0;
+  for (int i = 0; i < N; ++i) {
+    for (int j = 0; j < N; ++j)
+      row[j] = (i == j) ? 0 : oo_descriptor_distance(desc + (size_t)i * 32, desc + (size_t)j * 32);
+    /* nth_element(begin, begin + N/2, end): the (N/2)-th smallest value */
+    qsort(row, (size_t)N, sizeof(int), cmp_int);
+    const int median = row[N / 2];
+    if (median < bestMedian) {
+      bestMedian = median;
+      bestIndex = i;
+    }
+  }
+  free(row);
+  return bestIndex;
+}
+
+/* ---------- Frame::UndistortKeyPoints (src/Frame.cc:384-414) --------------
+ * cv::undistortPoints(src, dst, K, D, noArray(), K) of OpenCV 3.4
+ * (undistort.cpp cvUndistortPointsInternal): double arithmetic, 5 fixed
+ * iterations (TermCriteria(COUNT, 5, 0.01)), no tilt, R = I, P = K.  OpenCV's
+ * x86-64 baseline (SSE3) has no FMA: no contraction.  parity unpinned
+ * (OpenCV is not in the image). */
+void oo_undistort_keypoints(const oo_keypoint* in, int n, const float* K9, const float* dist,
+                            int ndist, oo_keypoint* out) {
+  for (int i = 0; i < n; ++i) out[i] = in[i];
+  if (ndist <= 0 || dist[0] == 0.0f) return; /* mvKeysUn = mvKeys (:386-390) */
+  double k[14] = {0};
+  for (int j = 0; j < ndist && j < 14; ++j) k[j] = (double)dist[j];
+  const double fx = K9[0], fy = K9[4], cx = K9[2], cy = K9[5];
+  const double ifx = 1. / fx, ify = 1. / fy;
+  for (int i = 0; i < n; ++i) {
+    double x = in[i].x, y = in[i].y, x0, y0;
+    x = (x - cx) * ifx;
+    y = (y - cy) * ify;
+    x0 = x;
+    y0 = y;
+    for (int j = 0; j < 5; j++) {
+      const double r2 = x * x + y * y;
+      const double icdist = (1 + ((k[7] * r2 + k[6]) * r2 + k[5]) * r2) /
+                            (1 + ((k[4] * r2 + k[1]) * r2 + k[0]) * r2);
+      const double deltaX = 2 * k[2] * x * y + k[3] * (r2 + 2 * x * x) + k[8] * r2 + k[9] * r2 * r2;
+      const double deltaY = k[2] * (r2 + 2 * y * y) + 2 * k[3] * x * y + k[10] * r2 + k[11] * r2 * r2;
+      x = (x0 - deltaX) * icdist;
+      y = (y0 - deltaY) * icdist;
+    }
+    /* RR = P * I = K: xx = fx*x + 0*y + cx, yy = 0*x + fy*y + cy, ww = 1/(0*x + 0*y + 1) */
+    const double xx = fx * x + 0. * y + cx;
+    const double yy = 0. * x + fy * y + cy;
+    const double ww = 1. / (0. * x + 0. * y + 1.);
+    out[i].x = (float)(xx * ww);
+    out[i].y = (float)(yy * ww);
+  }
+}

@@ -143,6 +143,12 @@ int oo_search_by_projection(int mode, int n, const oo_keypoint* keys, const uint
                             const uint8_t* qdesc, float nnratio, int th_dist, int check_ori,
                             int32_t* match);
 
+/* MapPoint::ComputeDistinctiveDescriptors (src/MapPoint.cc:222-271) */
+int oo_distinctive_descriptor(const uint8_t* desc, int N);
+/* Frame::UndistortKeyPoints (src/Frame.cc:384-414) with cv::undistortPoints */
+void oo_undistort_keypoints(const oo_keypoint* in, int n, const float* K9, const float* dist,
+                            int ndist, oo_keypoint* out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,91 @@
+// kernels_misc.hip -- gfx950 kernels of SURVEY.md §8f rank 4:
+//   MapPoint::ComputeDistinctiveDescriptors (src/MapPoint.cc:222-271) -> k_distinctive
+//   Frame::UndistortKeyPoints (src/Frame.cc:384-414, cv::undistortPoints) -> k_undistort
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/orbx.h"
+
+namespace orbx {
+
+__device__ __forceinline__ int hamming32(const uint8_t* a, const uint8_t* b) {
+  const uint4* pa = reinterpret_cast<const uint4*>(a);
+  const uint4* pb = reinterpret_cast<const uint4*>(b);
+  const uint4 a0 = pa[0], a1 = pa[1], b0 = pb[0], b1 = pb[1];
+  return __popc(a0.x ^ b0.x) + __popc(a0.y ^ b0.y) + __popc(a0.z ^ b0.z) + __popc(a0.w ^ b0.w) +
+         __popc(a1.x ^ b1.x) + __popc(a1.y ^ b1.y) + __popc(a1.z ^ b1.z) + __popc(a1.w ^ b1.w);
+}
+
+// One wavefront per map point; lane = observation row i.  The median of row
+// i (nth_element at N/2 over the N distances, d_ii = 0 included) is the
+// smallest v with #{j : d_ij <= v} > N/2, found by a binary search over the
+// distance range [0, 256]; the chosen row is the first minimum (strict '<').
+__global__ __launch_bounds__(256) void k_distinctive(const uint8_t* __restrict__ desc,
+                                                     const int32_t* __restrict__ off, int nmp,
+                                                     int32_t* __restrict__ best) {
+  const int lane = threadIdx.x & 63;
+  const int m = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (m >= nmp) return;
+  const int b = off[m], N = off[m + 1] - b;
+  if (N <= 0) {
+    if (lane == 0) best[m] = -1;
+    return;
+  }
+  const uint8_t* D = desc + (size_t)b * 32;
+  const int need = N / 2 + 1;
+  uint32_t bk = 0xFFFFFFFFu;  // (median << 20) | i
+  for (int i0 = 0; i0 < N; i0 += 64) {
+    const int i = i0 + lane;
+    if (i < N) {
+      int lo = 0, hi = 256;  // count(hi) = N >= need
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        int c = 0;
+        for (int j = 0; j < N; ++j) c += (j == i ? 0 : hamming32(D + (size_t)i * 32, D + (size_t)j * 32)) <= mid;
+        if (c >= need) hi = mid; else lo = mid + 1;
+      }
+      bk = min(bk, ((uint32_t)lo << 20) | (uint32_t)i);
+    }
+  }
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) bk = min(bk, (uint32_t)__shfl_xor((int)bk, d, 64));
+  if (lane == 0) best[m] = (int32_t)(bk & 0xFFFFFu);
+}
+
+struct UndistortArgs {
+  double fx, fy, cx, cy, ifx, ify;
+  double k[14];
+};
+
+// cv::undistortPoints (OpenCV 3.4 undistort.cpp) in double, 5 iterations,
+// R = I, P = K; operation order as written there (no contraction: the
+// translation unit is built with -ffp-contract=off)
+__global__ __launch_bounds__(256) void k_undistort(const orbx_keypoint* __restrict__ in, int n,
+                                                   const UndistortArgs A,
+                                                   orbx_keypoint* __restrict__ out) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  orbx_keypoint kp = in[i];
+  double x = kp.x, y = kp.y;
+  x = (x - A.cx) * A.ifx;
+  y = (y - A.cy) * A.ify;
+  const double x0 = x, y0 = y;
+  const double* k = A.k;
+  for (int j = 0; j < 5; j++) {
+    const double r2 = x * x + y * y;
+    const double icdist = (1 + ((k[7] * r2 + k[6]) * r2 + k[5]) * r2) /
+                          (1 + ((k[4] * r2 + k[1]) * r2 + k[0]) * r2);
+    const double deltaX = 2 * k[2] * x * y + k[3] * (r2 + 2 * x * x) + k[8] * r2 + k[9] * r2 * r2;
+    const double deltaY = k[2] * (r2 + 2 * y * y) + 2 * k[3] * x * y + k[10] * r2 + k[11] * r2 * r2;
+    x = (x0 - deltaX) * icdist;
+    y = (y0 - deltaY) * icdist;
+  }
+  const double xx = A.fx * x + 0. * y + A.cx;
+  const double yy = 0. * x + A.fy * y + A.cy;
+  const double ww = 1. / (0. * x + 0. * y + 1.);
+  kp.x = (float)(xx * ww);
+  kp.y = (float)(yy * ww);
+  out[i] = kp;
+}
+
+}  // namespace orbx

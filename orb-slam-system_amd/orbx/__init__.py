@@ -53,6 +53,7 @@ EXPORTED = [
     "orbs_plan_check", "orbs_plan_set_timing", "orbs_plan_stage_times",
     "orbv_vocab_load_text", "orbv_vocab_create", "orbv_vocab_destroy", "orbv_vocab_info",
     "orbv_transform", "orbv_transform_batch", "orbv_check", "orbm_search_by_projection",
+    "orbm_compute_distinctive_descriptors", "orbx_undistort_keypoints",
 ]
 
 
@@ -145,6 +146,8 @@ _sig = {
     "orbv_transform_batch": (I, [P, I, P, P, I, I, P, P, P, P, P, P, P, P]),
     "orbv_check": (I, [P, P]),
     "orbm_search_by_projection": (I, [I, P, P, P, I, F, I, I, I, P, P]),
+    "orbm_compute_distinctive_descriptors": (I, [P, P, I, I, P]),
+    "orbx_undistort_keypoints": (I, [P, I, P, P, I, I, P]),
 }
 for _n, (_r, _a) in _sig.items():
     _f = getattr(_lib, _n)
@@ -425,6 +428,31 @@ def search_by_projection(mode, frame, queries, qdesc, nnratio=0.6, th_dist=100, 
                                           device, _p(m), ctypes.byref(nm)),
            "orbm_search_by_projection")
     return m[:len(keys)].copy(), nm.value
+
+
+def compute_distinctive_descriptors(groups, device=0):
+    """MapPoint::ComputeDistinctiveDescriptors for a list of (N_m, 32) descriptor
+    arrays; returns int32[len(groups)] chosen rows (-1 for empty)."""
+    off = np.zeros(len(groups) + 1, np.int32)
+    off[1:] = np.cumsum([len(g) for g in groups])
+    desc = np.ascontiguousarray(np.concatenate([np.asarray(g, np.uint8).reshape(-1, 32)
+                                                for g in groups]) if groups else
+                                np.zeros((0, 32), np.uint8))
+    best = np.zeros(max(len(groups), 1), np.int32)
+    _check(_lib.orbm_compute_distinctive_descriptors(_p(desc), _p(off), len(groups), device,
+                                                     _p(best)), "distinctive descriptors")
+    return best[:len(groups)].copy()
+
+
+def undistort_keypoints(kps, K, dist, device=0):
+    """Frame::UndistortKeyPoints (cv::undistortPoints, OpenCV 3.4 algorithm)."""
+    k = np.ascontiguousarray(kps, KEYPOINT_DTYPE)
+    K9 = np.ascontiguousarray(K, np.float32).reshape(9)
+    D = np.ascontiguousarray(dist, np.float32).reshape(-1)
+    out = np.zeros_like(k)
+    _check(_lib.orbx_undistort_keypoints(_p(k), len(k), _p(K9), _p(D), len(D), device, _p(out)),
+           "orbx_undistort_keypoints")
+    return out
 
 
 # --------------------------------------------------------------------------- batched device path
