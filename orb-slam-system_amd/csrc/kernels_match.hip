@@ -36,6 +36,24 @@ __device__ __forceinline__ int hamming_u(const uint32_t d1[8], const uint32_t* b
          __popc(d1[6] ^ b1.z) + __popc(d1[7] ^ b1.w);
 }
 
+// 256-bit Hamming distance as one accumulate chain: v_bcnt_u32_b32 adds its
+// second operand, so 8 xor + 8 bcnt (the compiler's add3 trees cost 3 more)
+__device__ __forceinline__ uint32_t bcnt_acc(uint32_t x, uint32_t acc) {
+  uint32_t r;
+  asm("v_bcnt_u32_b32 %0, %1, %2" : "=v"(r) : "v"(x), "v"(acc));
+  return r;
+}
+__device__ __forceinline__ uint32_t ham256(uint4 a0, uint4 a1, uint4 b0, uint4 b1) {
+  uint32_t d = bcnt_acc(a0.x ^ b0.x, 0u);
+  d = bcnt_acc(a0.y ^ b0.y, d);
+  d = bcnt_acc(a0.z ^ b0.z, d);
+  d = bcnt_acc(a0.w ^ b0.w, d);
+  d = bcnt_acc(a1.x ^ b1.x, d);
+  d = bcnt_acc(a1.y ^ b1.y, d);
+  d = bcnt_acc(a1.z ^ b1.z, d);
+  return bcnt_acc(a1.w ^ b1.w, d);
+}
+
 __device__ __forceinline__ int find_node_pair(const MNodePair* nps, int nnp, int r) {
   int lo = 0, hi = nnp;  // last np with row_base <= r
   while (lo < hi) {
@@ -320,9 +338,7 @@ __global__ __launch_bounds__(256) void k_match_cand_rows(
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
       const uint4 b0 = bd[2 * q], b1 = bd[2 * q + 1];
-      const uint32_t d = __popc(q0.x ^ b0.x) + __popc(q0.y ^ b0.y) + __popc(q0.z ^ b0.z) +
-                         __popc(q0.w ^ b0.w) + __popc(q1.x ^ b1.x) + __popc(q1.y ^ b1.y) +
-                         __popc(q1.z ^ b1.z) + __popc(q1.w ^ b1.w);
+      const uint32_t d = ham256(q0, q1, b0, b1);
       const uint32_t inval = ((vw >> q) & 1u) - 1u;  // 0 or 0xFFFFFFFF (uniform)
       kk[q] = ((d << 16) | (uint32_t)(j0 + q)) | inval;
     }
