@@ -4,6 +4,8 @@
 //   orbx::ORBextractor  <->  ORB_SLAM2::ORBextractor  (reference include/ORBextractor.h:25-91)
 //   orbx::ORBmatcher    <->  ORB_SLAM2::ORBmatcher    (reference include/ORBmatcher.h:16-81)
 //   orbx::ComputeStereoMatches <-> Frame::ComputeStereoMatches (reference src/Frame.cc:446-620)
+//   orbx::ORBVocabulary <-> DBoW2::TemplatedVocabulary<FORB> (Thirdparty/DBoW2/DBoW2/TemplatedVocabulary.h)
+//   orbx::UndistortKeyPoints / ComputeDistinctiveDescriptor <-> Frame.cc:384-414 / MapPoint.cc:222-271
 //
 // Same constructor arguments, same getters, same operator() contract
 // (keypoints cleared and refilled level-major; untouched when no keypoint
@@ -193,6 +195,25 @@ class ORBmatcher {
     return n;
   }
 
+  // SearchByProjection (ORBmatcher.cc:19-61 / 732-818 / 820-894) in query
+  // form: the caller projects and fills one orbx_query_proj per map point (see
+  // include/orbx.h); matches[i] = the query that took frame feature i, or -1.
+  //   mode 1: (Frame&, vector<MapPoint*>, th)        -- ratio test mfNNratio
+  //   mode 2: (Frame& Current, const Frame& Last)    -- th_dist = TH_HIGH
+  //   mode 3: (Frame& Current, KeyFrame*, set, ...)  -- th_dist = ORBdist
+  int SearchByProjection(int mode, const orbx_proj_frame& frame,
+                         const std::vector<orbx_query_proj>& queries,
+                         const std::vector<uint8_t>& query_desc, int th_dist,
+                         std::vector<int32_t>& matches) const {
+    matches.assign(frame.n, -1);
+    int n = 0;
+    check(orbm_search_by_projection(mode, &frame, queries.data(), query_desc.data(),
+                                    (int)queries.size(), mfNNratio, th_dist,
+                                    mbCheckOrientation ? 1 : 0, device_, matches.data(), &n),
+          "SearchByProjection");
+    return n;
+  }
+
   // SearchByBoW(KeyFrame*, Frame&, ...) in the reference is a stub that
   // returns 0 and leaves every match null (ORBmatcher.cc:88-119); kept as is.
   int SearchByBoWFrame(const KeyFrameView&, int frameN, std::vector<int32_t>& matches) const {
@@ -217,6 +238,79 @@ class ORBmatcher {
   bool mbCheckOrientation;
   int device_;
 };
+
+// DBoW2 vocabulary (ORBVocabulary) on the device: loadFromTextFile and
+// transform(features, BowVector&, FeatureVector&, levelsup).
+struct BowVector {
+  std::vector<uint32_t> word;  // ascending (std::map order)
+  std::vector<double> value;
+};
+
+class ORBVocabulary {
+ public:
+  explicit ORBVocabulary(int device = 0) : device_(device) {}
+  ~ORBVocabulary() { orbv_vocab_destroy(v_); }
+  ORBVocabulary(const ORBVocabulary&) = delete;
+  ORBVocabulary& operator=(const ORBVocabulary&) = delete;
+
+  bool loadFromTextFile(const std::string& filename) {
+    orbv_vocab* v = nullptr;
+    if (orbv_vocab_load_text(filename.c_str(), device_, &v) != ORBX_OK) return false;
+    orbv_vocab_destroy(v_);
+    v_ = v;
+    return true;
+  }
+  bool empty() const {
+    int nwords = 0;
+    return !v_ || orbv_vocab_info(v_, nullptr, nullptr, nullptr, nullptr, nullptr, &nwords) ||
+           nwords == 0;
+  }
+  // descriptors: n x 32 (mDescriptors); Frame::ComputeBoW uses levelsup = 4
+  void transform(const uint8_t* descriptors, int n, BowVector& bow, FeatureVector& fv,
+                 int levelsup) const {
+    bow.word.assign(n, 0);
+    bow.value.assign(n, 0.0);
+    fv.node_id.assign(n, 0);
+    fv.node_off.assign(n + 1, 0);
+    fv.feat.assign(n, 0);
+    int nb = 0, nf = 0;
+    check(orbv_transform(v_, descriptors, n, levelsup, bow.word.data(), bow.value.data(), &nb,
+                         fv.node_id.data(), fv.node_off.data(), fv.feat.data(), &nf),
+          "ORBVocabulary::transform");
+    bow.word.resize(nb);
+    bow.value.resize(nb);
+    fv.node_id.resize(nf);
+    fv.node_off.resize(nf + 1);
+    fv.feat.resize(fv.node_off[nf]);
+  }
+
+ private:
+  orbv_vocab* v_ = nullptr;
+  int device_;
+};
+
+// Frame::UndistortKeyPoints (src/Frame.cc:384-414): mvKeysUn from mvKeys,
+// K = mK (row-major 3x3), dist = mDistCoef (k1 k2 p1 p2 [k3]).
+inline std::vector<KeyPoint> UndistortKeyPoints(const std::vector<KeyPoint>& keys,
+                                                const float K[9], const std::vector<float>& dist,
+                                                int device = 0) {
+  std::vector<KeyPoint> out(keys.size());
+  check(orbx_undistort_keypoints(reinterpret_cast<const orbx_keypoint*>(keys.data()),
+                                 (int)keys.size(), K, dist.data(), (int)dist.size(), device,
+                                 reinterpret_cast<orbx_keypoint*>(out.data())),
+        "UndistortKeyPoints");
+  return out;
+}
+
+// MapPoint::ComputeDistinctiveDescriptors (src/MapPoint.cc:222-271): the row
+// of the observation descriptors (n x 32, mObservations order) to keep.
+inline int ComputeDistinctiveDescriptor(const uint8_t* descriptors, int n, int device = 0) {
+  const int32_t off[2] = {0, n};
+  int32_t best = -1;
+  check(orbm_compute_distinctive_descriptors(descriptors, off, 1, device, &best),
+        "ComputeDistinctiveDescriptors");
+  return best;
+}
 
 // Frame::ComputeStereoMatches (src/Frame.cc:446-620) for a rectified pair
 // whose images were the last operator() calls of `left` and `right` (the

@@ -93,3 +93,51 @@ def test_cpp_stereo_adapter_matches_oracle(gpu, oracle, tmp_path):
     assert n == n0
     assert np.array_equal(ur.view(np.uint32), ur0.view(np.uint32))
     assert np.array_equal(dep.view(np.uint32), dep0.view(np.uint32))
+
+
+def _build_vocab(tmp_path):
+    exe = tmp_path / "vocab_main"
+    subprocess.check_call(["g++", "-O2", "-std=c++17", "-I", os.path.join(PKG, "cpp"),
+                           os.path.join(ROOT, "tests", "cpp", "vocab_main.cpp"), "-o", str(exe),
+                           "-L", PKG, "-lorbx", "-Wl,-rpath," + PKG])
+    return exe
+
+
+def test_cpp_vocab_adapter_compiles(tmp_path):
+    assert _build_vocab(tmp_path).exists()
+
+
+@pytest.mark.gpu
+def test_cpp_vocab_adapter_matches_oracle(gpu, oracle, tmp_path):
+    exe = _build_vocab(tmp_path)
+    W, H = 1241, 376
+    voc = synth.vocabulary(10, 5, seed=3)
+    synth.write_vocabulary_text(tmp_path / "voc.txt", voc)
+    a, b = synth.frame(W, H, 61), synth.frame(W, H, 62)
+    (tmp_path / "a.raw").write_bytes(a.tobytes())
+    (tmp_path / "b.raw").write_bytes(b.tobytes())
+    out = tmp_path / "out.bin"
+    subprocess.check_call([str(exe), str(tmp_path / "voc.txt"), str(tmp_path / "a.raw"),
+                           str(tmp_path / "b.raw"), str(W), str(H), str(out)])
+    raw = out.read_bytes()
+    n1, nb, nf, nm = np.frombuffer(raw[:16], np.int32).tolist()
+    off = 16
+    bw = np.frombuffer(raw[off:off + 4 * nb], np.uint32); off += 4 * nb
+    bv = np.frombuffer(raw[off:off + 8 * nb], np.float64); off += 8 * nb
+    fn = np.frombuffer(raw[off:off + 4 * nf], np.uint32); off += 4 * nf
+    fo = np.frombuffer(raw[off:off + 4 * (nf + 1)], np.uint32); off += 4 * (nf + 1)
+    ff = np.frombuffer(raw[off:off + 4 * int(fo[-1])], np.uint32); off += 4 * int(fo[-1])
+    m12 = np.frombuffer(raw[off:off + 4 * n1], np.int32)
+    ex = oracle.Extractor(2000, 1.2, 8, 20, 7)
+    k1, d1 = ex.extract(a)
+    k2, d2 = ex.extract(b)
+    ov = oracle.Vocabulary.load_text(tmp_path / "voc.txt")
+    (rbw, rbv), rfv1 = ov.transform(d1, 4)
+    _, rfv2 = ov.transform(d2, 4)
+    assert np.array_equal(bw, rbw) and np.array_equal(bv.view(np.uint64), rbv.view(np.uint64))
+    assert np.array_equal(fn, rfv1["node_id"]) and np.array_equal(fo, rfv1["off"])
+    assert np.array_equal(ff, rfv1["feat"])
+    kf1 = dict(desc=d1, angle=k1["angle"], valid=None, **rfv1)
+    kf2 = dict(desc=d2, angle=k2["angle"], valid=None, **rfv2)
+    rm, rnm = oracle.search_by_bow(kf1, kf2, 0.75, True)
+    assert nm == rnm and np.array_equal(m12, rm)
