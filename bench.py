@@ -180,20 +180,19 @@ def main():
     desc = torch.zeros((B + 1, kcap, 32), dtype=torch.uint8, device=dev)
     counts = torch.zeros(B + 1, dtype=torch.int32, device=dev)
     xch = BoundaryExchange(kcap, world, dev)
-    prev_rank = (rank - 1) % world
 
     def step():
-        # slot 0 <- last frame of the previous step: own (1 GPU) or, in frame-
-        # sharded multi-GPU runs, the previous rank's via RCCL all-gather
-        if world > 1:
-            xch.pack(kps[B], desc[B], counts[B:B + 1])
-            xch.exchange(dist)
-            xch.unpack_into(prev_rank, kps[0], desc[0], counts[0:1])
-        else:
+        # slot 0 <- the predecessor of this step's first frame: on 1 GPU the
+        # previous step's last frame; frame-sharded over N GPUs the previous
+        # rank's last frame of this step, via an RCCL all-gather (orbx.dist)
+        if world == 1:
             kps[0].copy_(kps[B])
             desc[0].copy_(desc[B])
             counts[0:1].copy_(counts[B:B + 1])
         plan.extract(frames, out=(kps[1:], desc[1:], counts[1:]))
+        if world > 1:
+            xch.ring_step(dist, rank, (kps[B], desc[B], counts[B:B + 1]),
+                          (kps[0], desc[0], counts[0:1]))
         mp.match(B, kps[1:], desc[1:], counts[1:], kps, desc, counts, args.nnratio, True)
 
     for _ in range(args.warmup):
@@ -313,20 +312,18 @@ def main_c5(args):
     desc = torch.zeros((B + 1, kcap, 32), dtype=torch.uint8, device=dev)
     counts = torch.zeros(B + 1, dtype=torch.int32, device=dev)
     xch = BoundaryExchange(kcap, world, dev)
-    prev_rank = (rank - 1) % world
     mb, mbf = KITTI_BF / KITTI_FX, KITTI_BF
 
     def step():
-        if world > 1:
-            xch.pack(kps[B], desc[B], counts[B:B + 1])
-            xch.exchange(dist)
-            xch.unpack_into(prev_rank, kps[0], desc[0], counts[0:1])
-        else:
+        if world == 1:
             kps[0].copy_(kps[B])
             desc[0].copy_(desc[B])
             counts[0:1].copy_(counts[B:B + 1])
         pl.extract(fl, out=(kps[1:], desc[1:], counts[1:]))
         pr.extract(fr)
+        if world > 1:
+            xch.ring_step(dist, rank, (kps[B], desc[B], counts[B:B + 1]),
+                          (kps[0], desc[0], counts[0:1]))
         sp.match(pl, pr, fl, fr, mb, mbf, left_out=(kps[1:], desc[1:], counts[1:]))
         mp.match(B, kps[1:], desc[1:], counts[1:], kps, desc, counts, args.nnratio, True)
 

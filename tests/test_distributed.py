@@ -43,6 +43,21 @@ def _worker(rank, world, port, kcap, q):
         ed = torch.randint(0, 256, (kcap, 32), dtype=torch.uint8, generator=g2)
         ok = bool(torch.equal(k0, ek) and torch.equal(d0, ed) and int(c0[0]) == 100 + prev)
         ok = ok and shard_first_frame(rank, 8, step=3, world=world) == 3 * world * 8 + rank * 8
+        # ring_step over two steps: rank r > 0 gets rank r-1's frame of the same
+        # step; rank 0 gets rank W-1's frame of the previous step (zeros first)
+        y = BoundaryExchange(kcap, world, torch.device("cpu"))
+        for st in range(2):
+            last = (torch.full((kcap, 28), 10 * st + rank, dtype=torch.uint8),
+                    torch.full((kcap, 32), 10 * st + rank, dtype=torch.uint8),
+                    torch.tensor([10 * st + rank], dtype=torch.int32))
+            s0 = (torch.empty((kcap, 28), dtype=torch.uint8),
+                  torch.empty((kcap, 32), dtype=torch.uint8), torch.zeros(1, dtype=torch.int32))
+            y.ring_step(dist, rank, last, s0)
+            if rank > 0:
+                want = 10 * st + rank - 1
+            else:
+                want = 0 if st == 0 else 10 * (st - 1) + world - 1
+            ok = ok and int(s0[2][0]) == want and int(s0[0][0, 0]) == want
         q.put((rank, ok))
     finally:
         dist.destroy_process_group()
