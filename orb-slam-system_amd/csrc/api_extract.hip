@@ -151,6 +151,7 @@ extern "C" int orbx_plan_create(const orbx_params* prm, int width, int height, i
   if (device < 0 || device >= ndev) return ORBX_ERR_NO_DEVICE;
   orbx_plan* p = new orbx_plan();
   if (const char* e = getenv("ORBX_DEBUG_STOP")) p->dbg = atoi(e);
+  if (const char* e = getenv("ORBX_DEBUG_OBDIV")) p->ob_div = atoi(e);
   int rc = plan_geometry(*prm, width, height, p->P);
   if (rc) { delete p; return rc; }
   const Plan& P = p->P;
@@ -299,7 +300,8 @@ extern "C" int orbx_plan_extract(orbx_plan* p, const uint8_t* frames, int nframe
   // K4+K5+K6+K7 orientation, blur-at-sample descriptors, assembly
   p->timer.begin(ORBX_STAGE_BRIEF, s);
   // waves stride over each frame's keypoints (about nfeatures of them)
-  const int ob_waves = std::max(4, std::min(P.kcap, P.params.nfeatures + 256));
+  int ob_waves = std::max(4, std::min(P.kcap, P.params.nfeatures + 256));
+  if (p->ob_div > 1) ob_waves = std::max(4, ob_waves / p->ob_div); /* profiling only */
   hipLaunchKernelGGL(k_orient_brief, dim3((ob_waves + 3) / 4, n),
                      dim3(256), 0, s, frames, fstride, rstride, p->d_pyr, p->pyr_stride, p->bargs,
                      p->d_qout, p->qout_stride, p->d_lcount, kps, desc,

@@ -1018,24 +1018,35 @@ __global__ __launch_bounds__(256) void k_orient_brief(
     if (cur.aligned) brief_issue(cur, R, lane);
   }
   const int l = me.l, x = me.x, score = me.score, px0 = me.px0;
-  const uint8_t* P8 = reinterpret_cast<const uint8_t*>(P);
-  // IC_Angle (:21-48) on the unblurred level: lane = patch row v + 15,
-  // u in [-umax[|v|], umax[|v|]] (integer sums: order-free)
+  // IC_Angle (:21-48) on the unblurred level (integer sums: order-free).
+  // Lane (< 62) = patch row v = lane/2 - 15, half = lane & 1: five dwords of
+  // the row (columns 4..23 or 24..43; the disk spans cc-15..cc+15 <= 39).
+  // The disk's byte mask (|u| <= umax[|v|]) comes from a 20-bit column mask,
+  // four bits per dword spread to bytes by a multiply; sum I and
+  // sum (u + 19) I are two v_dot4_u32_u8 per dword (weights u + 19 keep every
+  // byte of a touched dword in 1..37: no borrow between bytes).
   const int cc = x - px0, cr = KP_R;
   int m10 = 0, m01 = 0;
-  if (lane < 31) {
-    const int v = lane - 15, av = v < 0 ? -v : v;
+  if (lane < 62) {
+    const int v = (lane >> 1) - 15, av = v < 0 ? -v : v;
     const uint32_t uw = (av >> 2) == 0 ? A.umaxw[0] : (av >> 2) == 1 ? A.umaxw[1]
                       : (av >> 2) == 2 ? A.umaxw[2] : A.umaxw[3];
     const int um = (int)((uw >> (8 * (av & 3))) & 0xFFu);
-    const uint8_t* rowp = P8 + (cr + v) * KP_COLS + cc;
-    int sum = 0;
-    for (int uu = -um; uu <= um; ++uu) {
-      const int I = rowp[uu];
-      sum += I;
-      m10 += uu * I;
+    const int b0 = (lane & 1) ? 24 : 4;
+    const int nhi = min(max(cc + um - b0 + 1, 0), 20), nlo = min(max(cc - um - b0, 0), 20);
+    const uint32_t bits = ((1u << nhi) - 1u) & ~((1u << nlo) - 1u);
+    const uint32_t* rowp = &P[cr + v][b0 >> 2];
+    const uint32_t W = (uint32_t)(b0 - cc + 19) * 0x01010101u + 0x03020100u;
+    uint32_t s = 0, m = 0;
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+      const uint32_t ones = (__umul24((bits >> (4 * k)) & 0xFu, 0x00204081u)) & 0x01010101u;
+      const uint32_t I = rowp[k];
+      s = __builtin_amdgcn_udot4(I, ones, s, false);
+      m = __builtin_amdgcn_udot4(I, (W + 0x04040404u * k) & ((ones << 8) - ones), m, false);
     }
-    m01 = v * sum;
+    m10 = (int)m - 19 * (int)s;
+    m01 = __mul24(v, (int)s);
   }
 #pragma unroll
   for (int d = 32; d >= 1; d >>= 1) {
@@ -1066,14 +1077,16 @@ __global__ __launch_bounds__(256) void k_orient_brief(
       const int col = (int)__builtin_rintf(__builtin_fmaf(fx, cs, -yb));
       const int r0 = cr + row - 3, c0 = cc + col - 3;
       const int qd = c0 >> 2, sh = c0 & 3;
+      const uint32_t* prow = &P[0][0] + __mul24(r0, KP_COLS / 4) + qd;  // |r0| < 64: 24-bit multiply
       uint32_t acc = 0;
 #pragma unroll
       for (int jj = 0; jj < 7; ++jj) {
-        const uint32_t w0 = P[r0 + jj][qd], w1 = P[r0 + jj][qd + 1], w2 = P[r0 + jj][qd + 2];
+        const uint32_t w0 = prow[jj * (KP_COLS / 4)], w1 = prow[jj * (KP_COLS / 4) + 1],
+                       w2 = prow[jj * (KP_COLS / 4) + 2];
         const uint32_t lo4 = __builtin_amdgcn_alignbyte(w1, w0, sh);
         const uint32_t hi4 = __builtin_amdgcn_alignbyte(w2, w1, sh);
         const uint32_t h = __builtin_amdgcn_udot4(hi4, K1, __builtin_amdgcn_udot4(lo4, K0, 0u, false), false);
-        acc += GK[jj] * h;
+        acc = __umul24(h, GK[jj]) + acc;  // v_mad_u32_u24: h <= 65280 (v_mul_lo_u32 is quarter rate)
       }
       t[e] = (int)min((acc + 32768u) >> 16, 255u);
     }
