@@ -249,7 +249,10 @@ static bool try_segment(Plan& P, const std::vector<int>& lev, int TW, int TH, Py
 }
 
 /* per tile column / row LUT blobs (layout: orbx_internal.h) */
-static void build_blobs(Plan& P, const std::vector<int>& lev, PyrSeg& g, const std::vector<Iv>& xs,
+/* returns false when k_pyramid's packed arithmetic does not apply: the 4
+ * columns of a thread must read bytes within 8 of the first one's sx, and
+ * every coefficient must lie in [0, 4095] (INTER_LINEAR downscale: [0, 2048]) */
+static bool build_blobs(Plan& P, const std::vector<int>& lev, PyrSeg& g, const std::vector<Iv>& xs,
                         const std::vector<Iv>& ys) {
   const int ns = (int)lev.size();
   for (int axis = 0; axis < 2; ++axis) {
@@ -275,11 +278,15 @@ static void build_blobs(Plan& P, const std::vector<int>& lev, PyrSeg& g, const s
           e = c.chi;
         }
         if (c.chi <= c.clo) e = b;
+        int glo = 0;
         for (int d = b; d < e; ++d) {
           const int dd = std::min(std::max(d, c.clo), c.chi - 1);
           int lo, hi;
           src_span(P, lev[s], isx, dd, lo, hi);
           const int16_t* cf = isx ? &P.alpha[2 * (lv.lut_x + dd)] : &P.beta[2 * (lv.lut_y + dd)];
+          if (cf[0] < 0 || cf[0] > 4095 || cf[1] < 0 || cf[1] > 4095) return false;
+          if (isx && ((d - b) & 3) == 0) glo = lo;
+          if (isx && hi - glo > 7) return false;
           P.pyr_blob.push_back((uint32_t)(lo - origin) | ((uint32_t)(hi - origin) << 16));
           P.pyr_blob.push_back((uint32_t)(uint16_t)cf[0] | ((uint32_t)(uint16_t)cf[1] << 16));
           ++n;
@@ -291,6 +298,7 @@ static void build_blobs(Plan& P, const std::vector<int>& lev, PyrSeg& g, const s
     P.pyr_bo.push_back((int)(P.pyr_blob.size() / 2));
     (isx ? g.lds_xl : g.lds_yl) = 8 * maxn;
   }
+  return true;
 }
 
 /* greedy: longest run of unique levels from `first` that fits a tile of at
@@ -322,7 +330,7 @@ static int plan_pyramid(Plan& P) {
         g.ys_off = (int)(P.pyr_ys.size() / 4);
         for (const Iv& v : xs) P.pyr_xs.insert(P.pyr_xs.end(), {v.clo, v.chi, v.plo, v.phi});
         for (const Iv& v : ys) P.pyr_ys.insert(P.pyr_ys.end(), {v.clo, v.chi, v.plo, v.phi});
-        build_blobs(P, lev, g, xs, ys);
+        if (!build_blobs(P, lev, g, xs, ys)) return ORBX_ERR_UNSUPPORTED;
         P.segs.push_back(g);
         i = j;
         done = true;

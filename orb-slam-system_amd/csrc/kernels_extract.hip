@@ -71,6 +71,10 @@ __device__ __forceinline__ void stage_region(uint8_t* __restrict__ lds, int lpit
   }
 }
 
+typedef unsigned short us2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ us2 as_us2(uint32_t x) { return __builtin_bit_cast(us2, x); }
+__device__ __forceinline__ uint32_t as_u32(us2 x) { return __builtin_bit_cast(uint32_t, x); }
+
 // ---------------------------------------------------------------------------
 // k_pyramid: a chain of unique levels (PyrSeg) with OpenCV's INTER_LINEAR
 // fixed-point arithmetic (resize.cpp HResizeLinear / VResizeLinear<uchar>):
@@ -150,14 +154,24 @@ __global__ __launch_bounds__(256) void k_pyramid(const uint8_t* __restrict__ fra
       const int R = 256 / ncg;
       if (tid < R * ncg) {
         const int cg = tid % ncg, r0 = tid / ncg;
-        int sx[4], sx1[4], a0[4], a1[4];
+        // the 4 columns' source bytes lie in an 8-byte window from sx[0]
+        // (scale < 2: sx1[3] - sx[0] <= 7, checked by the planner): two
+        // v_alignbyte of three LDS dwords per source row, then one v_perm
+        // (bytes sx, sx1 -> u16 pair) and one v_dot2_u32_u16 with the
+        // (a0, a1) pair per column: D = S[sx]*a0 + S[sx1]*a1
+        uint32_t hsel[4], hcoef[4];
+        int hbase, hsh;
+        {
+          const int s0 = (int)(xl[xo + 4 * cg].x & 0xFFFF);
+          hbase = s0 & ~3;
+          hsh = s0 & 3;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const uint2 e = xl[xo + 4 * cg + k];
-          sx[k] = e.x & 0xFFFF;
-          sx1[k] = e.x >> 16;
-          a0[k] = (int)(int16_t)(e.y & 0xFFFF);
-          a1[k] = (int)e.y >> 16;
+          for (int k = 0; k < 4; ++k) {
+            const uint2 e = xl[xo + 4 * cg + k];
+            const uint32_t o0 = (e.x & 0xFFFF) - (uint32_t)s0, o1 = (e.x >> 16) - (uint32_t)s0;
+            hsel[k] = o0 | 0x0C00u | (o1 << 16) | 0x0C000000u;
+            hcoef[k] = e.y;  // a0 | a1 << 16, both in [0, 2048]
+          }
         }
         const int gx0 = dax + 4 * cg;
         const bool in_x = gx0 >= X.z && gx0 + 4 <= X.w;
@@ -172,18 +186,27 @@ __global__ __launch_bounds__(256) void k_pyramid(const uint8_t* __restrict__ fra
           for (int u = 0; u < PYR_U; ++u) {
             const int r = min(rb + u * R, nrows - 1);
             const uint2 e = yl[yo + r];
-            const int b0 = (int)(int16_t)(e.y & 0xFFFF), b1 = (int)e.y >> 16;
-            const uint8_t* R0 = cur + (int)(e.x & 0xFFFF) * cpitch;
-            const uint8_t* R1 = cur + (int)(e.x >> 16) * cpitch;
-            uint32_t pk = 0;
+            // vertical: ((b*(D>>4))>>16) == mulhi_u24(b << 12, D & ~15)
+            // (b <= 2048, D <= 255*2048: both operands < 2^24, exact)
+            const uint64_t b0s = (uint64_t)((e.y & 0xFFFu) << 12), b1s = (uint64_t)(((e.y >> 16) & 0xFFFu) << 12);
+            const uint32_t* R0 = reinterpret_cast<const uint32_t*>(cur + __mul24((int)(e.x & 0xFFFF), cpitch) + hbase);
+            const uint32_t* R1 = reinterpret_cast<const uint32_t*>(cur + __mul24((int)(e.x >> 16), cpitch) + hbase);
+            const uint32_t lo0 = __builtin_amdgcn_alignbyte(R0[1], R0[0], hsh);
+            const uint32_t hi0 = __builtin_amdgcn_alignbyte(R0[2], R0[1], hsh);
+            const uint32_t lo1 = __builtin_amdgcn_alignbyte(R1[1], R1[0], hsh);
+            const uint32_t hi1 = __builtin_amdgcn_alignbyte(R1[2], R1[1], hsh);
+            uint32_t v[4];
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
-              const int d0 = R0[sx[k]] * a0[k] + R0[sx1[k]] * a1[k];
-              const int d1 = R1[sx[k]] * a0[k] + R1[sx1[k]] * a1[k];
-              const int v = (((b0 * (d0 >> 4)) >> 16) + ((b1 * (d1 >> 4)) >> 16) + 2) >> 2;
-              pk |= (uint32_t)(v & 0xFF) << (8 * k);
+              const uint32_t d0 = __builtin_amdgcn_udot2(as_us2(__builtin_amdgcn_perm(hi0, lo0, hsel[k])),
+                                                         as_us2(hcoef[k]), 0u, false);
+              const uint32_t d1 = __builtin_amdgcn_udot2(as_us2(__builtin_amdgcn_perm(hi1, lo1, hsel[k])),
+                                                         as_us2(hcoef[k]), 0u, false);
+              const uint32_t t0 = (uint32_t)((b0s * (uint64_t)(d0 & 0xFFFFF0u)) >> 32);
+              const uint32_t t1 = (uint32_t)((b1s * (uint64_t)(d1 & 0xFFFFF0u)) >> 32);
+              v[k] = (t0 + t1 + 2u) >> 2;
             }
-            packed[u] = pk;
+            packed[u] = __builtin_amdgcn_perm(v[1], v[0], 0x0C0C0400u) | __builtin_amdgcn_perm(v[3], v[2], 0x04000C0Cu);
           }
 #pragma unroll
           for (int u = 0; u < PYR_U; ++u) {
@@ -349,9 +372,6 @@ __device__ __forceinline__ void wave_sync_lds() {
 #define FS_L2CAP 128 /* per-wave even-test survivors: < 64 carried + <= 64 new */
 #define FS_CCAP 1024 /* per-strip corner list (overflow falls back to a map scan) */
 
-typedef unsigned short us2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ us2 as_us2(uint32_t x) { return __builtin_bit_cast(us2, x); }
-__device__ __forceinline__ uint32_t as_u32(us2 x) { return __builtin_bit_cast(uint32_t, x); }
 
 __global__ __launch_bounds__(256) void k_fast_strips(
     const uint8_t* __restrict__ frames, size_t fstride, size_t rstride,
