@@ -86,7 +86,10 @@ __device__ __forceinline__ uint32_t as_u32(us2 x) { return __builtin_bit_cast(ui
 // is written once and the intermediate levels are never re-read from HBM.
 // Thread = 4 consecutive columns (dword in LDS and HBM) of a row.
 // ---------------------------------------------------------------------------
-#define PYR_U 1 /* rows in flight per thread (more measured slower) */
+#ifndef PYR_U
+#define PYR_U 1
+#endif
+// PYR_U: rows in flight per thread (more measured slower)
 
 __global__ __launch_bounds__(256) void k_pyramid(const uint8_t* __restrict__ frames, size_t fstride,
                                                  size_t rstride, uint8_t* __restrict__ pyr,
@@ -450,14 +453,17 @@ __global__ __launch_bounds__(256) void k_fast_strips(
     if (corner && q < FS_CCAP) clist[q] = (uint16_t)e;
   };
   auto even_batch = [&](int e, bool act) {
-    const bool keep = act && fast_even_test(tile + (e >> 9) * tpitch + (e & 511), tpitch, t_lo);
+    const int ec = e & 511;
+    const bool keep = act && ec >= c0 && ec < c1 && fast_even_test(tile + (e >> 9) * tpitch + ec, tpitch, t_lo);
     const unsigned long long bal = __ballot(keep);
     if (keep) L2[n2 + __popcll(bal & lt)] = (uint16_t)e;
     n2 += __popcll(bal);
     if (n2 >= 64) {
       wave_sync_lds();
       n2 -= 64;
+#ifndef FAST_SKIP_C  // profiling only: drop the even-test survivors
       strength_batch(L2[n2 + lane], true);
+#endif
       wave_sync_lds();
     }
   };
@@ -495,21 +501,41 @@ __global__ __launch_bounds__(256) void k_fast_strips(
           if (h) chi = x; else clo = x;
         }
         reinterpret_cast<uint32_t*>(amap + r * tpitch)[g] = 0u;
+#ifdef FAST_PAD
+        // profiling only: FAST_PAD dependent VALU ops per group (issue-bound probe)
+        uint32_t pz = clo;
+#pragma unroll
+        for (int z = 0; z < FAST_PAD; ++z) asm volatile("v_xor_b32 %0, %0, %1" : "+v"(pz) : "v"(chi));
+        clo |= pz & 0u;
+        asm volatile("" : "+v"(clo));
+#endif
       }
+#ifdef FAST_NO_APPEND  // profiling only: stage A without the list appends
+      if (it < ntask) reinterpret_cast<uint32_t*>(amap + r * tpitch)[g] = (clo | chi) & 0x01000000u;
+#else
+      // append: the ballot is the compare's SGPR result, the lane's slot is
+      // mbcnt of it, only survivors store (stores of every lane to a dummy
+      // slot measured 13 % slower).  Columns outside [c0, c1) are appended
+      // too and rejected in stage B.
+      const uint32_t ebase = ((uint32_t)r << 9) | (uint32_t)(4 * g);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const int c = 4 * g + j;
         const uint32_t x = (j & 1) ? chi : clo;
-        const bool k = ((j & 2) ? (x >> 16) : (x & 0xFFFFu)) != 0 && c >= c0 && c < c1;
+        const bool k = ((j & 2) ? (x >> 16) : (x & 0xFFFFu)) != 0;
         const unsigned long long bal = __ballot(k);
-        if (k) L1[n1 + __popcll(bal & lt)] = (uint16_t)((r << 9) | c);
+        const int pos = n1 + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
+                                                            __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+        if (k) L1[pos] = (uint16_t)(ebase + (uint32_t)j);
         n1 += __popcll(bal);
       }
+#endif
       if (n1 >= 64) {  // wave-uniform
         wave_sync_lds();
         while (n1 >= 64) {
           n1 -= 64;
+#ifndef FAST_SKIP_B  // profiling only: drop the cardinal survivors
           even_batch(L1[n1 + lane], true);
+#endif
         }
         wave_sync_lds();
       }

@@ -19,6 +19,8 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(os.path.dirname(HERE), "liborbx.so")
+if os.environ.get("ORBX_VARIANT"):  # profiling only: tools/variant.sh builds liborbx_<name>.so
+    LIB_PATH = os.path.join(os.path.dirname(HERE), "liborbx_%s.so" % os.environ["ORBX_VARIANT"])
 
 if not os.path.exists(LIB_PATH):
     raise ImportError("liborbx.so not built (%s): run __graft_entry__.build() or "
