@@ -15,7 +15,9 @@ __global__ void k_match_candidates(const MProblem*, const MNodePair*, int, int, 
                                    int2*);
 template <int NJ>
 __global__ void k_match_cand_lds(const MProblem*, const MNodePair*, uint2*, int4*, int2*);
-__global__ void k_match_cand_rows(const MProblem*, const MNodePair*, uint2*, int4*, int2*);
+__global__ void k_match_cand_rows(const MProblem*, const MNodePair*, const uint4*, const uint32_t*,
+                                  uint2*, int4*, int2*);
+__global__ void k_match_gather2(const MProblem*, const MNodePair*, uint4*, uint32_t*);
 __global__ void k_match_resolve(const MProblem*, const MNodePair*, int, int, const uint2*,
                                 const int4*, int2*);
 __global__ void k_match_resolve_spec(const MProblem*, const MNodePair*, int, const uint2*,
@@ -70,18 +72,19 @@ int check_frame(const orbx_bow_frame* k) {
 }
 
 void launch_match(const MProblem* d_probs, int nprob, const MNodePair* d_nps, int nnp, int nrows,
-                  int sequential, int max_n1, int max_n2, int max_bitmap_n2, uint2* d_cand,
-                  int4* d_rowinfo, int2* d_ev, int* d_last, const int* d_last_off, hipStream_t s,
-                  StageTimer* timer) {
+                  int sequential, int max_n1, int max_n2, int max_bitmap_n2, uint4* d_gdesc2,
+                  uint32_t* d_gval2, uint2* d_cand, int4* d_rowinfo, int2* d_ev, int* d_last,
+                  const int* d_last_off, hipStream_t s, StageTimer* timer) {
   if (timer) timer->begin(ORBX_STAGE_MCAND, s);
   if (nrows > 0 && nnp > 0) {
-    if (max_n2 <= 4096 && nnp <= 65535) {
-      // lane = row; list2 staged in LDS (broadcast reads); running top-T in registers
-      const size_t lds = (size_t)std::max(max_n2, 1) * 32 + ((size_t)(max_n2 + 31) / 32) * 4;
-      hipFuncSetAttribute((const void*)k_match_cand_rows,
-                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-      hipLaunchKernelGGL(k_match_cand_rows, dim3((max_n1 + 255) / 256, nnp), dim3(256), lds, s,
-                         d_probs, d_nps, d_cand, d_rowinfo, d_ev);
+    if (max_n2 <= ORBM_MAX_N2 && nnp <= 65535 && d_gdesc2) {
+      // list2 descriptors gathered into node order, then two rows per lane,
+      // the 4 waves splitting the positions; descriptors stream through LDS
+      if (max_n2 > 0)
+        hipLaunchKernelGGL(k_match_gather2, dim3((max_n2 + 127) / 128, nnp), dim3(256), 0, s, d_probs,
+                           d_nps, d_gdesc2, d_gval2);
+      hipLaunchKernelGGL(k_match_cand_rows, dim3((max_n1 + 127) / 128, nnp), dim3(256), 0, s,
+                         d_probs, d_nps, d_gdesc2, d_gval2, d_cand, d_rowinfo, d_ev);
     } else if (max_n2 <= 64 * 32 && nnp <= 65535) {
       // list2 staged in LDS, distances in registers (32 per lane)
       const size_t lds = (size_t)std::max(max_n2, 1) * 32;
@@ -141,7 +144,7 @@ extern "C" int orbm_search_by_bow(const orbx_bow_frame* kf1, const orbx_bow_fram
   // merge-join of the two FeatureVectors (ORBmatcher.cc:305-350): common
   // NodeIds in ascending order
   std::vector<MNodePair> nps;
-  int rows = 0, max_n1 = 0, max_n2 = 0;
+  int rows = 0, max_n1 = 0, max_n2 = 0, g2 = 0;
   {
     int f1 = 0, f2 = 0;
     while (f1 < kf1->nnodes && f2 < kf2->nnodes) {
@@ -155,8 +158,9 @@ extern "C" int orbm_search_by_bow(const orbx_bow_frame* kf1, const orbx_bow_fram
         np.n2 = (int)(kf2->node_off[f2 + 1] - kf2->node_off[f2]);
         if (np.n2 > 0xFFFF) return ORBX_ERR_UNSUPPORTED; /* 16-bit list positions */
         np.row_base = rows;
-        np.pad = 0;
+        np.g2 = g2;
         rows += np.n1;
+        g2 += np.n2;
         max_n1 = std::max(max_n1, np.n1);
         max_n2 = std::max(max_n2, np.n2);
         nps.push_back(np);
@@ -222,15 +226,18 @@ extern "C" int orbm_search_by_bow(const orbx_bow_frame* kf1, const orbx_bow_fram
     int4* d_rowinfo = B.alloc<int4>(rows);
     int2* d_ev = B.alloc<int2>(rows);
     int* d_last = B.alloc<int>(kf1->n);
+    uint4* d_gdesc2 = B.alloc<uint4>((size_t)g2 * 2);
+    uint32_t* d_gval2 = kf2->valid ? B.alloc<uint32_t>((size_t)g2) : nullptr;
     const int zero = 0;
     int* d_last_off = B.upload(&zero, 1, s);
     if (!P.desc1 || !P.desc2 || !P.ang1 || !P.ang2 || !P.feat1 || !P.feat2 || !P.match12 ||
         !P.nmatches || !d_prob || !d_nps || !d_cand || !d_rowinfo || !d_ev || !d_last ||
-        !d_last_off || (kf1->valid && !P.valid1) || (kf2->valid && !P.valid2)) {
+        !d_last_off || !d_gdesc2 || (kf1->valid && !P.valid1) ||
+        (kf2->valid && (!P.valid2 || !d_gval2))) {
       result = ORBX_ERR_HIP;
     } else {
       launch_match(d_prob, 1, d_nps, (int)nps.size(), rows, sequential, max_n1, max_n2, kf2->n,
-                   d_cand, d_rowinfo, d_ev, d_last, d_last_off, s, nullptr);
+                   d_gdesc2, d_gval2, d_cand, d_rowinfo, d_ev, d_last, d_last_off, s, nullptr);
       if (hipGetLastError() != hipSuccess ||
           hipMemcpyAsync(match12, P.match12, sizeof(int32_t) * (size_t)kf1->n,
                          hipMemcpyDeviceToHost, s) != hipSuccess ||
@@ -323,7 +330,7 @@ __global__ void k_match_setup(MProblem* probs, MNodePair* nps, int npairs,
   NP.off2 = 0;
   NP.n2 = 0;
   NP.row_base = p * topn;
-  NP.pad = 0;
+  NP.g2 = p * topn;
   nps[p] = NP;
   last_off[p] = p * kcap;
 }
@@ -335,6 +342,7 @@ struct orbm_plan {
   MNodePair* d_nps = nullptr;
   uint32_t* d_sel = nullptr;
   uint2* d_cand = nullptr;
+  uint4* d_gdesc2 = nullptr;
   int4* d_rowinfo = nullptr;
   int2* d_ev = nullptr;
   int *d_last = nullptr, *d_last_off = nullptr;
@@ -344,8 +352,8 @@ struct orbm_plan {
 static void mplan_free(orbm_plan* m) {
   if (!m) return;
   hipSetDevice(m->device);
-  void* b[] = {m->d_probs, m->d_nps, m->d_sel, m->d_cand, m->d_rowinfo, m->d_ev, m->d_last,
-               m->d_last_off};
+  void* b[] = {m->d_probs, m->d_nps, m->d_sel, m->d_cand, m->d_gdesc2, m->d_rowinfo, m->d_ev,
+               m->d_last, m->d_last_off};
   for (void* p : b)
     if (p) hipFree(p);
   m->timer.release();
@@ -370,6 +378,7 @@ extern "C" int orbm_plan_create(int max_pairs, int kcap, int topn, int device, o
       hipMalloc((void**)&m->d_nps, P * sizeof(MNodePair)) != hipSuccess ||
       hipMalloc((void**)&m->d_sel, P * 2 * topn * sizeof(uint32_t)) != hipSuccess ||
       hipMalloc((void**)&m->d_cand, rows * ORBM_T * sizeof(uint2)) != hipSuccess ||
+      hipMalloc((void**)&m->d_gdesc2, rows * 2 * sizeof(uint4)) != hipSuccess ||
       hipMalloc((void**)&m->d_rowinfo, rows * sizeof(int4)) != hipSuccess ||
       hipMalloc((void**)&m->d_ev, rows * sizeof(int2)) != hipSuccess ||
       hipMalloc((void**)&m->d_last, P * kcap * sizeof(int)) != hipSuccess ||
@@ -417,6 +426,7 @@ extern "C" int orbm_plan_match_frames(orbm_plan* m, int npairs, const orbx_keypo
                      kps_a, count_a, kps_b, count_b, m->kcap, m->topn, m->d_sel);
   m->timer.end(ORBX_STAGE_MSELECT, s);
   launch_match(m->d_probs, npairs, m->d_nps, npairs, npairs * m->topn, 0, m->topn, m->topn,
-               m->kcap, m->d_cand, m->d_rowinfo, m->d_ev, m->d_last, m->d_last_off, s, &m->timer);
+               m->kcap, m->d_gdesc2, nullptr, m->d_cand, m->d_rowinfo, m->d_ev, m->d_last,
+               m->d_last_off, s, &m->timer);
   return hipGetLastError() == hipSuccess ? ORBX_OK : ORBX_ERR_HIP;
 }

@@ -54,6 +54,18 @@ __device__ __forceinline__ uint32_t ham256(uint4 a0, uint4 a1, uint4 b0, uint4 b
   return bcnt_acc(a1.w ^ b1.w, d);
 }
 
+typedef uint32_t v4u_ __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint32_t ham256v(uint4 a0, uint4 a1, v4u_ b0, v4u_ b1) {
+  uint32_t d = bcnt_acc(a0.x ^ b0.x, 0u);
+  d = bcnt_acc(a0.y ^ b0.y, d);
+  d = bcnt_acc(a0.z ^ b0.z, d);
+  d = bcnt_acc(a0.w ^ b0.w, d);
+  d = bcnt_acc(a1.x ^ b1.x, d);
+  d = bcnt_acc(a1.y ^ b1.y, d);
+  d = bcnt_acc(a1.z ^ b1.z, d);
+  return bcnt_acc(a1.w ^ b1.w, d);
+}
+
 __device__ __forceinline__ int find_node_pair(const MNodePair* nps, int nnp, int r) {
   int lo = 0, hi = nnp;  // last np with row_base <= r
   while (lo < hi) {
@@ -266,117 +278,241 @@ template __global__ void k_match_cand_lds<32>(const MProblem*, const MNodePair*,
 
 
 // ---------------------------------------------------------------------------
-// k_match_cand_rows: lane = row (KF1 feature), 256 rows per workgroup.
-// The node's list2 descriptors are staged once in LDS and read at a
-// wave-uniform address (broadcast); each lane keeps its 8 smallest
-// (distance<<16 | list position) keys sorted in registers, so the list is
-// exactly the first 8 of the reference's scan order.  Positions are visited
-// in list order; a wave skips the insertion network when no lane improves.
+// k_match_gather2: list2 descriptors of every node pair into node order,
+// gdesc2[NP.g2 + j] = desc2[feat2[off2 + j]] (and, with a validity array,
+// gval2[NP.g2 + j] = 0 if valid else ~0), so k_match_cand_rows reads each
+// group of positions as contiguous scalar loads with no index indirection.
 // ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_match_gather2(const MProblem* __restrict__ probs,
+                                                       const MNodePair* __restrict__ nps,
+                                                       uint4* __restrict__ gdesc2,
+                                                       uint32_t* __restrict__ gval2) {
+  const MNodePair NP = nps[blockIdx.y];
+  const int i = blockIdx.x * 256 + threadIdx.x;  // (position, half)
+  const int j = i >> 1;
+  if (j >= NP.n2) return;
+  const MProblem& P = probs[NP.prob];
+  const uint32_t idx2 = P.feat2[NP.off2 + j];
+  gdesc2[(size_t)(NP.g2 + j) * 2 + (i & 1)] = reinterpret_cast<const uint4*>(P.desc2 + (size_t)idx2 * 32)[i & 1];
+  if (gval2 && (i & 1) == 0) gval2[NP.g2 + j] = (P.valid2 && !P.valid2[idx2]) ? 0xFFFFFFFFu : 0u;
+}
+
+// ---------------------------------------------------------------------------
+// k_match_cand_rows: 128 rows (KF1 features) per workgroup, two per lane
+// (rows a0+lane and a0+64+lane); the 4 waves split the list2 positions
+// (wave w takes quarter w of every chunk), so a 2000-row node pair runs 64
+// waves and every descriptor read from LDS feeds 128 distances.  The
+// gathered list2 descriptors (k_match_gather2) stream through two 16-KB LDS
+// chunks: chunk c+1 is loaded into registers while chunk c is matched, then
+// stored to the other buffer (one barrier per chunk).  Reads are
+// wave-uniform (broadcast).  Each lane keeps, per row, its 8 smallest
+// (distance<<16 | list position) keys sorted in registers; keys carry the
+// position, so the 4 waves' lists merge (LDS) into exactly the first 8 of
+// the reference's scan order.  A wave skips the insertion network when no
+// lane improves.
+// ---------------------------------------------------------------------------
+#define MC_CHUNK 512  /* positions per LDS chunk (16 KB of descriptors) */
+
+// sorted insertion of k into L (ascending): new L[t] = median(L[t-1], k, L[t])
+// -- one v_min + 7 independent v_med3_u32 instead of a 16-deep min/max chain
+__device__ __forceinline__ uint32_t med3u(uint32_t a, uint32_t b, uint32_t c) {
+  uint32_t r;
+  asm("v_med3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+__device__ __forceinline__ void topk_insert(uint32_t (&L)[ORBM_T], uint32_t k) {
+  uint32_t N[ORBM_T];
+  N[0] = min(L[0], k);
+#pragma unroll
+  for (int t = 1; t < ORBM_T; ++t) N[t] = med3u(L[t - 1], k, L[t]);
+#pragma unroll
+  for (int t = 0; t < ORBM_T; ++t) L[t] = N[t];
+}
+
 __global__ __launch_bounds__(256) void k_match_cand_rows(
     const MProblem* __restrict__ probs, const MNodePair* __restrict__ nps,
+    const uint4* __restrict__ gdesc2, const uint32_t* __restrict__ gval2,
     uint2* __restrict__ cand, int4* __restrict__ rowinfo, int2* __restrict__ ev) {
-  extern __shared__ uint4 sdesc[];  // 2 per list2 position, then validity bits
-  const int tid = threadIdx.x;
+  __shared__ uint4 sdesc[2][2 * MC_CHUNK];        // 2 x 16 KB; the merge area aliases it
+  __shared__ uint32_t sval[2][MC_CHUNK];          // per-position invalid masks (validity arrays only)
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const MNodePair NP = nps[blockIdx.y];
-  const int a0 = blockIdx.x * 256;
-  if (a0 >= NP.n1) return;
+  const int a0 = blockIdx.x * 128;
+  if (a0 >= NP.n1) return;  // workgroup-uniform
   const MProblem P = probs[NP.prob];
   const uint32_t* f2 = P.feat2 + NP.off2;
+  const uint4* g2 = gdesc2 + (size_t)NP.g2 * 2;
+  const uint32_t* gv = gval2 ? gval2 + NP.g2 : nullptr;
+  const bool hasv = P.valid2 != nullptr;
   const int n2 = NP.n2;
-  uint32_t* svalid = reinterpret_cast<uint32_t*>(sdesc + 2 * n2);
-  for (int i = tid; i < ((n2 + 31) >> 5); i += 256) svalid[i] = 0u;
-  __syncthreads();
-  for (int i = tid; i < 2 * n2; i += 256) {
-    const uint32_t idx2 = f2[i >> 1];
-    sdesc[i] = reinterpret_cast<const uint4*>(P.desc2 + (size_t)idx2 * 32)[i & 1];
-    if ((i & 1) == 0 && !(P.valid2 && !P.valid2[idx2]))
-      atomicOr(&svalid[(i >> 1) >> 5], 1u << ((i >> 1) & 31));
-  }
-  __syncthreads();
-  const int a = a0 + tid;
-  const bool act = a < NP.n1;
-  const int r = NP.row_base + a;
-  int idx1 = 0;
-  bool v1 = false;
-  uint4 q0 = make_uint4(0, 0, 0, 0), q1 = q0;
-  if (act) {
-    idx1 = (int)P.feat1[NP.off1 + a];
-    v1 = !(P.valid1 && !P.valid1[idx1]);
-    q0 = reinterpret_cast<const uint4*>(P.desc1 + (size_t)idx1 * 32)[0];
-    q1 = reinterpret_cast<const uint4*>(P.desc1 + (size_t)idx1 * 32)[1];
+  // the lane's two rows
+  int idx1[2] = {0, 0};
+  bool act[2], v1[2] = {false, false};
+  uint4 q[2][2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int a = a0 + 64 * h + lane;
+    act[h] = a < NP.n1;
+    q[h][0] = q[h][1] = make_uint4(0, 0, 0, 0);
+    if (act[h]) {
+      idx1[h] = (int)P.feat1[NP.off1 + a];
+      v1[h] = !(P.valid1 && !P.valid1[idx1[h]]);
+      q[h][0] = reinterpret_cast<const uint4*>(P.desc1 + (size_t)idx1[h] * 32)[0];
+      q[h][1] = reinterpret_cast<const uint4*>(P.desc1 + (size_t)idx1[h] * 32)[1];
+    }
   }
   // lists start full of sentinels at the distance cap: only d < dcap enters
   const uint32_t sent = (uint32_t)P.dcap << 16;
-  uint32_t L[ORBM_T];
+  uint32_t LA[ORBM_T], LB[ORBM_T];
 #pragma unroll
-  for (int t = 0; t < ORBM_T; ++t) L[t] = sent;
-  auto dist = [&](int j) {
-    const uint4 b0 = sdesc[2 * j], b1 = sdesc[2 * j + 1];
-    return __popc(q0.x ^ b0.x) + __popc(q0.y ^ b0.y) + __popc(q0.z ^ b0.z) +
-           __popc(q0.w ^ b0.w) + __popc(q1.x ^ b1.x) + __popc(q1.y ^ b1.y) +
-           __popc(q1.z ^ b1.z) + __popc(q1.w ^ b1.w);
+  for (int t = 0; t < ORBM_T; ++t) LA[t] = LB[t] = sent;
+  // chunk staging: thread loads uint4 entries tid + 256*u of a chunk
+  uint4 pre[4];
+  uint32_t prev[2];
+  auto load_chunk = [&](int c0) {
+    const int cn = min(MC_CHUNK, n2 - c0);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int i = tid + 256 * u;
+      pre[u] = i < 2 * cn ? g2[(size_t)c0 * 2 + i] : make_uint4(0, 0, 0, 0);
+    }
+    if (hasv) {
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int i = tid + 256 * u;
+        prev[u] = i < cn ? gv[c0 + i] : 0xFFFFFFFFu;
+      }
+    }
   };
-  auto insert = [&](uint32_t k) {
+  auto store_chunk = [&](int b) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) sdesc[b][tid + 256 * u] = pre[u];
+    if (hasv) {
+#pragma unroll
+      for (int u = 0; u < 2; ++u) sval[b][tid + 256 * u] = prev[u];
+    }
+  };
+  load_chunk(0);
+  store_chunk(0);
+  __syncthreads();
+  int buf = 0;
+  for (int c0 = 0; c0 < n2; c0 += MC_CHUNK, buf ^= 1) {  // workgroup-uniform
+    const int cn = min(MC_CHUNK, n2 - c0);
+    const bool more = c0 + MC_CHUNK < n2;
+    if (more) load_chunk(c0 + MC_CHUNK);  // in flight while this chunk is matched
+    const int qn = (((cn + 3) >> 2) + 7) & ~7;  // this wave's quarter (multiple of 8)
+    const int jb = min(wave * qn, cn), je = min(jb + qn, cn);
+    const int je8 = jb + ((je - jb) & ~3);
+    const uint4* sd = sdesc[buf];
+    for (int j0 = jb; j0 < je8; j0 += 4) {  // wave-uniform
+      // 8 independent Hamming chains (4 positions x 2 rows), advanced one
+      // descriptor word at a time: xors of all chains, then their v_bcnt
+      // accumulates -- no back-to-back dependent VALU instructions
+      uint4 lo[4], hi[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) lo[u] = sd[2 * (j0 + u)];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) hi[u] = sd[2 * (j0 + u) + 1];
+      uint32_t acc[2][4];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        uint32_t t[2][4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const uint4& b = k < 4 ? lo[u] : hi[u];
+          const uint32_t bw = (k & 3) == 0 ? b.x : (k & 3) == 1 ? b.y : (k & 3) == 2 ? b.z : b.w;
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const uint4& a = k < 4 ? q[h][0] : q[h][1];
+            const uint32_t aw = (k & 3) == 0 ? a.x : (k & 3) == 1 ? a.y : (k & 3) == 2 ? a.z : a.w;
+            t[h][u] = aw ^ bw;
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+          for (int h = 0; h < 2; ++h) acc[h][u] = bcnt_acc(t[h][u], k ? acc[h][u] : 0u);
+      }
+      uint32_t kA[4], kB[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const uint32_t inval = hasv ? __builtin_amdgcn_readfirstlane(sval[buf][j0 + u]) : 0u;
+        const uint32_t pos = (uint32_t)(c0 + j0 + u);
+        kA[u] = ((acc[0][u] << 16) | pos) | inval;
+        kB[u] = ((acc[1][u] << 16) | pos) | inval;
+      }
+      const uint32_t mA = min(min(kA[0], kA[1]), min(kA[2], kA[3]));
+      const uint32_t mB = min(min(kB[0], kB[1]), min(kB[2], kB[3]));
+      if (__ballot(mA < LA[ORBM_T - 1])) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          if (__ballot(kA[u] < LA[ORBM_T - 1])) topk_insert(LA, kA[u]);
+      }
+      if (__ballot(mB < LB[ORBM_T - 1])) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          if (__ballot(kB[u] < LB[ORBM_T - 1])) topk_insert(LB, kB[u]);
+      }
+    }
+    for (int j = je8; j < je; ++j) {
+      const uint4 b0 = sd[2 * j], b1 = sd[2 * j + 1];
+      const uint32_t inval = hasv ? __builtin_amdgcn_readfirstlane(sval[buf][j]) : 0u;
+      const uint32_t pos = (uint32_t)(c0 + j);
+      const uint32_t ka = ((ham256(q[0][0], q[0][1], b0, b1) << 16) | pos) | inval;
+      const uint32_t kb = ((ham256(q[1][0], q[1][1], b0, b1) << 16) | pos) | inval;
+      if (__ballot(ka < LA[ORBM_T - 1])) topk_insert(LA, ka);
+      if (__ballot(kb < LB[ORBM_T - 1])) topk_insert(LB, kb);
+    }
+    if (more) store_chunk(buf ^ 1);  // that buffer was last read before the previous barrier
+    __syncthreads();
+  }
+  // merge the 4 waves' lists of each row (keys are unique: position inside)
+  uint32_t* ml = reinterpret_cast<uint32_t*>(&sdesc[0][0]);  // [3][2][ORBM_T][64]
+  if (wave > 0) {
 #pragma unroll
     for (int t = 0; t < ORBM_T; ++t) {
-      const uint32_t lo = min(L[t], k);
-      k = max(L[t], k);
-      L[t] = lo;
-    }
-  };
-  const int n8 = n2 & ~7;
-  for (int j0 = 0; j0 < n8; j0 += 8) {
-    // validity of these 8 positions: one wave-uniform word; an invalid
-    // position's key is forced to ~0 with a scalar OR mask (no branches, so
-    // all 16 LDS reads of the group stay in flight together)
-    const uint32_t vw = __builtin_amdgcn_readfirstlane(svalid[j0 >> 5]) >> (j0 & 31);
-    uint4 bd[16];
-#pragma unroll
-    for (int q = 0; q < 16; ++q) bd[q] = sdesc[2 * j0 + q];  // all 16 reads in flight
-    uint32_t kk[8];
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      const uint4 b0 = bd[2 * q], b1 = bd[2 * q + 1];
-      const uint32_t d = ham256(q0, q1, b0, b1);
-      const uint32_t inval = ((vw >> q) & 1u) - 1u;  // 0 or 0xFFFFFFFF (uniform)
-      kk[q] = ((d << 16) | (uint32_t)(j0 + q)) | inval;
-    }
-    uint32_t kmin = kk[0];
-#pragma unroll
-    for (int q = 1; q < 8; ++q) kmin = min(kmin, kk[q]);
-    if (__ballot(kmin < L[ORBM_T - 1])) {
-#pragma unroll
-      for (int q = 0; q < 8; ++q)
-        if (__ballot(kk[q] < L[ORBM_T - 1])) insert(kk[q]);
+      ml[(((wave - 1) * 2 + 0) * ORBM_T + t) * 64 + lane] = LA[t];
+      ml[(((wave - 1) * 2 + 1) * ORBM_T + t) * 64 + lane] = LB[t];
     }
   }
-  for (int j = n8; j < n2; ++j) {
-    const bool ok = (svalid[j >> 5] >> (j & 31)) & 1u;
-    const uint32_t k = ok ? (((uint32_t)dist(j) << 16) | (uint32_t)j) : 0xFFFFFFFFu;
-    if (__ballot(k < L[ORBM_T - 1])) insert(k);
-  }
-  // a full list (no sentinel left) may have more candidates below the cap
-  const bool full = L[ORBM_T - 1] < sent;
+  __syncthreads();
+  if (wave > 0) return;
 #pragma unroll
-  for (int t = 0; t < ORBM_T; ++t)
-    if (L[t] >= sent) L[t] = 0xFFFFFFFFu;
-  if (!act) return;
-  ev[r] = make_int2(-1, 0);
-  if (!v1) {
-    rowinfo[r] = make_int4(0, 0, 0, idx1);
-    return;
-  }
-  const int minD = L[0] != 0xFFFFFFFFu ? (int)(L[0] >> 16) : (1 << 20);
-  // .y > ORBM_T: the list may be incomplete (resolve rescans when exhausted)
-  rowinfo[r] = make_int4(1, full ? ORBM_T + 1 : 0, minD, idx1);
-  if (minD >= ORBM_TH_LOW) return;
-  uint4* out = reinterpret_cast<uint4*>(cand + (size_t)r * ORBM_T);
+  for (int w = 0; w < 3; ++w)
 #pragma unroll
-  for (int t = 0; t < ORBM_T / 2; ++t) {
-    const uint32_t ka = L[2 * t], kb = L[2 * t + 1];
-    out[t] = make_uint4(ka, ka != 0xFFFFFFFFu ? f2[ka & 0xFFFFu] : 0u, kb,
-                        kb != 0xFFFFFFFFu ? f2[kb & 0xFFFFu] : 0u);
+    for (int t = 0; t < ORBM_T; ++t) {
+      const uint32_t ka = ml[((w * 2 + 0) * ORBM_T + t) * 64 + lane];
+      const uint32_t kb = ml[((w * 2 + 1) * ORBM_T + t) * 64 + lane];
+      if (__ballot(ka < LA[ORBM_T - 1])) topk_insert(LA, ka);
+      if (__ballot(kb < LB[ORBM_T - 1])) topk_insert(LB, kb);
+    }
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    uint32_t (&L)[ORBM_T] = h ? LB : LA;
+    // a full list (no sentinel left) may have more candidates below the cap
+    const bool full = L[ORBM_T - 1] < sent;
+#pragma unroll
+    for (int t = 0; t < ORBM_T; ++t)
+      if (L[t] >= sent) L[t] = 0xFFFFFFFFu;
+    if (!act[h]) continue;
+    const int r = NP.row_base + a0 + 64 * h + lane;
+    ev[r] = make_int2(-1, 0);
+    if (!v1[h]) {
+      rowinfo[r] = make_int4(0, 0, 0, idx1[h]);
+      continue;
+    }
+    const int minD = L[0] != 0xFFFFFFFFu ? (int)(L[0] >> 16) : (1 << 20);
+    // .y > ORBM_T: the list may be incomplete (resolve rescans when exhausted)
+    rowinfo[r] = make_int4(1, full ? ORBM_T + 1 : 0, minD, idx1[h]);
+    if (minD >= ORBM_TH_LOW) continue;
+    uint4* out = reinterpret_cast<uint4*>(cand + (size_t)r * ORBM_T);
+#pragma unroll
+    for (int t = 0; t < ORBM_T / 2; ++t) {
+      const uint32_t ka = L[2 * t], kb = L[2 * t + 1];
+      out[t] = make_uint4(ka, ka != 0xFFFFFFFFu ? f2[ka & 0xFFFFu] : 0u, kb,
+                          kb != 0xFFFFFFFFu ? f2[kb & 0xFFFFu] : 0u);
+    }
   }
 }
 
@@ -526,7 +662,6 @@ __global__ __launch_bounds__(64) void k_match_resolve_spec(
   for (int w = lane; w < P.n2; w += 64) claim[w] = 64;
   __builtin_amdgcn_wave_barrier();
   const float factor = 1.0f / ORBM_HISTO;
-  const uint64_t below = (1ull << lane) - 1ull;
   // the next chunk's row info and candidate lists are loaded while the
   // current chunk resolves (rows that are not feasible never read theirs)
   int4 inf_n = make_int4(0, 0, 0, 0);

@@ -55,7 +55,7 @@ struct MNodePair {
   int off1, n1;  /* list1 = feat1[off1 .. off1+n1) */
   int off2, n2;  /* list2 = feat2[off2 .. off2+n2) */
   int row_base;
-  int pad;
+  int g2;        /* list2 position j's descriptor is gdesc2[g2 + j] (k_match_gather2) */
 };
 
 #endif
