@@ -153,6 +153,11 @@ int orbx_plan_stage_times(orbx_plan* plan, double* ms, int* launches, int nstage
 int orbx_synth_frames(uint8_t* d_frames, int width, int height, size_t frame_stride, int nframes,
                       int first_idx, int kind, void* stream);
 
+/* Self-test of the rotated-BRIEF sin/cos (device memory): sc[2i], sc[2i+1] =
+ * the (sin, cos) k_orient_brief uses for angle x[i] -- glibc sincosf
+ * (ORBextractor.cc:58-59) wherever it moves a BRIEF sample (orbx_sincos.h). */
+int orbx_selftest_sincos(const float* d_x, int n, float* d_sc, void* stream);
+
 /* ---------------------------------------------------------------------------
  * ORBmatcher drop-in.
  * ------------------------------------------------------------------------- */

@@ -27,6 +27,7 @@ __global__ void k_orient_brief(const uint8_t*, size_t, size_t, const uint8_t*, s
                                const BriefArgs, const uint32_t*, size_t, const int*,
                                orbx_keypoint*, uint8_t*, int*, int);
 __global__ void k_synth(uint8_t*, int, int, size_t, int, int);
+__global__ void k_selftest_sincos(const float*, int, float*);
 }  // namespace orbx
 
 using namespace orbx;
@@ -335,6 +336,13 @@ extern "C" int orbx_synth_frames(uint8_t* d_frames, int W, int H, size_t fstride
   dim3 grid((unsigned)((npx + 4095) / 4096), nframes);
   hipLaunchKernelGGL(k_synth, grid, dim3(256), 0, (hipStream_t)stream, d_frames, W, H, fstride,
                      first_idx, kind);
+  return hipGetLastError() == hipSuccess ? ORBX_OK : ORBX_ERR_HIP;
+}
+
+extern "C" int orbx_selftest_sincos(const float* d_x, int n, float* d_sc, void* stream) {
+  if (n < 0 || (n > 0 && (!d_x || !d_sc))) return ORBX_ERR_ARG;
+  if (n == 0) return ORBX_OK;
+  hipLaunchKernelGGL(k_selftest_sincos, dim3(n), dim3(64), 0, (hipStream_t)stream, d_x, n, d_sc);
   return hipGetLastError() == hipSuccess ? ORBX_OK : ORBX_ERR_HIP;
 }
 

@@ -893,17 +893,19 @@ __device__ __forceinline__ float fast_atan2(float y, float x) {
   return a;
 }
 
-__device__ __forceinline__ void brief_sincos(float x, float* s, float* c) {
+// x is wave-uniform.  The exception keys live in two VGPRs per lane
+// (entries lane and lane + 64, loaded once per wave), so the lookup is two
+// compares and a ballot -- no chain of dependent scalar loads; the rare hit
+// reads its (sin, cos) pair.
+static_assert(ORBX_SINCOS_NEXC <= 128, "exception table fits two entries per lane");
+__device__ __forceinline__ void brief_sincos(float x, uint32_t exk0, uint32_t exk1, float* s, float* c) {
   orbx_sincos_core(x, s, c);
   const uint32_t b = orbx_f2u(x);
-  int lo = 0, hi = ORBX_SINCOS_NEXC;
-  while (lo < hi) {
-    const int mid = (lo + hi) >> 1;
-    if (ORBX_SINCOS_EXC[mid][0] < b) lo = mid + 1; else hi = mid;
-  }
-  if (lo < ORBX_SINCOS_NEXC && ORBX_SINCOS_EXC[lo][0] == b) {
-    *s = orbx_u2f(ORBX_SINCOS_EXC[lo][1]);
-    *c = orbx_u2f(ORBX_SINCOS_EXC[lo][2]);
+  const uint64_t m0 = __ballot(exk0 == b), m1 = __ballot(exk1 == b);
+  if (m0 | m1) {
+    const int i = m0 ? __ffsll((unsigned long long)m0) - 1 : 64 + __ffsll((unsigned long long)m1) - 1;
+    *s = orbx_u2f(ORBX_SINCOS_EXC[i][1]);
+    *c = orbx_u2f(ORBX_SINCOS_EXC[i][2]);
   }
 }
 
@@ -1004,6 +1006,9 @@ __global__ __launch_bounds__(256) void k_orient_brief(
   uint32_t(*P)[KP_COLS / 4] = patch[wave];
   // the 256 test pairs {x0, y0, x1, y1} in LDS (ds_read, not a vector load
   // that would wait behind the patch prefetch)
+  // sincos exception keys, entries lane and lane + 64 (brief_sincos)
+  const uint32_t exk0 = ORBX_SINCOS_EXC[lane < ORBX_SINCOS_NEXC ? lane : 0][0];
+  const uint32_t exk1 = lane + 64 < ORBX_SINCOS_NEXC ? ORBX_SINCOS_EXC[lane + 64][0] : 0xFFFFFFFFu;
   __shared__ uint32_t spat[256];
   spat[threadIdx.x] = *reinterpret_cast<const uint32_t*>(ORBX_BRIEF_PATTERN[threadIdx.x]);
   __syncthreads();
@@ -1104,7 +1109,7 @@ __global__ __launch_bounds__(256) void k_orient_brief(
   const float angle = fast_atan2((float)m01, (float)m10);
   const float factorPI = (float)(3.1415926535897932384626433832795 / 180.f);
   float sn, cs;
-  brief_sincos(angle * factorPI, &sn, &cs);
+  brief_sincos(angle * factorPI, exk0, exk1, &sn, &cs);
   // BRIEF (:57-73) on GaussianBlur(7x7, sigma 2) evaluated at each sample:
   // out = (sum_j k_j * (sum_i k_i p) + 32768) >> 16, rows via v_dot4_u32_u8
   const uint32_t K0 = 18u | (34u << 8) | (48u << 16) | (56u << 24), K1 = 48u | (34u << 8) | (18u << 16);
@@ -1207,6 +1212,24 @@ __global__ __launch_bounds__(256) void k_synth(uint8_t* __restrict__ frames, int
       v = min(max(v, 0), 255);
     }
     out[(size_t)y * W + x] = (uint8_t)v;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// k_selftest_sincos: brief_sincos exactly as k_orient_brief runs it (one
+// wave per input, exception keys in two VGPRs per lane); orbx_selftest_sincos.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(64) void k_selftest_sincos(const float* __restrict__ x, int n,
+                                                        float* __restrict__ sc) {
+  const int lane = threadIdx.x, i = blockIdx.x;
+  if (i >= n) return;
+  const uint32_t exk0 = ORBX_SINCOS_EXC[lane < ORBX_SINCOS_NEXC ? lane : 0][0];
+  const uint32_t exk1 = lane + 64 < ORBX_SINCOS_NEXC ? ORBX_SINCOS_EXC[lane + 64][0] : 0xFFFFFFFFu;
+  float s, c;  // x[i] is wave-uniform, as the BRIEF angle is
+  brief_sincos(__uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(x[i]))), exk0, exk1, &s, &c);
+  if (lane == 0) {
+    sc[2 * i] = s;
+    sc[2 * i + 1] = c;
   }
 }
 

@@ -55,7 +55,7 @@ EXPORTED = [
     "orbs_plan_check", "orbs_plan_set_timing", "orbs_plan_stage_times",
     "orbv_vocab_load_text", "orbv_vocab_create", "orbv_vocab_destroy", "orbv_vocab_info",
     "orbv_transform", "orbv_transform_batch", "orbv_check", "orbm_search_by_projection",
-    "orbm_compute_distinctive_descriptors", "orbx_undistort_keypoints",
+    "orbm_compute_distinctive_descriptors", "orbx_undistort_keypoints", "orbx_selftest_sincos",
 ]
 
 
@@ -150,6 +150,7 @@ _sig = {
     "orbm_search_by_projection": (I, [I, P, P, P, I, F, I, I, I, P, P]),
     "orbm_compute_distinctive_descriptors": (I, [P, P, I, I, P]),
     "orbx_undistort_keypoints": (I, [P, I, P, P, I, I, P]),
+    "orbx_selftest_sincos": (I, [P, I, P, P]),
 }
 for _n, (_r, _a) in _sig.items():
     _f = getattr(_lib, _n)
@@ -610,6 +611,17 @@ class StereoPlan:
         cnt = np.zeros(n, np.int32)
         _check(_lib.orbs_plan_stage_times(self._h, _p(ms), _p(cnt), n))
         return {name: (ms[i], int(cnt[i])) for i, name in enumerate(stage_names())}
+
+
+def selftest_sincos(x):
+    """(sin, cos) the BRIEF kernel uses for each float angle of the cuda float32
+    tensor x (radians); returns a cuda float32 tensor [n, 2]."""
+    import torch
+    out = torch.empty((x.numel(), 2), dtype=torch.float32, device=x.device)
+    _check(_lib.orbx_selftest_sincos(x.data_ptr(), x.numel(), out.data_ptr(), None),
+           "orbx_selftest_sincos")
+    torch.cuda.synchronize(x.device)
+    return out
 
 
 def synth_frames(out, first_idx, kind="rects", stream=None):

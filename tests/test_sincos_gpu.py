@@ -1,0 +1,111 @@
+"""Device sin/cos of the rotated-BRIEF stage (orbx_selftest_sincos runs the
+same brief_sincos as k_orient_brief: one wave per angle, exception keys held
+two per lane, ballot lookup).
+
+Expected value per angle x (radians, float32):
+  * x in the exception table (sincos_exceptions.inc, generated from glibc
+    2.35 sincosf -- ORBextractor.cc:58-59): glibc sincosf(x), bitwise;
+  * otherwise: orbx_sincos_core(x) (orbx_sincos.h), restated below in Python
+    double arithmetic (IEEE, no contraction), bitwise.
+tests/test_host.py::test_sincos_exception_table_is_current checks on the CPU,
+exhaustively, that this pair reproduces every BRIEF sample of glibc.
+"""
+import ctypes
+import math
+import os
+import re
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+INC = os.path.join(ROOT, "orb-slam-system_amd", "csrc", "sincos_exceptions.inc")
+
+PIO2_1 = 1.57079632673412561417e+00
+PIO2_1T = 6.07710050650619224932e-11
+INVPIO2 = 6.36619772367581382433e-01
+
+
+def _f32(v):
+    return float(np.float32(v))
+
+
+def _bits(v):
+    return int(np.float32(v).view(np.uint32))
+
+
+def _floor_d(v):
+    t = float(int(v))  # (double)(int64_t)v: truncation toward zero
+    return t - 1.0 if t > v else t
+
+
+def _ksin(r):
+    S1, S2, S3 = -1.66666666666666324348e-01, 8.33333333332248946124e-03, -1.98412698298579493134e-04
+    S4, S5, S6 = 2.75573137070700676789e-06, -2.50507602534068634195e-08, 1.58969099521155010221e-10
+    z = r * r
+    p = S2 + z * (S3 + z * (S4 + z * (S5 + z * S6)))
+    return r + r * z * (S1 + z * p)
+
+
+def _kcos(r):
+    C1, C2, C3 = 4.16666666666666019037e-02, -1.38888888888741095749e-03, 2.48015872894767294178e-05
+    C4, C5, C6 = -2.75573143513906633035e-07, 2.08757232129817482790e-09, -1.13596475577881948265e-11
+    z = r * r
+    p = z * (C1 + z * (C2 + z * (C3 + z * (C4 + z * (C5 + z * C6)))))
+    return (1.0 - 0.5 * z) + z * p
+
+
+def sincos_core(x):
+    """orbx_sincos_core (orbx_sincos.h:66-81) in Python doubles."""
+    xd = _f32(x)
+    kd = _floor_d(xd * INVPIO2 + 0.5)
+    k = int(kd)
+    r = (xd - kd * PIO2_1) - kd * PIO2_1T
+    sr, cr = _ksin(r), _kcos(r)
+    sv, cv = [(sr, cr), (cr, -sr), (-sr, -cr), (-cr, sr)][k & 3]
+    return _f32(sv), _f32(cv)
+
+
+def exception_table():
+    rows = re.findall(r"\{0x([0-9a-f]+)u, 0x([0-9a-f]+)u, 0x([0-9a-f]+)u\}", open(INC).read())
+    return {int(a, 16): (int(b, 16), int(c, 16)) for a, b, c in rows}
+
+
+def test_python_core_matches_glibc_mostly():
+    """Sanity of the restatement itself: it agrees with glibc sincosf on most
+    angles (exact agreement everywhere is not expected: glibc is not
+    correctly rounded, hence the exception table)."""
+    libm = ctypes.CDLL("libm.so.6")
+    libm.sincosf.argtypes = [ctypes.c_float, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float)]
+    s, c = ctypes.c_float(), ctypes.c_float()
+    rng = np.random.default_rng(3)
+    xs = rng.uniform(0, 2 * math.pi, 2000).astype(np.float32)
+    agree = 0
+    for x in xs:
+        libm.sincosf(float(x), ctypes.byref(s), ctypes.byref(c))
+        agree += (_bits(s.value), _bits(c.value)) == tuple(map(_bits, sincos_core(x)))
+    assert agree > 1600
+
+
+@pytest.mark.gpu
+def test_device_sincos_matches_table_and_core(gpu):
+    import torch
+    exc = exception_table()
+    assert len(exc) == 106
+    xs = []
+    for b in sorted(exc):  # every exception input and both float neighbours
+        xs += [b, b - 1, b + 1]
+    rng = np.random.default_rng(11)
+    xs += list(rng.uniform(0, 2 * math.pi, 4000).astype(np.float32).view(np.uint32))
+    xs += [0, _bits(2 * math.pi), _bits(math.pi / 2), _bits(math.pi)]
+    xbits = np.array(xs, dtype=np.uint32)
+    x = torch.from_numpy(xbits.view(np.float32).copy()).cuda()
+    got = gpu.selftest_sincos(x).cpu().numpy().view(np.uint32)
+    for i, b in enumerate(xbits):
+        b = int(b)
+        if b in exc:
+            want = exc[b]
+        else:
+            want = tuple(map(_bits, sincos_core(np.uint32(b).view(np.float32))))
+        assert (int(got[i, 0]), int(got[i, 1])) == want, \
+            "x=0x%08x: device (0x%08x, 0x%08x) vs (0x%08x, 0x%08x)" % (b, got[i, 0], got[i, 1], *want)
