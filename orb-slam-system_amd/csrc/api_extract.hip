@@ -301,8 +301,11 @@ extern "C" int orbx_plan_extract(orbx_plan* p, const uint8_t* frames, int nframe
   // K4+K5+K6+K7 orientation, blur-at-sample descriptors, assembly
   p->timer.begin(ORBX_STAGE_BRIEF, s);
   // waves stride over each frame's keypoints (about nfeatures of them)
-  int ob_waves = std::max(4, std::min(P.kcap, P.params.nfeatures + 256));
-  if (p->ob_div > 1) ob_waves = std::max(4, ob_waves / p->ob_div); /* profiling only */
+  // (about 4 keypoints per wave once the batch alone fills the chip: the
+  // next patch's loads overlap the current keypoint; measured 2 % faster)
+  const int ob_full = std::max(4, std::min(P.kcap, P.params.nfeatures + 256));
+  int ob_waves = std::min(ob_full, std::max((ob_full + 3) / 4, (16384 + n - 1) / n));
+  if (p->ob_div > 0) ob_waves = std::max(4, ob_full / p->ob_div); /* profiling only */
   hipLaunchKernelGGL(k_orient_brief, dim3((ob_waves + 3) / 4, n),
                      dim3(256), 0, s, frames, fstride, rstride, p->d_pyr, p->pyr_stride, p->bargs,
                      p->d_qout, p->qout_stride, p->d_lcount, kps, desc,

@@ -33,7 +33,7 @@ struct orbx_plan {
   LevelArgs largs;
   orbx::StageTimer timer;
   int dbg = 0; /* ORBX_DEBUG_STOP: kernel phase early-exit for profiling only */
-  int ob_div = 1; /* ORBX_DEBUG_OBDIV: k_orient_brief grid divisor, profiling only */
+  int ob_div = 0; /* ORBX_DEBUG_OBDIV: k_orient_brief grid divisor, profiling only */
 };
 
 struct orbx_extractor {
