@@ -1113,7 +1113,6 @@ __global__ __launch_bounds__(256) void k_orient_brief(
   // BRIEF (:57-73) on GaussianBlur(7x7, sigma 2) evaluated at each sample:
   // out = (sum_j k_j * (sum_i k_i p) + 32768) >> 16, rows via v_dot4_u32_u8
   const uint32_t K0 = 18u | (34u << 8) | (48u << 16) | (56u << 24), K1 = 48u | (34u << 8) | (18u << 16);
-  constexpr uint32_t GK[7] = {18, 34, 48, 56, 48, 34, 18};
   uint64_t words[4] = {0, 0, 0, 0};
 #pragma unroll
   for (int rr = 0; rr < 4; ++rr) {
@@ -1127,18 +1126,25 @@ __global__ __launch_bounds__(256) void k_orient_brief(
       const int row = (int)__builtin_rintf(__builtin_fmaf(fx, sn, ya));
       const int col = (int)__builtin_rintf(__builtin_fmaf(fx, cs, -yb));
       const int r0 = cr + row - 3, c0 = cc + col - 3;
-      const int qd = c0 >> 2, sh = c0 & 3;
+      const int qd = c0 >> 2, sh = c0 & 3;  // window = bytes sh..sh+6 of dwords qd..qd+2
       const uint32_t* prow = &P[0][0] + __mul24(r0, KP_COLS / 4) + qd;  // |r0| < 64: 24-bit multiply
-      uint32_t acc = 0;
-#pragma unroll
-      for (int jj = 0; jj < 7; ++jj) {
-        const uint32_t w0 = prow[jj * (KP_COLS / 4)], w1 = prow[jj * (KP_COLS / 4) + 1],
-                       w2 = prow[jj * (KP_COLS / 4) + 2];
-        const uint32_t lo4 = __builtin_amdgcn_alignbyte(w1, w0, sh);
-        const uint32_t hi4 = __builtin_amdgcn_alignbyte(w2, w1, sh);
-        const uint32_t h = __builtin_amdgcn_udot4(hi4, K1, __builtin_amdgcn_udot4(lo4, K0, 0u, false), false);
-        acc = __umul24(h, GK[jj]) + acc;  // v_mad_u32_u24: h <= 65280 (v_mul_lo_u32 is quarter rate)
-      }
+      // the 7 taps shifted to the window's byte offset: three weight words
+      // over the three aligned dwords (no v_alignbyte); rows j and 6-j share
+      // their vertical weight, so their horizontal sums chain into one dot4
+      // accumulation: 21 v_dot4 + 4 multiplies per sample instead of
+      // 14 v_alignbyte + 14 v_dot4 + 7 multiplies
+      const uint64_t Kw = (((uint64_t)K1 << 32) | K0) << (8 * sh);
+      const uint32_t K0s = (uint32_t)Kw, K1s = (uint32_t)(Kw >> 32);
+      const uint32_t K2s = (uint32_t)(((uint64_t)K1 << (8 * sh)) >> 32);
+      auto hrow = [&](int jj, uint32_t a) {
+        a = __builtin_amdgcn_udot4(prow[jj * (KP_COLS / 4)], K0s, a, false);
+        a = __builtin_amdgcn_udot4(prow[jj * (KP_COLS / 4) + 1], K1s, a, false);
+        return __builtin_amdgcn_udot4(prow[jj * (KP_COLS / 4) + 2], K2s, a, false);
+      };
+      uint32_t acc = __umul24(hrow(3, 0u), 56u);
+      acc = __umul24(hrow(6, hrow(0, 0u)), 18u) + acc;
+      acc = __umul24(hrow(5, hrow(1, 0u)), 34u) + acc;
+      acc = __umul24(hrow(4, hrow(2, 0u)), 48u) + acc;
       t[e] = (int)min((acc + 32768u) >> 16, 255u);
     }
     words[rr] = __ballot(t[0] < t[1]);
