@@ -284,7 +284,7 @@ extern "C" int orbx_plan_extract(orbx_plan* p, const uint8_t* frames, int nframe
   // K2 FAST cells
   p->timer.begin(ORBX_STAGE_FAST, s);
   if (!P.strips.empty()) {
-    hipLaunchKernelGGL(k_fast_strips, dim3((unsigned)P.strips.size(), n), dim3(256), p->fs_lds, s,
+    hipLaunchKernelGGL(k_fast_strips, dim3((unsigned)P.strips.size(), n), dim3(FS_NT), p->fs_lds, s,
                        frames, fstride, rstride, p->d_pyr, p->pyr_stride, p->largs, p->d_cells,
                        p->d_strips, p->d_slots, p->slot_stride, p->d_ccount, P.ncells, P.ini_th,
                        P.min_th, p->fs_tpitch, p->fs_tmaxh, p->fs_mcells, p->dbg);

@@ -371,12 +371,13 @@ __device__ __forceinline__ void wave_sync_lds() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+#define FS_NW (FS_NT / 64)
 #define FS_L1CAP 320 /* per-wave cardinal survivors: < 64 carried + <= 256 new */
 #define FS_L2CAP 128 /* per-wave even-test survivors: < 64 carried + <= 64 new */
 #define FS_CCAP 1024 /* per-strip corner list (overflow falls back to a map scan) */
 
 
-__global__ __launch_bounds__(256) void k_fast_strips(
+__global__ __launch_bounds__(FS_NT) void k_fast_strips(
     const uint8_t* __restrict__ frames, size_t fstride, size_t rstride,
     const uint8_t* __restrict__ pyr, size_t pstride, const LevelArgs LA,
     const CellInfo* __restrict__ cells, const StripInfo* __restrict__ strips,
@@ -388,8 +389,8 @@ __global__ __launch_bounds__(256) void k_fast_strips(
   unsigned long long* mask = reinterpret_cast<unsigned long long*>(amap + tpitch * tmax_h);
   unsigned long long* mask2 = mask + mcells * (tmax_h - 6);
   int* cnt = reinterpret_cast<int*>(mask2 + mcells * (tmax_h - 6));  // mcells
-  __shared__ uint16_t wlist1[4][FS_L1CAP];
-  __shared__ uint16_t wlist2[4][FS_L2CAP];
+  __shared__ uint16_t wlist1[FS_NW][FS_L1CAP];
+  __shared__ uint16_t wlist2[FS_NW][FS_L2CAP];
   __shared__ uint16_t clist[FS_CCAP];  // corners at t_lo (A > t_lo), any order
   __shared__ int cslot[ORBX_STRIP_MAXCELLS];
   __shared__ int ncorner;
@@ -409,11 +410,11 @@ __global__ __launch_bounds__(256) void k_fast_strips(
   const int tw = lead + st.w;           // columns in use
   {
     const uint8_t* s0 = base + (size_t)st.y * pitch + xal;
-    if (aligned16) stage_region<v4u, 4, 256>(tile, tpitch, s0, pitch, st.h, (tw + 15) >> 4, tid);
-    else if (aligned) stage_region<uint32_t, 12, 256>(tile, tpitch, s0, pitch, st.h, (tw + 3) >> 2, tid);
-    else stage_region<uint8_t, 16, 256>(tile, tpitch, s0, pitch, st.h, tw, tid);
+    if (aligned16) stage_region<v4u, 4, FS_NT>(tile, tpitch, s0, pitch, st.h, (tw + 15) >> 4, tid);
+    else if (aligned) stage_region<uint32_t, 12, FS_NT>(tile, tpitch, s0, pitch, st.h, (tw + 3) >> 2, tid);
+    else stage_region<uint8_t, 16, FS_NT>(tile, tpitch, s0, pitch, st.h, tw, tid);
   }
-  for (int i = tid; i < st.ncells * bh; i += 256) mask[i] = mask2[i] = 0ull;
+  for (int i = tid; i < st.ncells * bh; i += FS_NT) mask[i] = mask2[i] = 0ull;
   if (tid < st.ncells) {
     cnt[tid] = 0;
     cslot[tid] = slot_pref;
@@ -471,8 +472,8 @@ __global__ __launch_bounds__(256) void k_fast_strips(
     const uint32_t tt = (uint32_t)t_lo * 0x00010001u;
     const int it_first = wave * 64 + lane;
     int r = 3 + it_first / ng, g = g0 + it_first % ng;
-    const int dr = 256 / ng, dg = 256 - dr * ng;
-    for (int it0 = wave * 64; it0 < ntask; it0 += 256) {  // wave-uniform trip count
+    const int dr = FS_NT / ng, dg = FS_NT - dr * ng;
+    for (int it0 = wave * 64; it0 < ntask; it0 += FS_NT) {  // wave-uniform trip count
       const int it = it0 + lane;
       uint32_t clo = 0, chi = 0;  // candidate words: pixels 0,2 / 1,3 (16-bit lanes)
       if (it < ntask) {
@@ -578,13 +579,13 @@ __global__ __launch_bounds__(256) void k_fast_strips(
   };
   const int nc = ncorner;
   if (nc <= FS_CCAP) {
-    for (int q = tid; q < nc; q += 256) {
+    for (int q = tid; q < nc; q += FS_NT) {
       const int e = clist[q];
       const int r = e >> 9, c = e & 511;
       nms_pixel(r, c, amap[r * tpitch + c]);
     }
   } else {  // list overflow: scan the strength map
-    const int dr = 256 / ng, dg = 256 - dr * ng;
+    const int dr = FS_NT / ng, dg = FS_NT - dr * ng;
     int r = 3 + tid / ng, g = g0 + tid % ng;
     for (; r < 3 + bh;) {
       const uint32_t w4 = reinterpret_cast<const uint32_t*>(amap + r * tpitch)[g];
@@ -606,7 +607,7 @@ __global__ __launch_bounds__(256) void k_fast_strips(
   // pass 4: raster-order output per cell: one wave per cell, lane = band row,
   // row offsets by a wave prefix sum of the row popcounts
   uint32_t* fslots = slots + (size_t)f * slot_stride;
-  for (int k = wave; k < st.ncells; k += 4) {
+  for (int k = wave; k < st.ncells; k += FS_NW) {
     const unsigned long long* mk = (cnt[k] != 0 ? mask : mask2) + k * bh;
     const int cb0 = c0 + k * wcell, so = cslot[k];
     int carry = 0;

@@ -93,6 +93,9 @@ struct StereoArgs {
   float scale[ORBX_MAX_LEVELS], inv_scale[ORBX_MAX_LEVELS];
   float mb, mbf;
 };
+#ifndef FS_NT
+#define FS_NT 256 /* threads per k_fast_strips workgroup (one strip) */
+#endif
 #define ORBX_DEVERR_STEREO 4 /* the reference would index out of range / throw */
 #define ORBX_STEREO_MAXROWS 8192
 
