@@ -687,6 +687,8 @@ __device__ __forceinline__ void child_rect(int rx, int ry, int q, int* crx, int*
   *cry = ny0 | (ny1 << 16);
 }
 
+#define QT_J 16 /* keys per thread held in registers by k_quadtree (4096 per level) */
+
 __device__ __forceinline__ int upper_bound_i(const int* a, int n, int v) {
   int lo = 0, hi = n;
   while (lo < hi) {
@@ -730,10 +732,40 @@ __global__ __launch_bounds__(256) void k_quadtree(
   if (tid == 0) cell_off[nc] = C;
   __syncthreads();
   const uint32_t* fslots = slots + (size_t)f * slot_stride;
-  for (int k = tid; k < C; k += 256) {
+  // keys k = tid + 256 j (j < QT_J) and their node ids live in registers for
+  // the whole distribution (every pass walks all keys twice: from global
+  // memory that was a load-latency chain per pass); more keys than that
+  // spill to the global scratch.  keys[] in global memory also serves the
+  // final gather of the winners.
+  uint32_t kr[QT_J];
+  int nr[QT_J];
+#pragma unroll
+  for (int j = 0; j < QT_J; ++j) {
+    const int k = tid + 256 * j;
+    kr[j] = 0u;
+    nr[j] = -1;
+    if (k < C) {
+      const int c = upper_bound_i(cell_off, nc, k) - 1;
+      kr[j] = fslots[cells[U.cell_begin + c].slot_off + (k - cell_off[c])];
+      keys[k] = kr[j];
+    }
+  }
+  for (int k = tid + 256 * QT_J; k < C; k += 256) {
     const int c = upper_bound_i(cell_off, nc, k) - 1;
     keys[k] = fslots[cells[U.cell_begin + c].slot_off + (k - cell_off[c])];
   }
+  auto for_keys = [&](auto&& body) {  // body(k, key, node&)
+#pragma unroll
+    for (int j = 0; j < QT_J; ++j) {
+      const int k = tid + 256 * j;
+      if (k < C) body(k, kr[j], nr[j]);
+    }
+    for (int k = tid + 256 * QT_J; k < C; k += 256) {
+      int n = node[k];
+      body(k, keys[k], n);
+      node[k] = n;
+    }
+  };
   // initial nodes (:230-252)
   const int nIni = L.nini;
   int S = nIni;
@@ -743,16 +775,15 @@ __global__ __launch_bounds__(256) void k_quadtree(
     cnt[i] = 0;
   }
   __syncthreads();
-  for (int k = tid; k < C; k += 256) {
-    int n = -1;
+  for_keys([&](int, uint32_t key, int& n) {
+    n = -1;
     if (nIni > 0) {
-      const float x = (float)(keys[k] >> 20);
+      const float x = (float)(key >> 20);
       const int idx = (int)(x / L.hX);
       if (idx >= 0 && idx < nIni) n = idx;
     }
-    node[k] = n;
     if (n >= 0) atomicAdd(&cnt[n], 1);
-  }
+  });
   __syncthreads();
 
   int newS = 0;
@@ -765,10 +796,9 @@ __global__ __launch_bounds__(256) void k_quadtree(
     for (int i = tid; i < 4 * S; i += 256) child[i] = 0;
     if (tid == 0) s_flag = 0;
     __syncthreads();
-    for (int k = tid; k < C; k += 256) {
-      const int n = node[k];
-      if (n >= 0 && cnt[n] >= 2) atomicAdd(&child[4 * n + quadrant(keys[k], rx[n], ry[n])], 1);
-    }
+    for_keys([&](int, uint32_t key, int& n) {
+      if (n >= 0 && cnt[n] >= 2) atomicAdd(&child[4 * n + quadrant(key, rx[n], ry[n])], 1);
+    });
     __syncthreads();
     for (int i = tid; i < S; i += 256) {
       const int cn = cnt[i];
@@ -812,11 +842,9 @@ __global__ __launch_bounds__(256) void k_quadtree(
       }
     }
     __syncthreads();
-    for (int k = tid; k < C; k += 256) {
-      const int n = node[k];
-      if (n < 0) continue;
-      node[k] = (cnt[n] >= 2) ? child[4 * n + quadrant(keys[k], rx[n], ry[n])] : child[4 * n];
-    }
+    for_keys([&](int, uint32_t key, int& n) {
+      if (n >= 0) n = (cnt[n] >= 2) ? child[4 * n + quadrant(key, rx[n], ry[n])] : child[4 * n];
+    });
     const bool finish = (newS >= L.N) || (s_flag == 0);
     __syncthreads();
     if (finish) break;
@@ -836,11 +864,9 @@ __global__ __launch_bounds__(256) void k_quadtree(
   }
   for (int i = tid; i < newS; i += 256) best[i] = 0u;
   __syncthreads();
-  for (int k = tid; k < C; k += 256) {
-    const int n = node[k];
-    if (n >= 0 && n < newS)
-      atomicMax(&best[n], ((keys[k] & 0xFFu) << 24) | (0xFFFFFFu - (uint32_t)k));
-  }
+  for_keys([&](int k, uint32_t key, int& n) {
+    if (n >= 0 && n < newS) atomicMax(&best[n], ((key & 0xFFu) << 24) | (0xFFFFFFu - (uint32_t)k));
+  });
   __syncthreads();
   uint32_t* out = qout + (size_t)f * qout_stride + L.kout_off;
   for (int i = tid; i < newS; i += 256) {
