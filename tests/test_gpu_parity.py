@@ -45,6 +45,31 @@ def test_extract_matches_oracle(gpu, oracle, w, h, nf, L, guard, kind, idx):
         assert np.array_equal(ex.level(l), ref.level(l)), "pyramid level %d" % l
 
 
+# other pyramid ratios: the pyramid's 8-byte source window (k_pyramid) and
+# the planner's tiling change with the scale factor
+SCALE_CASES = [
+    # (w, h, nfeatures, scale, nlevels, kind, frame_idx)
+    (640, 480, 1000, 1.1, 12, "rects", 30),
+    (640, 480, 1000, 1.3, 8, "noise", 31),
+    (752, 480, 1200, 1.5, 6, "rects", 32),
+    (1241, 376, 2000, 1.7, 4, "noise", 33),
+    (640, 480, 800, 1.95, 3, "rects", 34),
+]
+
+
+@pytest.mark.parametrize("w,h,nf,sc,L,kind,idx", SCALE_CASES)
+def test_extract_scales_match_oracle(gpu, oracle, w, h, nf, sc, L, kind, idx):
+    img = synth.frame(w, h, idx, kind)
+    ref = oracle.Extractor(nf, sc, L, 20, 7, cell_guard="empty")
+    rk, rd = ref.extract(img)
+    ex = gpu.Extractor(nf, sc, L, 20, 7, cell_guard="empty")
+    k, d = ex.extract(img)
+    for l in range(L):
+        assert np.array_equal(ex.level(l), ref.level(l)), "pyramid level %d" % l
+    _cmp_kps(k, rk, "keypoints")
+    assert np.array_equal(d, rd), "descriptors differ"
+
+
 def test_strict_guard_1080p_raises(gpu):
     ex = gpu.Extractor(2000, 1.2, 8, 20, 7, cell_guard="strict")
     with pytest.raises(gpu.OrbxError) as e:
