@@ -372,7 +372,10 @@ __device__ __forceinline__ void wave_sync_lds() {
 }
 
 #define FS_NW (FS_NT / 64)
-#define FS_L1CAP 320 /* per-wave cardinal survivors: < 64 carried + <= 256 new */
+#ifndef FS_L1FLUSH
+#define FS_L1FLUSH 64 /* stage B runs once a wave's L1 holds this many entries */
+#endif
+#define FS_L1CAP (FS_L1FLUSH + 256) /* per-wave cardinal survivors: < FS_L1FLUSH carried + <= 256 new */
 #define FS_L2CAP 128 /* per-wave even-test survivors: < 64 carried + <= 64 new */
 #define FS_CCAP 1024 /* per-strip corner list (overflow falls back to a map scan) */
 
@@ -530,7 +533,7 @@ __global__ __launch_bounds__(FS_NT) void k_fast_strips(
         n1 += __popcll(bal);
       }
 #endif
-      if (n1 >= 64) {  // wave-uniform
+      if (n1 >= FS_L1FLUSH) {  // wave-uniform
         wave_sync_lds();
         while (n1 >= 64) {
           n1 -= 64;
@@ -545,6 +548,10 @@ __global__ __launch_bounds__(FS_NT) void k_fast_strips(
       if (g >= g1) { g -= ng; ++r; }
     }
     wave_sync_lds();
+    while (n1 >= 64) {  // leftovers above one batch (FS_L1FLUSH > 64)
+      n1 -= 64;
+      even_batch(L1[n1 + lane], true);
+    }
     if (n1 > 0) even_batch(lane < n1 ? (int)L1[lane] : 0, lane < n1);
     wave_sync_lds();
     if (n2 > 0) strength_batch(lane < n2 ? (int)L2[lane] : 0, lane < n2);
