@@ -198,8 +198,15 @@ extern "C" int orbx_plan_create(const orbx_params* prm, int width, int height, i
     p->fs_tmaxh = std::max(P.strip_max_h, 7);
     p->fs_qcap = 0;
     p->fs_mcells = std::max(P.strip_max_cells, 1);
-    p->fs_lds = 2 * (size_t)p->fs_tpitch * p->fs_tmaxh +
-                16 * (size_t)p->fs_mcells * (p->fs_tmaxh - 6) + 4 * (size_t)p->fs_mcells + 16;
+    /* tile + band-row strength map + counts; the NMS masks reuse the tile
+     * when they fit (k_fast_strips) */
+    const size_t tile = (size_t)p->fs_tpitch * p->fs_tmaxh;
+    const size_t masks = 16 * (size_t)p->fs_mcells * (p->fs_tmaxh - 6);
+    p->fs_lds = tile + (size_t)p->fs_tpitch * (p->fs_tmaxh - 6) + 4 * (size_t)((p->fs_mcells + 3) & ~3) +
+                (masks <= tile ? 0 : masks);
+#ifdef FS_LDS_PAD  // profiling variant: occupancy sensitivity of k_fast_strips
+    p->fs_lds += FS_LDS_PAD;
+#endif
     if (p->fs_lds > 150 * 1024) { plan_free(p); return ORBX_ERR_UNSUPPORTED; }
     if (hipFuncSetAttribute((const void*)k_fast_strips, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)p->fs_lds) != hipSuccess) { plan_free(p); return ORBX_ERR_HIP; }

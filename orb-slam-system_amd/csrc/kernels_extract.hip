@@ -386,12 +386,19 @@ __global__ __launch_bounds__(FS_NT) void k_fast_strips(
     const CellInfo* __restrict__ cells, const StripInfo* __restrict__ strips,
     uint32_t* __restrict__ slots, size_t slot_stride, uint32_t* __restrict__ ccount, int ncells,
     int ini_th, int min_th, int tpitch, int tmax_h, int mcells, int dbg) {
+  // LDS (occupancy is LDS-bound and the kernel is latency-bound: +12 KB per
+  // workgroup measured +38 % time): tile | strength map of the band rows only
+  // | per-cell counts; the NMS row masks reuse the tile, which is dead after
+  // pass 1 (fs_lds in api_extract.hip mirrors this layout)
   extern __shared__ __align__(16) uint32_t sm[];
   uint8_t* tile = reinterpret_cast<uint8_t*>(sm);                    // tpitch * tmax_h
-  uint8_t* amap = tile + tpitch * tmax_h;                             // tpitch * tmax_h
-  unsigned long long* mask = reinterpret_cast<unsigned long long*>(amap + tpitch * tmax_h);
+  uint8_t* amap_mem = tile + tpitch * tmax_h;                         // tpitch * (tmax_h - 6)
+  uint8_t* amap = amap_mem - 3 * tpitch;                              // indexed by tile row 3 .. 3+bh
+  int* cnt = reinterpret_cast<int*>(amap_mem + tpitch * (tmax_h - 6));  // mcells
+  const bool masks_in_tile = 16 * mcells * (tmax_h - 6) <= tpitch * tmax_h;
+  unsigned long long* mask = masks_in_tile ? reinterpret_cast<unsigned long long*>(tile)
+                                           : reinterpret_cast<unsigned long long*>(cnt + ((mcells + 3) & ~3));
   unsigned long long* mask2 = mask + mcells * (tmax_h - 6);
-  int* cnt = reinterpret_cast<int*>(mask2 + mcells * (tmax_h - 6));  // mcells
   __shared__ uint16_t wlist1[FS_NW][FS_L1CAP];
   __shared__ uint16_t wlist2[FS_NW][FS_L2CAP];
   __shared__ uint16_t clist[FS_CCAP];  // corners at t_lo (A > t_lo), any order
@@ -417,7 +424,6 @@ __global__ __launch_bounds__(FS_NT) void k_fast_strips(
     else if (aligned) stage_region<uint32_t, 12, FS_NT>(tile, tpitch, s0, pitch, st.h, (tw + 3) >> 2, tid);
     else stage_region<uint8_t, 16, FS_NT>(tile, tpitch, s0, pitch, st.h, tw, tid);
   }
-  for (int i = tid; i < st.ncells * bh; i += FS_NT) mask[i] = mask2[i] = 0ull;
   if (tid < st.ncells) {
     cnt[tid] = 0;
     cslot[tid] = slot_pref;
@@ -558,6 +564,8 @@ __global__ __launch_bounds__(FS_NT) void k_fast_strips(
   }
   __syncthreads();
   if (dbg == 2) return;
+  for (int i = tid; i < st.ncells * bh; i += FS_NT) mask[i] = mask2[i] = 0ull;  // over the dead tile
+  __syncthreads();
   // pass 2: cv::FAST NMS over the (sparse) nonzero strength map at both
   // thresholds in one scan: iniThFAST into mask (+ per-cell counts) and
   // minThFAST into mask2, used for cells left empty at iniThFAST (:293-296)
