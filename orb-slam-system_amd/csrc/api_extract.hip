@@ -282,7 +282,7 @@ extern "C" int orbx_plan_extract(orbx_plan* p, const uint8_t* frames, int nframe
   p->timer.begin(ORBX_STAGE_RESIZE, s);
   for (const PyrSeg& g : P.segs) {
     hipLaunchKernelGGL(k_pyramid, dim3(g.ntx * g.nty, n), dim3(256),
-                       g.lds_a + g.lds_b + g.lds_xl + g.lds_yl, s, frames, fstride, rstride,
+                       g.lds_a + g.lds_b + g.lds_yl, s, frames, fstride, rstride,
                        p->d_pyr, p->pyr_stride, g, reinterpret_cast<const int4*>(p->d_pyr_xs),
                        reinterpret_cast<const int4*>(p->d_pyr_ys),
                        reinterpret_cast<const uint4*>(p->d_pyr_blob), p->d_pyr_bo, p->dbg);
