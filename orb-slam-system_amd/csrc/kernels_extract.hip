@@ -989,24 +989,27 @@ __device__ __forceinline__ void brief_issue(const BriefKp& k, BriefRegs& R, int 
   } else {
     // patch crosses the level border: reflect-101 rows, dword loads where the
     // four columns are inside, reflected bytes at the left/right edge only
+    // 32-bit offsets from the wave-uniform level base (SGPR base + VGPR
+    // offset loads): this rare path must not set the kernel's VGPR count
     const int cx = k.px0 + (int)c4;
     const bool cin = cx >= 0 && cx + 4 <= k.UW;
 #pragma unroll
     for (int u = 0; u < 9; ++u) {
       const int r = min((int)r0 + 5 * u, KP_ROWS - 1);
       const int gy = reflect101(min(max(k.py0 + r, -3), k.UH + 2), k.UH);
-      const uint8_t* rowp = k.img + (size_t)gy * k.pitch;
+      const uint32_t ro = (uint32_t)(gy * k.pitch);
       if (cin) {
-        R.r[u] = *reinterpret_cast<const uint32_t*>(rowp + cx);
+        R.r[u] = *reinterpret_cast<const uint32_t*>(k.img + (ro + (uint32_t)cx));
       } else {
         uint32_t w = 0;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const int gx = reflect101(min(max(cx + j, -3), k.UW + 2), k.UW);
-          w |= (uint32_t)rowp[gx] << (8 * j);
+          w |= (uint32_t)k.img[ro + (uint32_t)gx] << (8 * j);
         }
         R.r[u] = w;
       }
+      __builtin_amdgcn_sched_barrier(0);  // one row's loads at a time
     }
   }
 }
@@ -1022,7 +1025,10 @@ __device__ __forceinline__ void brief_commit(const BriefRegs& R, uint32_t* P, in
   }
 }
 
-__global__ __launch_bounds__(256) void k_orient_brief(
+#ifndef OB_WPE
+#define OB_WPE 5
+#endif
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OB_WPE))) void k_orient_brief(
     const uint8_t* __restrict__ frames, size_t fstride, size_t rstride,
     const uint8_t* __restrict__ pyr, size_t pstride, const BriefArgs A,
     const uint32_t* __restrict__ qout, size_t qout_stride, const int* __restrict__ lcount,
@@ -1096,11 +1102,12 @@ __global__ __launch_bounds__(256) void k_orient_brief(
     brief_commit(R, &P[0][0], lane);
   } else {
     uint8_t* P8w = reinterpret_cast<uint8_t*>(P);
+#pragma clang loop unroll(disable) vectorize(disable) interleave(disable)
     for (int q = lane; q < KP_ROWS * KP_COLS; q += 64) {
       const int r = q / KP_COLS, c = q - r * KP_COLS;
       const int gy = reflect101(min(max(cur.py0 + r, -3), cur.UH + 2), cur.UH);
       const int gx = reflect101(min(max(cur.px0 + c, -3), cur.UW + 2), cur.UW);
-      P8w[q] = cur.img[(size_t)gy * cur.pitch + gx];
+      P8w[q] = cur.img[(uint32_t)(gy * cur.pitch + gx)];
     }
   }
   __builtin_amdgcn_wave_barrier();
