@@ -22,7 +22,7 @@ __global__ void k_match_resolve(const MProblem*, const MNodePair*, int, int, con
                                 const int4*, int2*);
 __global__ void k_match_resolve_spec(const MProblem*, const MNodePair*, int, const uint2*,
                                      const int4*, int2*, int);
-__global__ void k_match_finalize(const MProblem*, const MNodePair*, const int4*, const int2*, int*,
+__global__ void k_match_finalize(const MProblem*, const MNodePair*, const int4*, int2*, int*,
                                  const int*);
 __global__ void k_match_select(MProblem*, MNodePair*, const orbx_keypoint*, const int*,
                                const orbx_keypoint*, const int*, int, int, uint32_t*);

@@ -553,7 +553,6 @@ __global__ __launch_bounds__(256) void k_match_resolve(
   const int words = (P.n2 + 31) >> 5;
   for (int w = lane; w < words; w += 64) bm[w] = 0u;
   __builtin_amdgcn_wave_barrier();
-  const float factor = 1.0f / ORBM_HISTO;
   for (int j = np0; j < np1; ++j) {
     const MNodePair NP = nps[j];
     const uint32_t* f2 = P.feat2 + NP.off2;
@@ -616,16 +615,9 @@ __global__ __launch_bounds__(256) void k_match_resolve(
           }
         }
         if (best1 < ORBM_TH_LOW && (float)best1 < P.nnratio * (float)best2) {
-          int bin = 0;
-          if (P.check_ori) {
-            float rot = P.ang1[(size_t)idx1 * P.ang_stride] - P.ang2[(size_t)bidx2 * P.ang_stride];
-            if (rot < 0.0f) rot += 360.0f;
-            bin = (int)roundf(rot * factor);
-            if (bin == ORBM_HISTO) bin = 0;
-          }
-          if (lane == 0) {
+          if (lane == 0) {  // rotation bin: k_match_finalize
             bm[bidx2 >> 5] |= 1u << (bidx2 & 31);
-            ev[r] = make_int2(bidx2, bin);
+            ev[r] = make_int2(bidx2, 0);
           }
           __builtin_amdgcn_wave_barrier();
         }
@@ -661,43 +653,55 @@ __global__ __launch_bounds__(64) void k_match_resolve_spec(
   for (int w = lane; w < ((P.n2 + 31) >> 5); w += 64) bm[w] = 0u;
   for (int w = lane; w < P.n2; w += 64) claim[w] = 64;
   __builtin_amdgcn_wave_barrier();
-  const float factor = 1.0f / ORBM_HISTO;
-  // the next chunk's row info and candidate lists are loaded while the
-  // current chunk resolves (rows that are not feasible never read theirs)
-  int4 inf_n = make_int4(0, 0, 0, 0);
-  uint4 cv_n[ORBM_T / 2];
-  auto fetch = [&](int base) {
-    const int r = NP.row_base + base + lane;
-    inf_n = make_int4(0, 0, 0, 0);
-    if (base + lane < NP.n1) inf_n = rowinfo[r];
+  // row info + candidate lists of the chunks two ahead are in flight while
+  // a chunk resolves (two register buffers, used alternately)
+  // (unconditional loads at a clamped row: a load under a divergent branch
+  // would be waited for at the branch join; rows past n1 are masked in chunk)
+  auto fetch = [&](int4& inf_n, uint4 (&cv_n)[ORBM_T / 2], int base) {
+    const int r = NP.row_base + min(base + lane, NP.n1 - 1);
+    inf_n = rowinfo[r];
     const uint4* src = reinterpret_cast<const uint4*>(cand + (size_t)r * ORBM_T);
 #pragma unroll
-    for (int t = 0; t < ORBM_T / 2; ++t)
-      cv_n[t] = (base + lane < NP.n1) ? src[t] : make_uint4(0xFFFFFFFFu, 0u, 0xFFFFFFFFu, 0u);
+    for (int t = 0; t < ORBM_T / 2; ++t) cv_n[t] = src[t];
   };
-  fetch(0);
-  for (int base = 0; base < NP.n1; base += 64) {
+#ifdef RS_STATS
+  int st_feas = 0, st_chunks = 0, st_rounds = 0, st_hard = 0;
+#endif
+  auto chunk = [&](int4& inf_n, uint4 (&cv_n)[ORBM_T / 2], int base) {
     const int r = NP.row_base + base + lane;
     const int4 inf = inf_n;
-    const bool feas = inf.x != 0 && inf.z < ORBM_TH_LOW;
+    const bool feas = base + lane < NP.n1 && inf.x != 0 && inf.z < ORBM_TH_LOW;
     uint2 c[ORBM_T];
 #pragma unroll
     for (int t = 0; t < ORBM_T / 2; ++t) {
       c[2 * t] = feas ? make_uint2(cv_n[t].x, cv_n[t].y) : make_uint2(0xFFFFFFFFu, 0u);
       c[2 * t + 1] = feas ? make_uint2(cv_n[t].z, cv_n[t].w) : make_uint2(0xFFFFFFFFu, 0u);
     }
-    if (base + 64 < NP.n1) fetch(base + 64);
+    // the buffer is consumed before it is refilled, so the refill can take the
+    // same registers (otherwise the loop latch copies it, waiting on vmcnt)
+    __builtin_amdgcn_sched_barrier(0);
+    fetch(inf_n, cv_n, base + 128);  // unconditional (clamped rows)
     uint64_t pend = __ballot(feas);
-    if (!pend) continue;
+    if (!pend) return;
+#ifdef RS_STATS
+    st_feas += __popcll(pend); st_chunks++;
+#endif
     while (pend) {
+#ifdef RS_STATS
+      st_rounds++;
+#endif
       const bool mine = (pend >> lane) & 1ull;
-      int k1 = INT_MAX, k2 = INT_MAX, id1 = -1, nun = 0, plen = ORBM_T;
-      if (mine) {
+      // all bitmap words first (independent LDS reads, one wait), then the
+      // in-order scan in registers; empty slots read word 0 harmlessly
+      uint32_t bw[ORBM_T];
 #pragma unroll
-        for (int t = 0; t < ORBM_T; ++t) {
-          if (nun >= 2 || c[t].x == 0xFFFFFFFFu) continue;
-          const int i2 = (int)c[t].y;
-          if ((bm[i2 >> 5] >> (i2 & 31)) & 1u) continue;
+      for (int t = 0; t < ORBM_T; ++t) bw[t] = bm[c[t].y >> 5];
+      int k1 = INT_MAX, k2 = INT_MAX, id1 = -1, nun = 0, plen = ORBM_T;
+#pragma unroll
+      for (int t = 0; t < ORBM_T; ++t) {
+        const int i2 = (int)c[t].y;
+        const bool un = c[t].x != 0xFFFFFFFFu && !((bw[t] >> (i2 & 31)) & 1u);
+        if (un && nun < 2) {
           if (nun == 0) { k1 = (int)(c[t].x >> 16); id1 = i2; }
           else { k2 = (int)(c[t].x >> 16); plen = t + 1; }
           ++nun;
@@ -707,31 +711,29 @@ __global__ __launch_bounds__(64) void k_match_resolve_spec(
       const bool acc = mine && !hard && k1 < ORBM_TH_LOW && (float)k1 < P.nnratio * (float)k2;
       if (acc) atomicMin(&claim[id1], lane);
       __builtin_amdgcn_wave_barrier();
-      bool conf = false;
-      if (mine) {
+      int cl[ORBM_T];
 #pragma unroll
-        for (int t = 0; t < ORBM_T; ++t)
-          if (t < plen && c[t].x != 0xFFFFFFFFu && claim[c[t].y] < lane) conf = true;
-      }
+      for (int t = 0; t < ORBM_T; ++t) cl[t] = claim[c[t].y];
+      bool conf = false;
+#pragma unroll
+      for (int t = 0; t < ORBM_T; ++t)
+        conf |= t < plen && c[t].x != 0xFFFFFFFFu && cl[t] < lane;
+      conf = conf && mine;
       const uint64_t cm = __ballot(conf || hard);
       const int bnd = cm ? (__ffsll((unsigned long long)cm) - 1) : 64;
       __builtin_amdgcn_wave_barrier();
       if (acc) claim[id1] = 64;
-      if (mine && lane < bnd && acc) {
-        int bin = 0;
-        if (P.check_ori) {
-          float rot = P.ang1[(size_t)inf.w * P.ang_stride] - P.ang2[(size_t)id1 * P.ang_stride];
-          if (rot < 0.0f) rot += 360.0f;
-          bin = (int)roundf(rot * factor);
-          if (bin == ORBM_HISTO) bin = 0;
-        }
+      if (mine && lane < bnd && acc) {  // rotation bin: k_match_finalize
         atomicOr(&bm[id1 >> 5], 1u << (id1 & 31));
-        ev[r] = make_int2(id1, bin);
+        ev[r] = make_int2(id1, 0);
       }
       __builtin_amdgcn_wave_barrier();
       pend &= (bnd >= 64) ? 0ull : ~((1ull << bnd) - 1ull);
       if (pend && bnd < 64 && ((__ballot(hard) >> bnd) & 1ull)) {
         // lowest pending row ran out of candidates: exact rescan of list2 (whole wave)
+#ifdef RS_STATS
+        st_hard++;
+#endif
         const int idx1 = __shfl(inf.w, bnd, 64);
         const uint32_t* q1 = reinterpret_cast<const uint32_t*>(P.desc1 + (size_t)idx1 * 32);
         uint32_t d1[8];
@@ -755,22 +757,29 @@ __global__ __launch_bounds__(64) void k_match_resolve_spec(
         if (kb != 0xFFFFFFFFu) {
           const int b1 = (int)(kb >> 16), bi = (int)f2[kb & 0xFFFFu];
           if (b1 < ORBM_TH_LOW && (float)b1 < P.nnratio * (float)d2 && lane == bnd) {
-            int bin = 0;
-            if (P.check_ori) {
-              float rot = P.ang1[(size_t)idx1 * P.ang_stride] - P.ang2[(size_t)bi * P.ang_stride];
-              if (rot < 0.0f) rot += 360.0f;
-              bin = (int)roundf(rot * factor);
-              if (bin == ORBM_HISTO) bin = 0;
-            }
             atomicOr(&bm[bi >> 5], 1u << (bi & 31));
-            ev[r] = make_int2(bi, bin);
+            ev[r] = make_int2(bi, 0);
           }
         }
         __builtin_amdgcn_wave_barrier();
         pend &= ~(1ull << bnd);
       }
     }
+  };
+  int4 infA, infB;
+  uint4 cvA[ORBM_T / 2], cvB[ORBM_T / 2];
+  if (NP.n1 <= 0) return;
+  fetch(infA, cvA, 0);
+  fetch(infB, cvB, 64);
+  for (int base = 0; base < NP.n1; base += 128) {
+    chunk(infA, cvA, base);
+    if (base + 64 < NP.n1) chunk(infB, cvB, base + 64);
   }
+#ifdef RS_STATS
+  if (lane == 0 && unit < 4)
+    printf("RS unit %d n1 %d n2 %d feas %d chunks %d rounds %d hard %d\n", unit, NP.n1, NP.n2,
+           st_feas, st_chunks, st_rounds, st_hard);
+#endif
 }
 
 // ---------------------------------------------------------------------------
@@ -779,7 +788,7 @@ __global__ __launch_bounds__(64) void k_match_resolve_spec(
 __global__ __launch_bounds__(256) void k_match_finalize(const MProblem* __restrict__ probs,
                                                         const MNodePair* __restrict__ nps,
                                                         const int4* __restrict__ rowinfo,
-                                                        const int2* __restrict__ ev,
+                                                        int2* __restrict__ ev,
                                                         int* __restrict__ last_scratch,
                                                         const int* __restrict__ scratch_off) {
   __shared__ int hist[ORBM_HISTO];
@@ -787,6 +796,7 @@ __global__ __launch_bounds__(256) void k_match_finalize(const MProblem* __restri
   __shared__ int s_nev, s_nfilt;
   const int p = blockIdx.x, tid = threadIdx.x;
   const MProblem P = probs[p];
+  const float factor = 1.0f / ORBM_HISTO;
   int* last = last_scratch + scratch_off[p];
   for (int i = tid; i < P.n1; i += 256) {
     P.match12[i] = -1;
@@ -802,8 +812,16 @@ __global__ __launch_bounds__(256) void k_match_finalize(const MProblem* __restri
       const int2 e = ev[r];
       if (e.x < 0) continue;
       const int idx1 = rowinfo[r].w;
+      int bin = 0;  // rotation histogram bin (ORBmatcher.cc:332-340)
+      if (P.check_ori) {
+        float rot = P.ang1[(size_t)idx1 * P.ang_stride] - P.ang2[(size_t)e.x * P.ang_stride];
+        if (rot < 0.0f) rot += 360.0f;
+        bin = (int)roundf(rot * factor);
+        if (bin == ORBM_HISTO) bin = 0;
+        ev[r].y = bin;  // read back by this thread below
+      }
       atomicMax(&last[idx1], r);
-      atomicAdd(&hist[e.y], 1);
+      atomicAdd(&hist[bin], 1);
       ++nev;
     }
   }
