@@ -232,3 +232,19 @@ def test_search_by_bow_heavy_contention(gpu, oracle, seed):
         m, nm = gpu.search_by_bow(kf1, kf2, ratio, seed != 1)
         rm, rnm = oracle.search_by_bow(kf1, kf2, ratio, seed != 1)
         assert nm == rnm and np.array_equal(m, rm), ratio
+
+
+@pytest.mark.parametrize("n1,n2", [(1, 5), (63, 64), (64, 63), (65, 200), (128, 2), (129, 1), (130, 130)])
+def test_search_by_bow_chunk_edges(gpu, oracle, n1, n2):
+    """Node lists around the resolver's 64-row chunk and two-chunk prefetch
+    boundaries (rows past n1 are loaded clamped and must be masked)."""
+    rng = np.random.default_rng(n1 * 1000 + n2)
+    d1 = rng.integers(0, 256, (n1, 32), dtype=np.uint8)
+    d2 = _correlated(rng, d1[rng.integers(0, n1, n2)], rng.integers(0, 30, n2))
+    one = lambda d: dict(desc=d, angle=rng.uniform(0, 360, len(d)).astype(np.float32), valid=None,
+                         node_id=np.array([5], np.uint32), off=np.array([0, len(d)], np.uint32),
+                         feat=np.arange(len(d), dtype=np.uint32))
+    kf1, kf2 = one(d1), one(d2)
+    m, nm = gpu.search_by_bow(kf1, kf2, 0.75, True)
+    rm, rnm = oracle.search_by_bow(kf1, kf2, 0.75, True)
+    assert nm == rnm and np.array_equal(m, rm)
