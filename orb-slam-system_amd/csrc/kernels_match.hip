@@ -321,12 +321,11 @@ __device__ __forceinline__ uint32_t med3u(uint32_t a, uint32_t b, uint32_t c) {
   return r;
 }
 __device__ __forceinline__ void topk_insert(uint32_t (&L)[ORBM_T], uint32_t k) {
-  uint32_t N[ORBM_T];
-  N[0] = min(L[0], k);
+  // in place, last slot first: each result takes the register of the value
+  // it replaces (ascending order made the allocator rotate 7 v_mov per insert)
 #pragma unroll
-  for (int t = 1; t < ORBM_T; ++t) N[t] = med3u(L[t - 1], k, L[t]);
-#pragma unroll
-  for (int t = 0; t < ORBM_T; ++t) L[t] = N[t];
+  for (int t = ORBM_T - 1; t >= 1; --t) L[t] = med3u(L[t - 1], k, L[t]);
+  L[0] = min(L[0], k);
 }
 
 __global__ __launch_bounds__(256) void k_match_cand_rows(
