@@ -49,25 +49,31 @@ template <typename T, int U, int NT>
 __device__ __forceinline__ void stage_region(uint8_t* __restrict__ lds, int lpitch,
                                              const uint8_t* __restrict__ src, size_t sp, int nrows,
                                              int nper, int tid) {
+  // (row, column) of element tid + NT*k advance by (dr, dc) per step: no
+  // per-load division; offsets are 24-bit products (rows * pitch < 2^32,
+  // both factors < 2^24) added to the wave-uniform base
   const int total = nrows * nper;
+  if (total <= 0) return;
+  const int dr = NT / nper, dc = NT - dr * nper;
+  int r = tid / nper, c = tid - r * nper;
+  const uint32_t spu = (uint32_t)sp;
   for (int i0 = tid; i0 < total; i0 += NT * U) {
     T v[U];
+    int rr[U], cc[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int i = i0 + NT * u;
-      if (i < total) {
-        const int r = i / nper, c = i - r * nper;
-        v[u] = reinterpret_cast<const T*>(src + (size_t)r * sp)[c];
-      }
+      rr[u] = r;
+      cc[u] = c;
+      if (i0 + NT * u < total)
+        v[u] = *reinterpret_cast<const T*>(src + (__umul24((uint32_t)r, spu) + (uint32_t)c * (uint32_t)sizeof(T)));
+      r += dr;
+      c += dc;
+      if (c >= nper) { c -= nper; ++r; }
     }
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int i = i0 + NT * u;
-      if (i < total) {
-        const int r = i / nper, c = i - r * nper;
-        reinterpret_cast<T*>(lds + r * lpitch)[c] = v[u];
-      }
-    }
+    for (int u = 0; u < U; ++u)
+      if (i0 + NT * u < total)
+        reinterpret_cast<T*>(lds + __mul24(rr[u], lpitch))[cc[u]] = v[u];
   }
 }
 
@@ -484,10 +490,13 @@ __global__ __launch_bounds__(FS_NT) void k_fast_strips(
       const int it = it0 + lane;
       uint32_t clo = 0, chi = 0;  // candidate words: pixels 0,2 / 1,3 (16-bit lanes)
       if (it < ntask) {
-        const uint32_t* row0 = reinterpret_cast<const uint32_t*>(tile + r * tpitch);
-        const uint32_t w0 = g > 0 ? row0[g - 1] : 0u, w1 = row0[g], w2 = row0[g + 1];
-        const uint32_t up = reinterpret_cast<const uint32_t*>(tile + (r - 3) * tpitch)[g];
-        const uint32_t dn = reinterpret_cast<const uint32_t*>(tile + (r + 3) * tpitch)[g];
+        // (g = 0: w0 is the previous row's last dword -- only pixels left of
+        // the band, rejected in stage B, read it; r >= 3 keeps it in the tile)
+        const int ro = __mul24(r, tpitch);
+        const uint32_t* row0 = reinterpret_cast<const uint32_t*>(tile + ro);
+        const uint32_t w0 = row0[g - 1], w1 = row0[g], w2 = row0[g + 1];
+        const uint32_t up = reinterpret_cast<const uint32_t*>(tile + ro - 3 * tpitch)[g];
+        const uint32_t dn = reinterpret_cast<const uint32_t*>(tile + ro + 3 * tpitch)[g];
         const uint32_t I4 = __builtin_amdgcn_alignbyte(w2, w1, 3);   // (x+3, y)
         const uint32_t I12 = __builtin_amdgcn_alignbyte(w1, w0, 1);  // (x-3, y)
 #pragma unroll
@@ -508,7 +517,7 @@ __global__ __launch_bounds__(FS_NT) void k_fast_strips(
           const uint32_t x = as_u32(db) | as_u32(dd);
           if (h) chi = x; else clo = x;
         }
-        reinterpret_cast<uint32_t*>(amap + r * tpitch)[g] = 0u;
+        reinterpret_cast<uint32_t*>(amap + ro)[g] = 0u;
 #ifdef FAST_PAD
         // profiling only: FAST_PAD dependent VALU ops per group (issue-bound probe)
         uint32_t pz = clo;
