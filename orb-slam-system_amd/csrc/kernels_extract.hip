@@ -64,8 +64,10 @@ __device__ __forceinline__ void stage_region(uint8_t* __restrict__ lds, int lpit
     for (int u = 0; u < U; ++u) {
       rr[u] = r;
       cc[u] = c;
-      if (i0 + NT * u < total)
-        v[u] = *reinterpret_cast<const T*>(src + (__umul24((uint32_t)r, spu) + (uint32_t)c * (uint32_t)sizeof(T)));
+      // unconditional (a guarded load is waited for at its branch join):
+      // elements past the end read the last row, and are not stored
+      v[u] = *reinterpret_cast<const T*>(
+          src + (__umul24((uint32_t)min(r, nrows - 1), spu) + (uint32_t)c * (uint32_t)sizeof(T)));
       r += dr;
       c += dc;
       if (c >= nper) { c -= nper; ++r; }
