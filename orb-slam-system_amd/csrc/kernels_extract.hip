@@ -962,7 +962,8 @@ __device__ __forceinline__ void brief_sincos(float x, uint32_t exk0, uint32_t ex
   }
 }
 
-// Keypoint patch: rows y-21..y+21, 48 columns from (x-21) & ~3 (dword aligned);
+// Keypoint patch: rows y-21..y+21, 48 columns from (x-21) & ~3 (a multiple of
+// 4 in level coordinates; the row addresses need not be dword aligned);
 // covers IC_Angle's radius-15 disk and every blur tap of the radius-18 samples.
 #define KP_R 21
 #define KP_ROWS 43
@@ -976,7 +977,6 @@ struct BriefKp {
   const uint8_t* img;
   int pitch, UW, UH, px0, py0;
   bool inside;   // the whole patch lies in the level
-  bool aligned;  // level base and pitch are dword aligned (register path usable)
 };
 
 // the patch is 43 rows x 12 dwords: lane (< 60) owns column lane % 12 of
@@ -987,6 +987,14 @@ struct BriefRegs {
   uint32_t r[9];
 };
 
+// dword load at any byte address (gfx950 global memory accepts unaligned
+// dword accesses; the memcpy form lets the compiler emit one global_load_dword)
+__device__ __forceinline__ uint32_t ld32u(const uint8_t* p) {
+  uint32_t w;
+  __builtin_memcpy(&w, p, 4);
+  return w;
+}
+
 __device__ __forceinline__ void brief_issue(const BriefKp& k, BriefRegs& R, int lane) {
   const int ln = min(lane, 59);
   const uint32_t c4 = (uint32_t)(ln % 12) * 4u, r0 = (uint32_t)(ln / 12);
@@ -995,7 +1003,7 @@ __device__ __forceinline__ void brief_issue(const BriefKp& k, BriefRegs& R, int 
 #pragma unroll
     for (int u = 0; u < 9; ++u) {
       const uint32_t row = min(r0 + 5u * u, (uint32_t)(KP_ROWS - 1));
-      R.r[u] = *reinterpret_cast<const uint32_t*>(b + (row * (uint32_t)k.pitch + c4));
+      R.r[u] = ld32u(b + (row * (uint32_t)k.pitch + c4));
     }
   } else {
     // patch crosses the level border: reflect-101 rows, dword loads where the
@@ -1010,7 +1018,7 @@ __device__ __forceinline__ void brief_issue(const BriefKp& k, BriefRegs& R, int 
       const int gy = reflect101(min(max(k.py0 + r, -3), k.UH + 2), k.UH);
       const uint32_t ro = (uint32_t)(gy * k.pitch);
       if (cin) {
-        R.r[u] = *reinterpret_cast<const uint32_t*>(k.img + (ro + (uint32_t)cx));
+        R.r[u] = ld32u(k.img + (ro + (uint32_t)cx));
       } else {
         uint32_t w = 0;
 #pragma unroll
@@ -1094,7 +1102,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OB_WPE))) v
     k.px0 = (k.x - KP_R) & ~3;
     k.py0 = k.y - KP_R;
     k.inside = k.px0 >= 0 && k.px0 + KP_COLS <= k.UW && k.py0 >= 0 && k.py0 + KP_ROWS <= k.UH;
-    k.aligned = ((reinterpret_cast<uintptr_t>(k.img) | (uintptr_t)k.pitch) & 3) == 0;
     return k;
   };
   // output position o (levels concatenated, :455-494); waves stride over
@@ -1106,27 +1113,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OB_WPE))) v
   if (o >= total) return;
   BriefKp cur = locate(o);
   BriefRegs R;
-  if (cur.aligned) brief_issue(cur, R, lane);
+  brief_issue(cur, R, lane);
   for (; o < total; o += stride) {  // wave-uniform
   // ---- stage this keypoint's patch (unblurred level), reflect-101 outside ----
-  if (cur.aligned) {
-    brief_commit(R, &P[0][0], lane);
-  } else {
-    uint8_t* P8w = reinterpret_cast<uint8_t*>(P);
-#pragma clang loop unroll(disable) vectorize(disable) interleave(disable)
-    for (int q = lane; q < KP_ROWS * KP_COLS; q += 64) {
-      const int r = q / KP_COLS, c = q - r * KP_COLS;
-      const int gy = reflect101(min(max(cur.py0 + r, -3), cur.UH + 2), cur.UH);
-      const int gx = reflect101(min(max(cur.px0 + c, -3), cur.UW + 2), cur.UW);
-      P8w[q] = cur.img[(uint32_t)(gy * cur.pitch + gx)];
-    }
-  }
+  brief_commit(R, &P[0][0], lane);
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   const BriefKp me = cur;
   if (o + stride < total) {  // next keypoint: its patch loads stay in flight
     cur = locate(o + stride);
-    if (cur.aligned) brief_issue(cur, R, lane);
+    brief_issue(cur, R, lane);
   }
   const int l = me.l, x = me.x, score = me.score, px0 = me.px0;
   // IC_Angle (:21-48) on the unblurred level (integer sums: order-free).
