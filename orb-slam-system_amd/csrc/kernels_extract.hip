@@ -79,6 +79,49 @@ __device__ __forceinline__ void stage_region(uint8_t* __restrict__ lds, int lpit
   }
 }
 
+// dword load at any byte address (gfx950 global memory accepts unaligned
+// dword accesses; the memcpy form lets the compiler emit one global_load_dword)
+__device__ __forceinline__ uint32_t ld32u(const uint8_t* p) {
+  uint32_t w;
+  __builtin_memcpy(&w, p, 4);
+  return w;
+}
+
+// Rows of nbytes at any byte alignment into dword-aligned LDS rows: one
+// unaligned dword load per 4 bytes.  A row's last dword is loaded ending at
+// the row's last byte and shifted into place, so nothing past the row is read
+// (the caller's frame may end there).  Same indexing as stage_region.
+template <int U, int NT>
+__device__ __forceinline__ void stage_rows_u32(uint8_t* __restrict__ lds, int lpitch,
+                                               const uint8_t* __restrict__ src, size_t sp,
+                                               int nrows, int nbytes, int tid) {
+  const int nper = (nbytes + 3) >> 2;
+  const int total = nrows * nper;
+  if (total <= 0) return;
+  const int dr = NT / nper, dc = NT - dr * nper;
+  int r = tid / nper, c = tid - r * nper;
+  const uint32_t spu = (uint32_t)sp;
+  const int lastc = max(nbytes - 4, 0);
+  for (int i0 = tid; i0 < total; i0 += NT * U) {
+    uint32_t v[U];
+    int rr[U], cc[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      rr[u] = r;
+      cc[u] = c;
+      const int cb = 4 * c, cl = min(cb, lastc);
+      v[u] = ld32u(src + (__umul24((uint32_t)min(r, nrows - 1), spu) + (uint32_t)cl)) >> (8 * (cb - cl));
+      r += dr;
+      c += dc;
+      if (c >= nper) { c -= nper; ++r; }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (i0 + NT * u < total)
+        reinterpret_cast<uint32_t*>(lds + __mul24(rr[u], lpitch))[cc[u]] = v[u];
+  }
+}
+
 typedef unsigned short us2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ us2 as_us2(uint32_t x) { return __builtin_bit_cast(us2, x); }
 __device__ __forceinline__ uint32_t as_u32(us2 x) { return __builtin_bit_cast(uint32_t, x); }
@@ -145,7 +188,7 @@ __global__ __launch_bounds__(256) void k_pyramid(const uint8_t* __restrict__ fra
       const int d0 = (X.x & ~3) - cax, nd = (((X.y + 3) & ~3) - (X.x & ~3)) >> 2;
       stage_region<uint32_t, 8, 256>(cur + d0, cpitch, s0 + cax + d0, sp, nr, nd, tid);
     } else {
-      stage_region<uint8_t, 16, 256>(cur + (X.x - cax), cpitch, s0 + X.x, sp, nr, X.y - X.x, tid);
+      stage_rows_u32<8, 256>(cur, cpitch, s0 + cax, sp, nr, X.y - cax, tid);
     }
   }
   __syncthreads();
@@ -428,7 +471,7 @@ __global__ __launch_bounds__(FS_NT) void k_fast_strips(
     const uint8_t* s0 = base + (size_t)st.y * pitch + xal;
     if (aligned16) stage_region<v4u, 4, FS_NT>(tile, tpitch, s0, pitch, st.h, (tw + 15) >> 4, tid);
     else if (aligned) stage_region<uint32_t, 12, FS_NT>(tile, tpitch, s0, pitch, st.h, (tw + 3) >> 2, tid);
-    else stage_region<uint8_t, 16, FS_NT>(tile, tpitch, s0, pitch, st.h, tw, tid);
+    else stage_rows_u32<12, FS_NT>(tile, tpitch, s0, pitch, st.h, tw, tid);
   }
   if (tid < st.ncells) {
     cnt[tid] = 0;
@@ -986,14 +1029,6 @@ struct BriefKp {
 struct BriefRegs {
   uint32_t r[9];
 };
-
-// dword load at any byte address (gfx950 global memory accepts unaligned
-// dword accesses; the memcpy form lets the compiler emit one global_load_dword)
-__device__ __forceinline__ uint32_t ld32u(const uint8_t* p) {
-  uint32_t w;
-  __builtin_memcpy(&w, p, 4);
-  return w;
-}
 
 __device__ __forceinline__ void brief_issue(const BriefKp& k, BriefRegs& R, int lane) {
   const int ln = min(lane, 59);
