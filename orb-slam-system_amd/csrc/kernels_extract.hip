@@ -585,8 +585,8 @@ __global__ __launch_bounds__(FS_NT) void k_fast_strips(
         const uint32_t x = (j & 1) ? chi : clo;
         const bool k = ((j & 2) ? (x >> 16) : (x & 0xFFFFu)) != 0;
         const unsigned long long bal = __ballot(k);
-        const int pos = n1 + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
-                                                            __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+        const int pos = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
+                                                       __builtin_amdgcn_mbcnt_lo((uint32_t)bal, (uint32_t)n1));
         if (k) L1[pos] = (uint16_t)(ebase + (uint32_t)j);
         n1 += __popcll(bal);
       }

@@ -18,6 +18,8 @@ EXTRACT_CASES = [
     (640, 480, 1000, 1, "strict", "rects", 3),     # config 2: single level
     (1241, 376, 2000, 8, "strict", "rects", 4),    # config 5 shape (KITTI)
     (752, 480, 1200, 8, "strict", "noise", 5),     # EuRoC shape
+    (644, 362, 1000, 8, "strict", "noise", 8),     # rows dword- but not 16-B-aligned
+    (642, 361, 1000, 8, "strict", "rects", 9),     # rows 2 mod 4: unaligned dword staging
     (1920, 1080, 2000, 8, "empty", "rects", 6),    # config 3 (cell_guard=empty)
     (1920, 1080, 2000, 8, "empty", "noise", 7),
 ]
