@@ -131,7 +131,7 @@ int orbx_plan_geometry(const orbx_plan* plan, orbx_geometry* g);
 
 /* d_frames: nframes images, frame i at d_frames + i*frame_stride, rows of
  * row_stride bytes (device memory; any byte alignment -- 16-B aligned rows
- * take the fastest staging path, and nothing outside the frames' width x
+ * take the fastest staging path; no byte outside a frame's row_stride x
  * height bytes is read).  Outputs (device memory):
  *   d_kps  [nframes][kcap], d_desc [nframes][kcap][32], d_counts [nframes].
  * Asynchronous on `stream` (a hipStream_t; NULL = the default stream).
