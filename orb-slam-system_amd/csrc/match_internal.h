@@ -10,7 +10,9 @@
 
 #include <stdint.h>
 
+#ifndef ORBM_T
 #define ORBM_T 8           /* candidates kept per row                     */
+#endif
 #define ORBM_TH_LOW 50     /* ORBmatcher::TH_LOW (ORBmatcher.cc:14)       */
 #define ORBM_HISTO 30      /* ORBmatcher::HISTO_LENGTH (ORBmatcher.cc:15) */
 #define ORBM_MAX_N2 65536  /* list positions / idx2 bitmap bound          */
