@@ -2,10 +2,10 @@
 """ORB extract+match throughput on MI355X (BASELINE.json metric).
 
 One step = one pass of the hot path over one resident batch of synthetic
-1920x1080 frames per GPU:
-  * ORBextractor on every frame (8-level pyramid, FAST cells, quadtree,
+frames per GPU:
+  * ORBextractor on every frame (pyramid, FAST cells, quadtree,
     orientation, rotated BRIEF) -- orbx_plan_extract;
-  * ORBmatcher::SearchByBoW brute force (one vocabulary node, top-2000
+  * ORBmatcher::SearchByBoW brute force (one vocabulary node, top-N
     keypoints by response) of every frame against its predecessor --
     orbm_plan_match_frames.  Frames are sharded in contiguous blocks per
     rank; the first frame of a rank is matched against the last frame of the
@@ -13,18 +13,31 @@ One step = one pass of the hot path over one resident batch of synthetic
     RCCL all-gather over xGMI (the one real exchange step).
 value = frames processed by all ranks / max-over-ranks wall time.
 
-python bench.py [--gpus N --steps K --warmup W --batch B]
-multi-GPU: python -m torch.distributed.run --nproc-per-node N bench.py --gpus N
+Workloads (--workload; BASELINE.json configs):
+  c4  (default, the headline) 1920x1080, 8 levels, 2000 features, extract +
+      top-2000 SearchByBoW vs the previous frame (cell_guard=empty: the
+      reference throws on 1080p, SURVEY §0.2d);
+  c3  the same extraction without the matcher;
+  c1  640x480, 8 levels, 1000 features (TUM1.yaml), extract + top-1000 match;
+  c2  640x480 single level, 1000 features, extract + top-1000 match;
+  c5  KITTI-shaped 1241x376 stereo pairs: extract left + right,
+      Frame::ComputeStereoMatches, SearchByBoW of every left frame vs its
+      predecessor.
+Frames are the temporally correlated 'pan' stream (orbx/synth.py) so the
+matcher commits hundreds of matches per pair; c5 uses rectified pairs.
 
---workload c5 (BASELINE config 5, not the headline line): KITTI-shaped
-1241x376 rectified stereo pairs; one step = ORBextractor on the left and the
-right frame of every pair, Frame::ComputeStereoMatches on every pair
-(orbs_plan_match) and SearchByBoW of every left frame against its
-predecessor, frames sharded per rank with the same RCCL boundary exchange.
+python bench.py [--gpus N --steps K --warmup W --batch B --workload c4]
+--gpus N > 1 without WORLD_SIZE in the environment starts N rank processes
+(one per GPU, before this process touches the GPU); under torchrun
+(WORLD_SIZE set) each process is one rank.
 """
 import argparse
 import json
 import os
+import platform
+import socket
+import statistics
+import subprocess
 import sys
 import time
 
@@ -35,6 +48,25 @@ sys.path.insert(0, os.path.join(ROOT, "orb-slam-system_amd"))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
+KITTI_FX, KITTI_BF = 718.856, 386.1448
+
+WORKLOADS = {
+    "c4": dict(W=1920, H=1080, nfeatures=2000, nlevels=8, guard="empty", topn=2000, batch=256,
+               match=True, name="BASELINE config 4: 1920x1080 8-level ORBextractor (2000 features, "
+                                "cell_guard=empty) + brute-force SearchByBoW top-2000 vs previous frame"),
+    "c3": dict(W=1920, H=1080, nfeatures=2000, nlevels=8, guard="empty", topn=2000, batch=256,
+               match=False, name="BASELINE config 3: 1920x1080 8-level ORBextractor (2000 features, "
+                                 "cell_guard=empty), no matcher"),
+    "c1": dict(W=640, H=480, nfeatures=1000, nlevels=8, guard="strict", topn=1000, batch=1024,
+               match=True, name="BASELINE config 1 shape on the GPU: 640x480 8-level ORBextractor "
+                                "(1000 features, TUM1.yaml) + brute-force SearchByBoW top-1000 vs "
+                                "previous frame"),
+    "c2": dict(W=640, H=480, nfeatures=1000, nlevels=1, guard="strict", topn=1000, batch=1024,
+               match=True, name="BASELINE config 2: 640x480 single-level FAST-9 + rotated BRIEF "
+                                "(1000 features) + brute-force SearchByBoW top-1000 vs previous frame"),
+    "c5": dict(W=1241, H=376, nfeatures=2000, nlevels=8, guard="strict", topn=2000, batch=256,
+               match=True, name="BASELINE config 5"),
+}
 
 
 def parse():
@@ -42,33 +74,76 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=256, help="frames per GPU per step")
-    ap.add_argument("--width", type=int, default=1920)
-    ap.add_argument("--height", type=int, default=1080)
-    ap.add_argument("--nfeatures", type=int, default=2000)
-    ap.add_argument("--nlevels", type=int, default=8)
-    ap.add_argument("--topn", type=int, default=2000)
-    ap.add_argument("--kind", default="rects")
+    ap.add_argument("--workload", choices=sorted(WORKLOADS), default="c4")
+    ap.add_argument("--batch", type=int, default=0, help="frames per GPU per step (0: workload default)")
+    ap.add_argument("--kind", default="pan", help="synthetic stream (orbx/synth.py)")
     ap.add_argument("--nnratio", type=float, default=0.75)
-    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--cpu-seconds", type=float, default=25.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"))
-    ap.add_argument("--workload", choices=("c4", "c5"), default="c4")
+    ap.add_argument("--no-latency", action="store_true")
+    ap.add_argument("--traffic", default="", help="PMC traffic summary (default profiles/traffic_<workload>.json)")
     a = ap.parse_args()
-    if a.workload == "c5":  # KITTI00-02.yaml: 1241x376, 2000 features, fx 718.856, bf 386.1448
-        a.width, a.height = 1241, 376
-    return a
+    wl = dict(WORKLOADS[a.workload])
+    if a.batch <= 0:
+        a.batch = wl["batch"]
+    if not a.traffic:
+        a.traffic = os.path.join(ROOT, "profiles", "traffic_%s.json" % a.workload)
+    return a, wl
 
 
-KITTI_FX, KITTI_BF = 718.856, 386.1448
+# --------------------------------------------------------------------------- launcher
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
 
 
-def stage_bytes(geo, nframes, kps_total, npairs, topn):
-    """Algorithmic bytes per step of each stage (DESIGN.md §4)."""
+def launch_ranks(n):
+    """Start n rank processes of this script (RANK/LOCAL_RANK/WORLD_SIZE set),
+    wait for all, return the worst exit code.  This process never initialises
+    the GPU (torch.cuda.device_count() does not, on this image)."""
+    import torch
+    ndev = torch.cuda.device_count()
+    if n > ndev:
+        print("bench.py: --gpus %d but only %d GPU(s) visible" % (n, ndev), file=sys.stderr)
+        return 2
+    port = str(_free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
+                                      env=env))
+    rc = 0
+    pending = list(procs)
+    while pending:
+        for p in list(pending):
+            c = p.poll()
+            if c is None:
+                continue
+            pending.remove(p)
+            if c != 0 and rc == 0:
+                rc = c
+                for q in pending:  # one rank failed: the collective would hang
+                    q.terminate()
+        time.sleep(0.05)
+    return rc
+
+
+# --------------------------------------------------------------------------- byte models
+def level_pixels(geo):
     L = geo.nlevels
     w, h, alias = geo.level("width"), geo.level("height"), geo.level("alias")
     P = [w[l] * h[l] for l in range(L)]
     uniq = [l for l in range(L) if alias[l] == l]
+    return P, uniq, alias
+
+
+def stage_bytes(geo, nframes, kps_total, npairs, topn):
+    """Algorithmic bytes per step of each stage (DESIGN.md §4, SURVEY §8d)."""
+    P, uniq, alias = level_pixels(geo)
     resize = sum(P[l] + P[alias[l - 1]] for l in uniq if l > 0)
     fast = sum(P[l] for l in uniq)
     # per keypoint: the 43x43 source patch the IC disk (r=15) and the blurred
@@ -80,127 +155,286 @@ def stage_bytes(geo, nframes, kps_total, npairs, topn):
             "orient_brief": brief, "match_candidates": match}
 
 
-def cpu_baseline(args):
+def min_pyr_fast_bytes(geo, nframes):
+    """Compulsory HBM bytes of the pyramid+FAST pass: read level 0 once,
+    write every other unique level once (FAST could run on tiles in flight)."""
+    P, uniq, _ = level_pixels(geo)
+    return nframes * (P[0] + sum(P[l] for l in uniq if l > 0))
+
+
+def load_traffic(path):
+    if os.path.exists(path):
+        try:  # tools/pmc_traffic.py: corrected FETCH_SIZE*2 + WRITE_SIZE per launch
+            return json.load(open(path))
+        except (OSError, ValueError):
+            return {}
+    return {}
+
+
+def roofline_entries(st, steps, by, geo, B, traffic):
+    per_step = {k: st[k][0] / steps for k in st if st[k][1]}
+    dom = max((k for k in per_step if k in by), key=per_step.get)
+    launches = st[dom][1] / steps
+    ach = by[dom] / (per_step[dom] * 1e-3) / 1e9
+    tr = traffic.get(dom, {}).get("bytes_per_launch")
+    roof = {"bound": "hbm", "kernel": dom, "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
+            "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": tr,
+            "traffic_unit": "HBM bytes per launch (rocprofv3 PMC FETCH_SIZE*2 + WRITE_SIZE, batch %d)" % B,
+            "algorithmic_bytes_per_launch": round(by[dom] / launches),
+            "launches_per_step": launches, "avg_launch_ms": round(per_step[dom] / launches, 5)}
+    # the north-star pass: pyramid + FAST together
+    t = per_step.get("resize", 0.0) + per_step.get("fast_cells", 0.0)
+    pf = None
+    if t > 0:
+        b = by["resize"] + by["fast_cells"]
+        bmin = min_pyr_fast_bytes(geo, B)
+        trs = [traffic.get(k, {}).get("bytes_per_launch") for k in ("resize", "fast_cells")
+               if k in per_step]
+        pf = {"bound": "hbm", "kernels": [k for k in ("resize", "fast_cells") if k in per_step],
+              "ms_per_step": round(t, 5), "algorithmic_bytes_per_step": b,
+              "achieved": round(b / (t * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+              "frac": round(b / (t * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+              "byte_model": "resize reads+writes + FAST reads of every unique level (SURVEY §8d)",
+              "compulsory_bytes_per_step": bmin,
+              "compulsory_frac": round(bmin / (t * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+              "traffic": (sum(trs) if trs and all(x is not None for x in trs) else None)}
+    return per_step, roof, pf
+
+
+# --------------------------------------------------------------------------- CPU baseline
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or "unknown"
+
+
+def _topn_sel(k, topn):
+    order = sorted(range(len(k)), key=lambda i: (-float(k["response"][i]), i))[:topn]
+    return np.sort(np.array(order, np.uint32))
+
+
+def _timed_median(fn, seconds, warm=20, want=256):
+    """BASELINE.md protocol: 20 untimed warm-up frames, then the median of
+    per-frame times over >= 256 frames -- bounded to `seconds` of CPU work
+    (fewer frames at 1080p; the count is reported)."""
+    i = 0
+    t_end = time.perf_counter() + seconds
+    while i < warm and time.perf_counter() < t_end:
+        fn(i)
+        i += 1
+    times = []
+    while len(times) < want and (time.perf_counter() < t_end or len(times) < 3):
+        t0 = time.perf_counter()
+        fn(i)
+        times.append(time.perf_counter() - t0)
+        i += 1
+    return statistics.median(times), len(times), i - len(times)
+
+
+def cpu_baseline(args, wl):
     """Bounded sample of the same workload on the oracle (1 host core)."""
     from oracle import oracle as O
     from orbx import synth
     O.build()
-    ex = O.Extractor(args.nfeatures, 1.2, args.nlevels, 20, 7, cell_guard="empty")
-    t0 = time.perf_counter()
-    prev = None
-    n = 0
-    while True:
-        img = synth.frame(args.width, args.height, n, args.kind)
-        ts = time.perf_counter()
-        k, d = ex.extract(img)
-        order = sorted(range(len(k)), key=lambda i: (-float(k["response"][i]), i))[:args.topn]
-        sel = np.sort(np.array(order, np.uint32))
-        cur = dict(desc=d, angle=k["angle"], valid=None, node_id=np.array([0], np.uint32),
-                   off=np.array([0, len(sel)], np.uint32), feat=sel)
-        if prev is not None:
-            O.search_by_bow(cur, prev, args.nnratio, True)
-        prev = cur
-        n += 1
-        if time.perf_counter() - t0 >= args.cpu_seconds and n >= 3:
-            break
-        del ts
-    el = time.perf_counter() - t0
-    return {"value": n / el, "unit": "frames/s", "cores": 1, "kind": "port",
-            "sample": "%d synthetic %s %dx%d frames, oracle ORBextractor + top-%d single-node "
-                      "SearchByBoW vs previous frame, single thread (scalar restatement)" %
-                      (n, args.kind, args.width, args.height, args.topn)}
+    ex = O.Extractor(wl["nfeatures"], 1.2, wl["nlevels"], 20, 7, cell_guard=wl["guard"])
+    imgs = [synth.frame(wl["W"], wl["H"], i, args.kind) for i in range(17)]
+    state = {"prev": None}
+
+    def one(i):
+        k, d = ex.extract(imgs[i % len(imgs)])
+        if wl["match"]:
+            sel = _topn_sel(k, wl["topn"])
+            cur = dict(desc=d, angle=k["angle"], valid=None, node_id=np.array([0], np.uint32),
+                       off=np.array([0, len(sel)], np.uint32), feat=sel)
+            if state["prev"] is not None:
+                O.search_by_bow(cur, state["prev"], args.nnratio, True)
+            state["prev"] = cur
+
+    med, n, warm = _timed_median(one, args.cpu_seconds)
+    return {"value": round(1.0 / med, 3), "unit": "frames/s", "cores": 1, "kind": "port",
+            "cpu": cpu_model(), "median_ms_per_frame": round(med * 1e3, 3),
+            "sample": "median per-frame time over %d timed frames after %d warm-up (synthetic %s "
+                      "%dx%d, %d levels), oracle ORBextractor%s, single thread (scalar C "
+                      "restatement of the reference, gcc -O2)" %
+                      (n, warm, args.kind, wl["W"], wl["H"], wl["nlevels"],
+                       " + top-%d single-node SearchByBoW vs previous frame" % wl["topn"]
+                       if wl["match"] else "")}
 
 
-def cpu_baseline_c5(args):
-    """Bounded sample of the stereo workload on the oracle (1 host core)."""
+def cpu_baseline_c5(args, wl):
     from oracle import oracle as O
     from orbx import synth
     O.build()
-    el = O.Extractor(args.nfeatures, 1.2, args.nlevels, 20, 7)
-    er = O.Extractor(args.nfeatures, 1.2, args.nlevels, 20, 7)
+    el = O.Extractor(wl["nfeatures"], 1.2, wl["nlevels"], 20, 7)
+    er = O.Extractor(wl["nfeatures"], 1.2, wl["nlevels"], 20, 7)
     t = el.tables()
-    pairs = [synth.stereo_pair(args.width, args.height, i) for i in range(4)]
-    t0 = time.perf_counter()
-    prev = None
-    n = 0
-    while True:
-        L, R = pairs[n % len(pairs)]
+    pairs = [synth.stereo_pair(wl["W"], wl["H"], i) for i in range(8)]
+    state = {"prev": None}
+
+    def one(i):
+        L, R = pairs[i % len(pairs)]
         kl, dl = el.extract(L)
         kr, dr = er.extract(R)
         O.compute_stereo_matches(kl, dl, kr, dr, t["scale"], t["inv_scale"],
-                                 [el.level(l) for l in range(args.nlevels)],
-                                 [er.level(l) for l in range(args.nlevels)],
+                                 [el.level(l) for l in range(wl["nlevels"])],
+                                 [er.level(l) for l in range(wl["nlevels"])],
                                  KITTI_BF / KITTI_FX, KITTI_BF)
-        order = sorted(range(len(kl)), key=lambda i: (-float(kl["response"][i]), i))[:args.topn]
-        sel = np.sort(np.array(order, np.uint32))
+        sel = _topn_sel(kl, wl["topn"])
         cur = dict(desc=dl, angle=kl["angle"], valid=None, node_id=np.array([0], np.uint32),
                    off=np.array([0, len(sel)], np.uint32), feat=sel)
-        if prev is not None:
-            O.search_by_bow(cur, prev, args.nnratio, True)
-        prev = cur
-        n += 1
-        if time.perf_counter() - t0 >= args.cpu_seconds and n >= 3:
-            break
-    el_s = time.perf_counter() - t0
-    return {"value": n / el_s, "unit": "stereo frames/s", "cores": 1, "kind": "port",
-            "sample": "%d synthetic %dx%d stereo pairs, oracle ORBextractor (left + right) + "
+        if state["prev"] is not None:
+            O.search_by_bow(cur, state["prev"], args.nnratio, True)
+        state["prev"] = cur
+
+    med, n, warm = _timed_median(one, args.cpu_seconds)
+    return {"value": round(1.0 / med, 3), "unit": "stereo frames/s", "cores": 1, "kind": "port",
+            "cpu": cpu_model(), "median_ms_per_frame": round(med * 1e3, 3),
+            "sample": "median per-pair time over %d timed pairs after %d warm-up (synthetic "
+                      "%dx%d stereo pairs), oracle ORBextractor (left + right) + "
                       "ComputeStereoMatches + top-%d single-node SearchByBoW vs previous left "
-                      "frame, single thread (scalar restatement)" %
-                      (n, args.width, args.height, args.topn)}
+                      "frame, single thread (scalar C restatement, gcc -O2)" %
+                      (n, warm, wl["W"], wl["H"], wl["topn"])}
 
 
-def main():
-    args = parse()
-    if args.workload == "c5":
-        return main_c5(args)
+# --------------------------------------------------------------------------- drop-in latency
+def _pct(xs, q):
+    xs = sorted(xs)
+    return xs[min(len(xs) - 1, int(round(q / 100.0 * (len(xs) - 1))))]
+
+
+def latency_leg(calls=200, warm=20):
+    """Per-call latency of the drop-in C ABI, one call at a time as Tracking
+    makes it (Frame::ExtractORB -> operator(), Frame.cc:227-233;
+    LoopClosing::ComputeSim3 -> SearchByBoW, LoopClosing.cc:149): host image
+    in, host keypoints/descriptors out, timed around the ctypes call."""
+    import ctypes
+    import orbx
+    from orbx import synth
+    L = orbx.lib()
+    out = {}
+    for tag, (W, H, nf, guard) in (("extract_640x480", (640, 480, 1000, "strict")),
+                                   ("extract_1920x1080", (1920, 1080, 2000, "empty"))):
+        ex = orbx.Extractor(nf, 1.2, 8, 20, 7, guard)
+        imgs = [np.ascontiguousarray(synth.frame(W, H, i, "pan")) for i in range(8)]
+        cap = ctypes.c_int(0)
+        orbx._check(L.orbx_extractor_capacity(ex._h, W, H, ctypes.byref(cap)))
+        kps = np.zeros(cap.value, orbx.KEYPOINT_DTYPE)
+        desc = np.zeros((cap.value, 32), np.uint8)
+        n = ctypes.c_int(0)
+        pk, pd, pn = orbx._p(kps), orbx._p(desc), ctypes.byref(n)
+        ptrs = [orbx._p(im) for im in imgs]
+        ts = []
+        for i in range(warm + calls):
+            t0 = time.perf_counter()
+            rc = L.orbx_extract(ex._h, ptrs[i % 8], W, H, W, pk, cap.value, pd, pn)
+            t1 = time.perf_counter()
+            orbx._check(rc, "orbx_extract")
+            if i >= warm:
+                ts.append((t1 - t0) * 1e6)
+        out[tag] = {"p50_us": round(_pct(ts, 50), 1), "p99_us": round(_pct(ts, 99), 1),
+                    "calls": calls, "keypoints": n.value}
+        del ex
+    # SearchByBoW(KF, KF): 2000 x 2000 in one vocabulary node
+    ex = orbx.Extractor(2000, 1.2, 8, 20, 7, "empty")
+    frames = []
+    for i in range(2):
+        k, d = ex.extract(synth.frame(1920, 1080, 100 + i, "pan"))
+        sel = _topn_sel(k, 2000)
+        frames.append(dict(desc=d, angle=k["angle"], valid=None, node_id=np.array([0], np.uint32),
+                           off=np.array([0, len(sel)], np.uint32), feat=sel))
+    keep = []
+    b1, b2 = orbx._bow_struct(frames[1], keep), orbx._bow_struct(frames[0], keep)
+    m = np.full(b1.n, -1, np.int32)
+    nm = ctypes.c_int(0)
+    ts = []
+    for i in range(warm + calls):
+        t0 = time.perf_counter()
+        rc = L.orbm_search_by_bow(ctypes.byref(b1), ctypes.byref(b2), 0.75, 1, 0, orbx._p(m),
+                                  ctypes.byref(nm))
+        t1 = time.perf_counter()
+        orbx._check(rc, "orbm_search_by_bow")
+        if i >= warm:
+            ts.append((t1 - t0) * 1e6)
+    out["search_by_bow_2000x2000"] = {"p50_us": round(_pct(ts, 50), 1),
+                                      "p99_us": round(_pct(ts, 99), 1), "calls": calls,
+                                      "features": [int(b1.n), int(b2.n)], "matches": nm.value}
+    out["note"] = ("one synchronous C-ABI call at a time from the host (image H2D, kernels, "
+                   "results D2H), timed around the call; the throughput line above is the "
+                   "batched device-resident path")
+    return out
+
+
+# --------------------------------------------------------------------------- distributed
+def dist_setup(args):
     import torch
     import torch.distributed as dist
-    import orbx
-    from orbx.dist import BoundaryExchange, shard_first_frame
-
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and not (world == 1 and args.gpus == 1):
+        raise SystemExit("bench.py: WORLD_SIZE=%d but --gpus %d" % (world, args.gpus))
+    torch.cuda.set_device(local)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    else:
-        torch.cuda.set_device(local)
+    return torch, dist, world, rank, local
+
+
+def finish_time(torch, dist, world, dev, el):
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    return el
+
+
+# --------------------------------------------------------------------------- mono workloads
+def main_mono(args, wl):
+    torch, dist, world, rank, local = dist_setup(args)
+    import orbx
+    from orbx.dist import BoundaryExchange, shard_first_frame
+
     dev = torch.device("cuda", local)
-    B, W, H = args.batch, args.width, args.height
-    prm = orbx.params(args.nfeatures, 1.2, args.nlevels, 20, 7, "empty")
+    B, W, H = args.batch, wl["W"], wl["H"]
+    prm = orbx.params(wl["nfeatures"], 1.2, wl["nlevels"], 20, 7, wl["guard"])
     plan = orbx.Plan(prm, W, H, B, device=local)
     kcap = plan.kcap
-    mp = orbx.MatchPlan(B, kcap, args.topn, device=local)
+    match = wl["match"]
+    mp = orbx.MatchPlan(B, kcap, wl["topn"], device=local) if match else None
     frames = torch.empty((B, H, W), dtype=torch.uint8, device=dev)
     orbx.synth_frames(frames, shard_first_frame(rank, B), args.kind)
     # frame slots: 0 = the frame preceding this batch, 1..B = this batch
     kps = torch.zeros((B + 1, kcap, 28), dtype=torch.uint8, device=dev)
     desc = torch.zeros((B + 1, kcap, 32), dtype=torch.uint8, device=dev)
     counts = torch.zeros(B + 1, dtype=torch.int32, device=dev)
-    xch = BoundaryExchange(kcap, world, dev)
+    xch = BoundaryExchange(kcap, world, dev) if match else None
 
     def step():
         # slot 0 <- the predecessor of this step's first frame: on 1 GPU the
         # previous step's last frame; frame-sharded over N GPUs the previous
         # rank's last frame of this step, via an RCCL all-gather (orbx.dist)
-        if world == 1:
+        if match and world == 1:
             kps[0].copy_(kps[B])
             desc[0].copy_(desc[B])
             counts[0:1].copy_(counts[B:B + 1])
         plan.extract(frames, out=(kps[1:], desc[1:], counts[1:]))
-        if world > 1:
-            xch.ring_step(dist, rank, (kps[B], desc[B], counts[B:B + 1]),
-                          (kps[0], desc[0], counts[0:1]))
-        mp.match(B, kps[1:], desc[1:], counts[1:], kps, desc, counts, args.nnratio, True)
+        if match:
+            if world > 1:
+                xch.ring_step(dist, rank, (kps[B], desc[B], counts[B:B + 1]),
+                              (kps[0], desc[0], counts[0:1]))
+            mp.match(B, kps[1:], desc[1:], counts[1:], kps, desc, counts, args.nnratio, True)
 
     for _ in range(args.warmup):
         step()
     plan.check()
     torch.cuda.synchronize()
     plan.set_timing(True)
-    mp.set_timing(True)
+    if mp:
+        mp.set_timing(True)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -213,46 +447,28 @@ def main():
     el = time.perf_counter() - t0
     plan.check()
     st = plan.stage_times()
-    mst = mp.stage_times()
-    for k, v in mst.items():
-        if v[1]:
-            st[k] = v
-    if world > 1:
-        t = torch.tensor([el], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
+    if mp:
+        for k, v in mp.stage_times().items():
+            if v[1]:
+                st[k] = v
+    el = finish_time(torch, dist, world, dev, el)
     kps_total = int(counts[1:].sum().item())
-    nmatch = int(mp.nmatches[:B].sum().item())
+    nmatch = int(mp.nmatches[:B].sum().item()) if mp else 0
     if rank != 0:
         if world > 1:
             dist.destroy_process_group()
         return
-    frames_total = world * B * args.steps
     geo = plan.geo
-    by = stage_bytes(geo, B, kps_total, B, args.topn)
-    per_step = {k: st[k][0] / args.steps for k in st if st[k][1]}
-    dom = max(per_step, key=per_step.get)
-    dom_launches = st[dom][1] / args.steps
-    roof = None
-    if dom in by:
-        ach = by[dom] / (per_step[dom] * 1e-3) / 1e9
-        traffic = None
-        if os.path.exists(args.traffic):
-            try:  # tools/pmc_traffic.py: corrected FETCH_SIZE+WRITE_SIZE per launch
-                ent = json.load(open(args.traffic)).get(dom)
-                traffic = ent["bytes_per_launch"] if ent else None
-            except (OSError, ValueError, KeyError):
-                traffic = None
-        roof = {"bound": "hbm", "kernel": dom, "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
-                "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
-                "traffic_unit": "HBM bytes per launch (rocprofv3 PMC, batch %d)" % B,
-                "algorithmic_bytes_per_launch": round(by[dom] / dom_launches),
-                "launches_per_step": dom_launches,
-                "avg_launch_ms": round(per_step[dom] / dom_launches, 5)}
+    by = stage_bytes(geo, B, kps_total, B, wl["topn"])
+    traffic = load_traffic(args.traffic)
+    per_step, roof, pf = roofline_entries(st, args.steps, by, geo, B, traffic)
+    unit = "frames/s"
+    metric = "ORB extract%s frames/sec at %dx%d, %d pyramid level%s" % (
+        "+match" if match else "", W, H, wl["nlevels"], "s" if wl["nlevels"] > 1 else "")
     out = {
-        "metric": "ORB extract+match frames/sec at %dx%d, %d pyramid levels" % (W, H, args.nlevels),
-        "value": round(frames_total / el, 2),
-        "unit": "frames/s",
+        "metric": metric,
+        "value": round(world * B * args.steps / el, 2),
+        "unit": unit,
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
@@ -261,46 +477,39 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "u8",
-        "data": "synthetic (orbx/synth.py '%s' frames, seeds 0x5EED0000+idx), resident in HBM" % args.kind,
-        "config": {"workload": "BASELINE config 4: %dx%d %d-level ORBextractor (%d features, "
-                               "cell_guard=empty) + brute-force SearchByBoW top-%d vs previous "
-                               "frame" % (W, H, args.nlevels, args.nfeatures, args.topn),
-                   "frames_per_gpu_per_step": B, "parallelism": "frame-sharded dp%d" % world,
-                   "keypoints_last_batch": kps_total, "matches_last_batch": nmatch},
+        "data": "synthetic (orbx/synth.py '%s' stream, seeds 0x5EED0000+idx), resident in HBM" % args.kind,
+        "config": {"workload": wl["name"], "frames_per_gpu_per_step": B,
+                   "parallelism": "frame-sharded dp%d" % world,
+                   "keypoints_last_batch": kps_total, "matches_last_batch": nmatch,
+                   "matches_per_pair": round(nmatch / B, 1)},
         "stages_ms_per_step": {k: round(v, 4) for k, v in per_step.items()},
         "roofline": roof,
+        "roofline_pyr_fast": pf,
     }
+    if world == 1 and not args.no_latency and args.workload == "c4":
+        out["latency"] = latency_leg()
     if world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(args)
-    print(json.dumps(out))
+        out["cpu_baseline"] = cpu_baseline(args, wl)
+    print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
 
 
-def main_c5(args):
-    import torch
-    import torch.distributed as dist
+# --------------------------------------------------------------------------- stereo (c5)
+def main_c5(args, wl):
+    torch, dist, world, rank, local = dist_setup(args)
     import orbx
     from orbx import synth
     from orbx.dist import BoundaryExchange
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    else:
-        torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    B, W, H = args.batch, args.width, args.height
-    prm = orbx.params(args.nfeatures, 1.2, args.nlevels, 20, 7)
+    B, W, H = args.batch, wl["W"], wl["H"]
+    prm = orbx.params(wl["nfeatures"], 1.2, wl["nlevels"], 20, 7)
     pl = orbx.Plan(prm, W, H, B, device=local)
     pr = orbx.Plan(prm, W, H, B, device=local)
     sp = orbx.StereoPlan(pl, device=local)
     kcap = pl.kcap
-    mp = orbx.MatchPlan(B, kcap, args.topn, device=local)
+    mp = orbx.MatchPlan(B, kcap, wl["topn"], device=local)
     # 16 distinct synthetic pairs (numpy spec), tiled over the batch
     npairs = min(16, B)
     first = rank * B
@@ -352,10 +561,7 @@ def main_c5(args):
             if v[1]:
                 a = st.get(k, (0.0, 0))
                 st[k] = (a[0] + v[0], a[1] + v[1])
-    if world > 1:
-        t = torch.tensor([el], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
+    el = finish_time(torch, dist, world, dev, el)
     kps_total = int(counts[1:].sum().item()) + int(pr.counts[:B].sum().item())
     nstereo = int(sp.nmatches[:B].sum().item())
     nmatch = int(mp.nmatches[:B].sum().item())
@@ -363,21 +569,12 @@ def main_c5(args):
         if world > 1:
             dist.destroy_process_group()
         return
-    by = stage_bytes(pl.geo, 2 * B, kps_total, B, args.topn)
-    per_step = {k: st[k][0] / args.steps for k in st}
-    dom = max(per_step, key=per_step.get)
-    dom_launches = st[dom][1] / args.steps
-    roof = None
-    if dom in by:
-        ach = by[dom] / (per_step[dom] * 1e-3) / 1e9
-        roof = {"bound": "hbm", "kernel": dom, "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
-                "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
-                "algorithmic_bytes_per_launch": round(by[dom] / dom_launches),
-                "launches_per_step": dom_launches,
-                "avg_launch_ms": round(per_step[dom] / dom_launches, 5)}
+    by = stage_bytes(pl.geo, 2 * B, kps_total, B, wl["topn"])
+    traffic = load_traffic(args.traffic)
+    per_step, roof, pf = roofline_entries(st, args.steps, by, pl.geo, 2 * B, traffic)
     out = {
         "metric": "ORB stereo extract+match frames/sec at %dx%d (KITTI-shaped), %d pyramid levels"
-                  % (W, H, args.nlevels),
+                  % (W, H, wl["nlevels"]),
         "value": round(world * B * args.steps / el, 2),
         "unit": "stereo frames/s",
         "n_gpus": world,
@@ -393,19 +590,29 @@ def main_c5(args):
         "config": {"workload": "BASELINE config 5: %dx%d stereo pairs, ORBextractor left+right "
                                "(%d features, %d levels), ComputeStereoMatches (fx %.3f, bf %.4f),"
                                " SearchByBoW top-%d vs previous left frame"
-                               % (W, H, args.nfeatures, args.nlevels, KITTI_FX, KITTI_BF,
-                                  args.topn),
+                               % (W, H, wl["nfeatures"], wl["nlevels"], KITTI_FX, KITTI_BF,
+                                  wl["topn"]),
                    "pairs_per_gpu_per_step": B, "parallelism": "frame-sharded dp%d" % world,
                    "keypoints_last_batch": kps_total, "stereo_matches_last_batch": nstereo,
                    "bow_matches_last_batch": nmatch},
         "stages_ms_per_step": {k: round(v, 4) for k, v in per_step.items()},
         "roofline": roof,
+        "roofline_pyr_fast": pf,
     }
     if world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline_c5(args)
-    print(json.dumps(out))
+        out["cpu_baseline"] = cpu_baseline_c5(args, wl)
+    print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def main():
+    args, wl = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus))
+    if args.workload == "c5":
+        return main_c5(args, wl)
+    return main_mono(args, wl)
 
 
 if __name__ == "__main__":

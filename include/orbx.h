@@ -150,7 +150,7 @@ int orbx_plan_set_timing(orbx_plan* plan, int enable); /* also resets the accumu
 /* after the stream is synchronised: total ms and launch count per stage */
 int orbx_plan_stage_times(orbx_plan* plan, double* ms, int* launches, int nstages);
 
-/* Device synthetic frames (same bytes as orbx/synth.py): kind 0 rects,
+/* Device synthetic frames (same bytes as orbx/synth.py): kind 0 rects, 3 pan,
  * 1 noise, 2 flat; frame i gets seed 0x5EED0000 + first_idx + i. */
 int orbx_synth_frames(uint8_t* d_frames, int width, int height, size_t frame_stride, int nframes,
                       int first_idx, int kind, void* stream);

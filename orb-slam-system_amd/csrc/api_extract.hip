@@ -339,7 +339,7 @@ extern "C" int orbx_plan_check(orbx_plan* p, void* stream) {
 
 extern "C" int orbx_synth_frames(uint8_t* d_frames, int W, int H, size_t fstride, int nframes,
                                  int first_idx, int kind, void* stream) {
-  if (!d_frames || W <= 0 || H <= 0 || nframes < 1 || kind < 0 || kind > 2 ||
+  if (!d_frames || W <= 0 || H <= 0 || nframes < 1 || kind < 0 || kind > 3 ||
       fstride < (size_t)W * H)
     return ORBX_ERR_ARG;
   const long long npx = (long long)W * H;

@@ -1204,9 +1204,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OB_WPE))) v
   // BRIEF (:57-73) on GaussianBlur(7x7, sigma 2) evaluated at each sample:
   // out = (sum_j k_j * (sum_i k_i p) + 32768) >> 16, rows via v_dot4_u32_u8
   const uint32_t K0 = 18u | (34u << 8) | (48u << 16) | (56u << 24), K1 = 48u | (34u << 8) | (18u << 16);
+  // Only pairs 0..181 carry information: the reference table has 728
+  // initialisers (ORBextractor.cc:75-113), so pairs 182..255 are {0,0,0,0},
+  // compare the centre with itself and give 0 bits.  Rounds of 64 pairs
+  // needed: 3 (pairs 182..191 of round 2 still evaluate to 0); round 3
+  // (bytes 24..31) is the constant 0 and is not evaluated.
+  static_assert(ORBX_BRIEF_INITIALISED_INTS <= 3 * 64 * 4,
+                "pattern has live pairs past 191: evaluate all four rounds");
   uint64_t words[4] = {0, 0, 0, 0};
 #pragma unroll
-  for (int rr = 0; rr < 4; ++rr) {
+  for (int rr = 0; rr < 3; ++rr) {
     const uint32_t pw = spat[lane + 64 * rr];
     int t[2];
 #pragma unroll
@@ -1274,14 +1281,22 @@ __device__ __forceinline__ uint64_t sm_at(uint64_t seed, uint64_t i) {
   return sm_mix(seed + (i + 1) * 0x9E3779B97F4A7C15ull);
 }
 
+#define ORBX_PAN_CLIP 16
+#define ORBX_PAN_STEP 2
 __global__ __launch_bounds__(256) void k_synth(uint8_t* __restrict__ frames, int W, int H,
                                                size_t fstride, int first_idx, int kind) {
   __shared__ int rect[96][5];
   const int f = blockIdx.y, tid = threadIdx.x;
-  const uint64_t seed = 0x5EED0000ull + (uint64_t)(first_idx + f);
-  if (kind == 0) {
+  const int fidx = first_idx + f;
+  const uint64_t seed = 0x5EED0000ull + (uint64_t)fidx;
+  // kind 3 (pan): the rectangles of the clip's first frame (clips of
+  // ORBX_PAN_CLIP frames) shifted right by ORBX_PAN_STEP px per frame
+  const int phase = kind == 3 ? fidx % ORBX_PAN_CLIP : 0;
+  const uint64_t rseed = seed - (uint64_t)phase;
+  const int shift = ORBX_PAN_STEP * phase;
+  if (kind == 0 || kind == 3) {
     for (int i = tid; i < 96 * 5; i += 256) {
-      const uint64_t v = sm_at(seed, (uint64_t)i);
+      const uint64_t v = sm_at(rseed, (uint64_t)i);
       const int r = i / 5, c = i - r * 5;
       const uint64_t m = (c == 0 || c == 1) ? (uint64_t)W : (c == 4) ? 256ull : (uint64_t)H;
       rect[r][c] = (int)(v % m);
@@ -1301,7 +1316,7 @@ __global__ __launch_bounds__(256) void k_synth(uint8_t* __restrict__ frames, int
     } else {
       v = 64 + (128 * x) / (W > 1 ? W - 1 : 1);
       for (int r = 0; r < 96; ++r) {
-        const int xa = min(rect[r][0], rect[r][1]), xb = max(rect[r][0], rect[r][1]);
+        const int xa = min(rect[r][0], rect[r][1]) + shift, xb = max(rect[r][0], rect[r][1]) + shift;
         const int ya = min(rect[r][2], rect[r][3]), yb = max(rect[r][2], rect[r][3]);
         if (x >= xa && x <= xb && y >= ya && y <= yb) v = rect[r][4];
       }

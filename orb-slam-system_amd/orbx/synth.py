@@ -9,6 +9,11 @@ kinds:
          (stream elements 5r..5r+4: x0, x1, y0, y1 mod W/H, value mod 256; later
          rectangles overwrite earlier ones; corners inclusive), then additive
          noise U{-6..6} (element 480 + y*W + x, mod 13, minus 6), clamped.
+  pan    temporally correlated stream: frame t shows the rectangles of
+         rects frame t - t % 16 (the clip's first frame) shifted right by
+         2 * (t % 16) px (clipped at the right edge), over the same
+         gradient, with frame t's own noise -- consecutive frames share most
+         corners, so SearchByBoW commits hundreds of matches per pair.
   noise  iid U{0..255} (element y*W + x, mod 256).
   flat   constant 128.
 
@@ -21,7 +26,8 @@ GOLDEN = np.uint64(0x9E3779B97F4A7C15)
 M1 = np.uint64(0xBF58476D1CE4E5B9)
 M2 = np.uint64(0x94D049BB133111EB)
 SEED_BASE = 0x5EED0000
-KINDS = {"rects": 0, "noise": 1, "flat": 2}
+KINDS = {"rects": 0, "noise": 1, "flat": 2, "pan": 3}
+PAN_CLIP, PAN_STEP = 16, 2
 
 
 def _mix(z):
@@ -44,16 +50,20 @@ def frame(w, h, frame_idx, kind="rects"):
         return np.full((h, w), 128, np.uint8)
     if kind == "noise":
         return (stream(seed, 0, w * h) % np.uint64(256)).astype(np.uint8).reshape(h, w)
-    if kind != "rects":
+    if kind not in ("rects", "pan"):
         raise ValueError(kind)
+    phase = frame_idx % PAN_CLIP if kind == "pan" else 0
+    shift = PAN_STEP * phase
     x = np.arange(w, dtype=np.int64)
     bg = 64 + (128 * x) // max(w - 1, 1)
     img = np.broadcast_to(bg, (h, w)).astype(np.int32).copy()
-    r = stream(seed, 0, 5 * 96).reshape(96, 5)
+    r = stream(seed - phase, 0, 5 * 96).reshape(96, 5)
     for x0, x1, y0, y1, v in r:
         x0, x1 = int(x0 % np.uint64(w)), int(x1 % np.uint64(w))
         y0, y1 = int(y0 % np.uint64(h)), int(y1 % np.uint64(h))
-        img[min(y0, y1):max(y0, y1) + 1, min(x0, x1):max(x0, x1) + 1] = int(v % np.uint64(256))
+        xa = min(x0, x1) + shift
+        if xa < w:
+            img[min(y0, y1):max(y0, y1) + 1, xa:max(x0, x1) + shift + 1] = int(v % np.uint64(256))
     noise = (stream(seed, 480, w * h) % np.uint64(13)).astype(np.int32).reshape(h, w) - 6
     return np.clip(img + noise, 0, 255).astype(np.uint8)
 

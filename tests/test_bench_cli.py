@@ -1,0 +1,31 @@
+"""bench.py contract checks that need no GPU."""
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_gpus_beyond_visible_devices_fails_loudly():
+    # --gpus N without WORLD_SIZE starts N ranks; with fewer GPUs visible it
+    # must exit non-zero before touching any device (no silent 1-GPU run)
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["HIP_VISIBLE_DEVICES"] = ""  # none visible, also on a GPU box
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "64"],
+                       env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode != 0
+    assert "GPU(s) visible" in r.stderr
+
+
+def test_bench_byte_models():
+    sys.path.insert(0, ROOT)
+    import bench
+    import orbx
+    geo = orbx.geometry(orbx.params(2000, 1.2, 8, 20, 7, "empty"), 1920, 1080)
+    by = bench.stage_bytes(geo, 1, 0, 0, 2000)
+    # B_pyr+FAST at 1080p / 8 levels counts level 1 (= level 0,
+    # partial_sum quirk) as its own level; orbx aliases it, so FAST reads and
+    # resize moves only the unique levels
+    P = [w * h for w, h in zip(geo.level("width"), geo.level("height"))]
+    assert by["fast_cells"] == sum(P) - P[1]
+    assert bench.min_pyr_fast_bytes(geo, 1) == sum(P) - P[1]

@@ -81,11 +81,12 @@ def test_strict_guard_1080p_raises(gpu):
 
 def test_synth_device_matches_numpy(gpu):
     import torch
-    for kind in ("rects", "noise", "flat"):
+    for kind in ("rects", "noise", "flat", "pan"):
         t = torch.empty((3, 376, 1241), dtype=torch.uint8, device="cuda")
-        gpu.synth_frames(t, 10, kind)
+        first = 29 if kind == "pan" else 10  # pan: crosses a clip boundary (frame 32)
+        gpu.synth_frames(t, first, kind)
         torch.cuda.synchronize()
-        ref = synth.frames(1241, 376, 10, 3, kind)
+        ref = synth.frames(1241, 376, first, 3, kind)
         assert np.array_equal(t.cpu().numpy(), ref), kind
 
 
@@ -192,14 +193,20 @@ def _topn_bow(k, d, topn):
                 node_id=np.array([0], np.uint32), off=np.array([0, len(sel)], np.uint32), feat=sel)
 
 
-@pytest.mark.parametrize("W,H,nf,kind", [(640, 480, 1000, "noise"), (1920, 1080, 2000, "rects")])
-def test_match_plan_matches_oracle(gpu, oracle, W, H, nf, kind):
+@pytest.mark.parametrize("W,H,nf,kind,first", [(640, 480, 1000, "noise", 40),
+                                                (1920, 1080, 2000, "rects", 40),
+                                                (640, 480, 1000, "pan", 40),
+                                                (1920, 1080, 2000, "pan", 45)])
+def test_match_plan_matches_oracle(gpu, oracle, W, H, nf, kind, first):
+    """Batched SearchByBoW of consecutive frames; 'pan' frames are temporally
+    correlated, so hundreds of matches per pair go through the serial
+    vbMatched2 resolver (and frame 48 starts a new clip)."""
     import torch
     B = 4
     guard = "empty" if W == 1920 else "strict"
     prm = gpu.params(nf, 1.2, 8, 20, 7, guard)
     plan = gpu.Plan(prm, W, H, B)
-    frames = torch.from_numpy(synth.frames(W, H, 40, B, kind)).cuda()
+    frames = torch.from_numpy(synth.frames(W, H, first, B, kind)).cuda()
     plan.extract(frames)
     mp = gpu.MatchPlan(B - 1, plan.kcap, topn=nf)
     mp.match(B - 1, plan.kps[1:], plan.desc[1:], plan.counts[1:], plan.kps, plan.desc,
@@ -214,6 +221,8 @@ def test_match_plan_matches_oracle(gpu, oracle, W, H, nf, kind):
         rm, rnm = oracle.search_by_bow(_topn_bow(ka, da, nf), _topn_bow(kb, db, nf), 0.75, True)
         assert nm[p] == rnm
         assert np.array_equal(m12[p, :len(ka)], rm)
+    if kind == "pan":
+        assert int(nm[0]) >= 100, nm  # the resolver is exercised at real density
 
 
 @pytest.mark.parametrize("seed", range(3))
