@@ -132,7 +132,8 @@ int orbx_plan_geometry(const orbx_plan* plan, orbx_geometry* g);
 /* d_frames: nframes images, frame i at d_frames + i*frame_stride, rows of
  * row_stride bytes (device memory; any byte alignment -- 16-B aligned rows
  * take the fastest staging path; no byte outside a frame's row_stride x
- * height bytes is read).  Outputs (device memory):
+ * height bytes is read; row_stride < 2^24, else ORBX_ERR_UNSUPPORTED: the
+ * kernels form row offsets with 24-bit multiplies).  Outputs (device memory):
  *   d_kps  [nframes][kcap], d_desc [nframes][kcap][32], d_counts [nframes].
  * Asynchronous on `stream` (a hipStream_t; NULL = the default stream).
  * Device-side failures (quadtree stuck) are latched; read them with
@@ -199,7 +200,10 @@ int orbm_descriptor_distance_batch(const uint8_t* a, int na, const uint8_t* b, i
  * keypoint index in frame B or -1.  Frame p of side A is d_kps_a + p*kcap,
  * d_desc_a + p*kcap*32, d_count_a[p] (side B likewise), i.e. the layout of
  * orbx_plan_extract outputs; d_match12 is [npairs][kcap], d_nmatches
- * [npairs].  Asynchronous on `stream`. */
+ * [npairs].  Asynchronous on `stream`.  The descriptors must be
+ * orbx_plan_extract outputs: their bytes 24..31 are zero (the reference's
+ * 728-entry BRIEF pattern), which the candidate kernel relies on to skip
+ * those two dwords; orbm_search_by_bow takes arbitrary descriptors. */
 typedef struct orbm_plan orbm_plan;
 int orbm_plan_create(int max_pairs, int kcap, int topn, int device, orbm_plan** out);
 int orbm_plan_destroy(orbm_plan* mp);

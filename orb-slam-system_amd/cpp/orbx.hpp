@@ -164,13 +164,19 @@ class ORBmatcher {
   explicit ORBmatcher(float nnratio = 0.6f, bool checkOri = true, int device = 0)
       : mfNNratio(nnratio), mbCheckOrientation(checkOri), device_(device) {}
 
-  // DescriptorDistance (ORBmatcher.cc:896-908), evaluated on the device.
-  // Bulk callers should use DescriptorDistances().
-  int DescriptorDistance(const uint8_t* a, const uint8_t* b) const {
-    int32_t z = 0, d = 0;
-    check(orbm_descriptor_distance_batch(a, 1, b, 1, &z, &z, 1, device_, &d),
-          "DescriptorDistance");
-    return d;
+  // DescriptorDistance (ORBmatcher.cc:896-908): exact host popcount of the
+  // 8 dwords -- the reference calls it per pair inside CPU loops
+  // (Frame.cc:521, MapPoint.cc:252), where a device round trip per pair
+  // would cost more than it saves.  Bulk callers use DescriptorDistances().
+  static int DescriptorDistance(const uint8_t* a, const uint8_t* b) {
+    int dist = 0;
+    for (int i = 0; i < 8; ++i) {
+      uint32_t va, vb;
+      memcpy(&va, a + 4 * i, 4);
+      memcpy(&vb, b + 4 * i, 4);
+      dist += __builtin_popcount(va ^ vb);
+    }
+    return dist;
   }
   std::vector<int32_t> DescriptorDistances(const uint8_t* a, int na, const uint8_t* b, int nb,
                                            const std::vector<int32_t>& ia,

@@ -39,6 +39,10 @@ struct orbv_vocab {
   int* d_err = nullptr;
   BowRes* d_res = nullptr;
   size_t res_cap = 0;
+  /* outgrown d_res buffers: launches on callers' streams may still read
+   * them, so they are freed with the vocabulary, not on growth (no device
+   * synchronisation on the transform path) */
+  std::vector<void*> retired;
   /* host drop-in staging (one frame) */
   uint8_t* d_desc1 = nullptr;
   int* d_cnt1 = nullptr;
@@ -56,6 +60,7 @@ static void vocab_free(orbv_vocab* v) {
                   v->d_desc1, v->d_cnt1, v->d_bw, v->d_fn, v->d_fo, v->d_ff, v->d_bv, v->d_n2};
   for (void* b : bufs)
     if (b) hipFree(b);
+  for (void* b : v->retired) hipFree(b);
   if (v->stream) hipStreamDestroy(v->stream);
   delete v;
 }
@@ -242,9 +247,7 @@ extern "C" int orbv_transform_batch(orbv_vocab* v, int nframes, const uint8_t* d
   hipStream_t s = (hipStream_t)stream;
   const size_t need = (size_t)nframes * kcap;
   if (need > v->res_cap) {
-    ORBX_TRY(hipStreamSynchronize(s));
-    ORBX_TRY(hipDeviceSynchronize());
-    if (v->d_res) hipFree(v->d_res);
+    if (v->d_res) v->retired.push_back(v->d_res);
     v->d_res = nullptr;
     v->res_cap = 0;
     ORBX_TRY(hipMalloc((void**)&v->d_res, need * sizeof(BowRes)));
@@ -332,6 +335,7 @@ extern "C" int orbv_transform(orbv_vocab* v, const uint8_t* desc, int n, int lev
   int nfeat = 0;
   ORBX_TRY(hipMemcpyAsync(&nfeat, v->d_fo + cnts[1], 4, hipMemcpyDeviceToHost, s));
   ORBX_TRY(hipStreamSynchronize(s));
-  ORBX_TRY(hipMemcpy(fv_feat, v->d_ff, (size_t)nfeat * 4, hipMemcpyDeviceToHost));
+  ORBX_TRY(hipMemcpyAsync(fv_feat, v->d_ff, (size_t)nfeat * 4, hipMemcpyDeviceToHost, s));
+  ORBX_TRY(hipStreamSynchronize(s));
   return ORBX_OK;
 }

@@ -96,6 +96,56 @@ struct StageTimer {
   }
 };
 
+// ---------------------------------------------------------------------------
+// Per-call workspaces of the synchronous drop-in entry points
+// (orbm_search_by_bow, orbm_descriptor_distance_batch,
+// orbm_search_by_projection, ...): a grow-only device arena, a grow-only
+// pinned host staging buffer and a non-blocking stream.  Workspaces live in a
+// per-device pool: a call takes one (a concurrent call takes another, so the
+// entry points stay re-entrant from the Tracking / LocalMapping /
+// LoopClosing threads) and returns it; steady-state calls do no hipMalloc,
+// hipFree or stream creation, and never synchronise the device.
+// ---------------------------------------------------------------------------
+struct CallWs {
+  int device = -1;
+  hipStream_t stream = nullptr;
+  uint8_t* d = nullptr;  // device arena
+  size_t dcap = 0;
+  uint8_t* h = nullptr;  // pinned host staging
+  size_t hcap = 0;
+  // grow-only; a grow waits for this workspace's stream only
+  int reserve(size_t dbytes, size_t hbytes);
+};
+
+// arena carving: 256-B aligned offsets
+struct Carve {
+  size_t off = 0;
+  size_t take(size_t bytes) {
+    const size_t o = off;
+    off += (bytes + 255) & ~(size_t)255;
+    return o;
+  }
+};
+
+CallWs* ws_acquire(int device);  // after hipSetDevice(device); nullptr on failure
+void ws_release(CallWs* w);
+
+// RAII lease of a pooled workspace
+struct WsLease {
+  CallWs* w;
+  explicit WsLease(int device) : w(ws_acquire(device)) {}
+  ~WsLease() {
+    if (w) ws_release(w);
+  }
+  WsLease(const WsLease&) = delete;
+  WsLease& operator=(const WsLease&) = delete;
+};
+
+// hipFuncAttributeMaxDynamicSharedMemorySize is process-wide per kernel:
+// set it once per (kernel, device) to the CU's whole LDS, never per call (a
+// concurrent call writing a smaller value could undercut a larger launch).
+int set_max_dynamic_lds(const void* kernel, int device);
+
 }  // namespace orbx
 
 #endif

@@ -126,15 +126,18 @@ static void plan_free(orbx_plan* p) {
   for (void* b : bufs)
     if (b) hipFree(b);
   p->timer.release();
+  if (p->h_err) hipHostFree(p->h_err);
   if (p->stream) hipStreamDestroy(p->stream);
   delete p;
 }
 
+// stream-ordered upload (the host vectors outlive the plan_create call,
+// which ends with a synchronisation of this stream only)
 template <typename T>
-static int upload(T** dst, const std::vector<T>& v) {
+static int upload(T** dst, const std::vector<T>& v, hipStream_t s) {
   size_t n = v.size() ? v.size() : 1;
   if (hipMalloc((void**)dst, n * sizeof(T)) != hipSuccess) return ORBX_ERR_HIP;
-  if (v.size() && hipMemcpy(*dst, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice) != hipSuccess)
+  if (v.size() && hipMemcpyAsync(*dst, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice, s) != hipSuccess)
     return ORBX_ERR_HIP;
   return ORBX_OK;
 }
@@ -162,9 +165,11 @@ extern "C" int orbx_plan_create(const orbx_params* prm, int width, int height, i
   // quadtree LDS: cell offsets + 12 int arrays of qt_smax (see k_quadtree)
   p->qt_lds = sizeof(int) * ((size_t)P.qt_max_cells + 1 + 12 * (size_t)P.qt_smax);
   if (p->qt_lds > 150 * 1024) { plan_free(p); return ORBX_ERR_UNSUPPORTED; }
-  if (hipFuncSetAttribute((const void*)k_quadtree, hipFuncAttributeMaxDynamicSharedMemorySize,
-                          (int)p->qt_lds) != hipSuccess) { plan_free(p); return ORBX_ERR_HIP; }
-  if (hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking) != hipSuccess) { plan_free(p); return ORBX_ERR_HIP; }
+  if (set_max_dynamic_lds((const void*)k_quadtree, device) ||
+      set_max_dynamic_lds((const void*)k_fast_strips, device) ||
+      set_max_dynamic_lds((const void*)k_pyramid, device)) { plan_free(p); return ORBX_ERR_HIP; }
+  if (hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipHostMalloc((void**)&p->h_err, 64, hipHostMallocDefault) != hipSuccess) { plan_free(p); return ORBX_ERR_HIP; }
   memset(&p->bargs, 0, sizeof(p->bargs));
   // IC_Angle row extents (ORBextractor.cc:28-45): the centre row spans
   // [-15, 15], row v spans [-umax[|v|], umax[|v|]]
@@ -208,15 +213,14 @@ extern "C" int orbx_plan_create(const orbx_params* prm, int width, int height, i
     p->fs_lds += FS_LDS_PAD;
 #endif
     if (p->fs_lds > 150 * 1024) { plan_free(p); return ORBX_ERR_UNSUPPORTED; }
-    if (hipFuncSetAttribute((const void*)k_fast_strips, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)p->fs_lds) != hipSuccess) { plan_free(p); return ORBX_ERR_HIP; }
   }
-  if (upload(&p->d_lv, P.levels) || upload(&p->d_cells, P.cells) || upload(&p->d_strips, P.strips) ||
-      upload(&p->d_xofs, P.xofs) ||
-      upload(&p->d_xofs1, P.xofs1) || upload(&p->d_yofs, P.yofs) || upload(&p->d_alpha, P.alpha) ||
-      upload(&p->d_beta, P.beta) ||
-      upload(&p->d_pyr_xs, P.pyr_xs) || upload(&p->d_pyr_ys, P.pyr_ys) ||
-      upload(&p->d_pyr_bo, P.pyr_bo) || upload(&p->d_pyr_blob, P.pyr_blob)) {
+  hipStream_t us = p->stream;
+  if (upload(&p->d_lv, P.levels, us) || upload(&p->d_cells, P.cells, us) ||
+      upload(&p->d_strips, P.strips, us) || upload(&p->d_xofs, P.xofs, us) ||
+      upload(&p->d_xofs1, P.xofs1, us) || upload(&p->d_yofs, P.yofs, us) ||
+      upload(&p->d_alpha, P.alpha, us) || upload(&p->d_beta, P.beta, us) ||
+      upload(&p->d_pyr_xs, P.pyr_xs, us) || upload(&p->d_pyr_ys, P.pyr_ys, us) ||
+      upload(&p->d_pyr_bo, P.pyr_bo, us) || upload(&p->d_pyr_blob, P.pyr_blob, us)) {
     plan_free(p);
     return ORBX_ERR_HIP;
   }
@@ -237,9 +241,11 @@ extern "C" int orbx_plan_create(const orbx_params* prm, int width, int height, i
     plan_free(p);
     return ORBX_ERR_HIP;
   }
-  hipMemset(p->d_err, 0, 16);
-  hipMemset(p->d_ccount, 0, B * (size_t)(P.ncells ? P.ncells : 1) * 4);
-  if (hipDeviceSynchronize() != hipSuccess) { plan_free(p); return ORBX_ERR_HIP; }
+  // stream-ordered: no device-wide synchronisation (other extractors and
+  // the matcher may be running on this device from other threads)
+  if (hipMemsetAsync(p->d_err, 0, 16, us) != hipSuccess ||
+      hipMemsetAsync(p->d_ccount, 0, B * (size_t)(P.ncells ? P.ncells : 1) * 4, us) != hipSuccess ||
+      hipStreamSynchronize(us) != hipSuccess) { plan_free(p); return ORBX_ERR_HIP; }
   *out = p;
   return ORBX_OK;
 }
@@ -275,6 +281,8 @@ extern "C" int orbx_plan_extract(orbx_plan* p, const uint8_t* frames, int nframe
     return ORBX_ERR_ARG;
   const Plan& P = p->P;
   if (rstride < (size_t)P.W || fstride < rstride * (size_t)P.H) return ORBX_ERR_ARG;
+  /* the kernels form row offsets with 24-bit multiplies (__umul24) */
+  if (rstride >= ((size_t)1 << 24)) return ORBX_ERR_UNSUPPORTED;
   ORBX_TRY(hipSetDevice(p->device));
   hipStream_t s = (hipStream_t)stream; /* NULL = the default stream */
   const int L = P.params.nlevels, n = nframes;
@@ -326,11 +334,12 @@ extern "C" int orbx_plan_check(orbx_plan* p, void* stream) {
   if (!p) return ORBX_ERR_ARG;
   ORBX_TRY(hipSetDevice(p->device));
   hipStream_t s = (hipStream_t)stream; /* NULL = the default stream */
+  ORBX_TRY(hipMemcpyAsync(p->h_err, p->d_err, sizeof(int), hipMemcpyDeviceToHost, s));
   ORBX_TRY(hipStreamSynchronize(s));
-  int err = 0;
-  ORBX_TRY(hipMemcpy(&err, p->d_err, sizeof(int), hipMemcpyDeviceToHost));
+  const int err = *p->h_err;
   if (err) {
-    ORBX_TRY(hipMemset(p->d_err, 0, sizeof(int)));
+    ORBX_TRY(hipMemsetAsync(p->d_err, 0, sizeof(int), s));
+    ORBX_TRY(hipStreamSynchronize(s));
     if (err & ORBX_DEVERR_QUADTREE) return ORBX_ERR_QUADTREE;
     return ORBX_ERR_CAPACITY;
   }
@@ -368,8 +377,9 @@ static void extractor_release_plan(orbx_extractor* e) {
   if (e->d_kps) hipFree(e->d_kps);
   if (e->d_desc) hipFree(e->d_desc);
   if (e->d_count) hipFree(e->d_count);
+  if (e->h_res) hipHostFree(e->h_res);
   e->plan = nullptr; e->d_img = nullptr; e->d_kps = nullptr; e->d_desc = nullptr;
-  e->d_count = nullptr; e->W = e->H = 0; e->have_frame = false;
+  e->d_count = nullptr; e->h_res = nullptr; e->W = e->H = 0; e->have_frame = false;
 }
 
 static int extractor_prepare(orbx_extractor* e, int W, int H) {
@@ -377,14 +387,17 @@ static int extractor_prepare(orbx_extractor* e, int W, int H) {
   extractor_release_plan(e);
   int rc = orbx_plan_create(&e->params, W, H, 1, e->device, &e->plan);
   if (rc) return rc;
-  const int kcap = e->plan->P.kcap;
+  const size_t kcap = (size_t)std::max(e->plan->P.kcap, 1);
   if (dev_alloc((void**)&e->d_img, (size_t)W * H) ||
-      dev_alloc((void**)&e->d_kps, sizeof(orbx_keypoint) * (size_t)(kcap ? kcap : 1)) ||
-      dev_alloc((void**)&e->d_desc, 32 * (size_t)(kcap ? kcap : 1)) ||
-      dev_alloc((void**)&e->d_count, sizeof(int))) {
+      dev_alloc((void**)&e->d_kps, sizeof(orbx_keypoint) * kcap) ||
+      dev_alloc((void**)&e->d_desc, 32 * kcap) ||
+      dev_alloc((void**)&e->d_count, sizeof(int)) ||
+      hipHostMalloc((void**)&e->h_res, 64 + (sizeof(orbx_keypoint) + 32) * kcap,
+                    hipHostMallocDefault) != hipSuccess) {
     extractor_release_plan(e);
     return ORBX_ERR_HIP;
   }
+  e->last_k = 0;
   e->W = W;
   e->H = H;
   return ORBX_OK;
@@ -429,24 +442,47 @@ extern "C" int orbx_extract(orbx_extractor* e, const uint8_t* img, int W, int H,
   int rc = extractor_prepare(e, W, H);
   if (rc) return rc;
   ORBX_TRY(hipSetDevice(e->device));
-  hipStream_t s = e->plan->stream;
+  orbx_plan* p = e->plan;
+  hipStream_t s = p->stream;
   ORBX_TRY(hipMemcpy2DAsync(e->d_img, (size_t)W, img, stride, (size_t)W, (size_t)H,
                             hipMemcpyHostToDevice, s));
-  rc = orbx_plan_extract(e->plan, e->d_img, 1, (size_t)W * H, (size_t)W, e->d_kps, e->d_desc,
+  rc = orbx_plan_extract(p, e->d_img, 1, (size_t)W * H, (size_t)W, e->d_kps, e->d_desc,
                          e->d_count, s);
   if (rc) return rc;
-  int K = 0;
-  ORBX_TRY(hipMemcpyAsync(&K, e->d_count, sizeof(int), hipMemcpyDeviceToHost, s));
-  rc = orbx_plan_check(e->plan, s);
-  e->have_frame = (rc == ORBX_OK);
-  if (rc) return rc;
+  // one round trip in the common case: the error word, the count and a
+  // speculative prefix of the rows (sized by the previous call) come back
+  // together into pinned staging; only a larger frame needs a second copy
+  const int kcap = std::max(p->P.kcap, 1);
+  const int guess = std::min(kcap, e->last_k + e->last_k / 4 + 64);
+  int* h_cnt = reinterpret_cast<int*>(e->h_res);
+  orbx_keypoint* h_kps = reinterpret_cast<orbx_keypoint*>(e->h_res + 64);
+  uint8_t* h_desc = e->h_res + 64 + sizeof(orbx_keypoint) * (size_t)kcap;
+  ORBX_TRY(hipMemcpyAsync(p->h_err, p->d_err, sizeof(int), hipMemcpyDeviceToHost, s));
+  ORBX_TRY(hipMemcpyAsync(h_cnt, e->d_count, sizeof(int), hipMemcpyDeviceToHost, s));
+  ORBX_TRY(hipMemcpyAsync(h_kps, e->d_kps, sizeof(orbx_keypoint) * (size_t)guess,
+                          hipMemcpyDeviceToHost, s));
+  ORBX_TRY(hipMemcpyAsync(h_desc, e->d_desc, 32 * (size_t)guess, hipMemcpyDeviceToHost, s));
+  ORBX_TRY(hipStreamSynchronize(s));
+  if (*p->h_err) {
+    rc = orbx_plan_check(p, s); /* resets the device error word */
+    e->have_frame = false;
+    return rc ? rc : ORBX_ERR_CAPACITY;
+  }
+  e->have_frame = true;
+  const int K = *h_cnt;
   *n = K;
   if (K == 0) return ORBX_OK; /* keypoints untouched, descriptors released (:460-463) */
   if (K > cap || !kps || !desc) return ORBX_ERR_CAPACITY;
-  ORBX_TRY(hipMemcpyAsync(kps, e->d_kps, sizeof(orbx_keypoint) * (size_t)K,
-                          hipMemcpyDeviceToHost, s));
-  ORBX_TRY(hipMemcpyAsync(desc, e->d_desc, 32 * (size_t)K, hipMemcpyDeviceToHost, s));
-  ORBX_TRY(hipStreamSynchronize(s));
+  if (K > guess) {
+    ORBX_TRY(hipMemcpyAsync(h_kps + guess, e->d_kps + guess,
+                            sizeof(orbx_keypoint) * (size_t)(K - guess), hipMemcpyDeviceToHost, s));
+    ORBX_TRY(hipMemcpyAsync(h_desc + 32 * (size_t)guess, e->d_desc + 32 * (size_t)guess,
+                            32 * (size_t)(K - guess), hipMemcpyDeviceToHost, s));
+    ORBX_TRY(hipStreamSynchronize(s));
+  }
+  e->last_k = K;
+  memcpy(kps, h_kps, sizeof(orbx_keypoint) * (size_t)K);
+  memcpy(desc, h_desc, 32 * (size_t)K);
   return ORBX_OK;
 }
 
@@ -469,7 +505,8 @@ extern "C" int orbx_extractor_level(orbx_extractor* e, int level, uint8_t* dst, 
     src = e->plan->d_pyr + e->plan->P.levels[L.unique].pyr_off;
     pitch = (size_t)L.pitch;
   }
-  ORBX_TRY(hipMemcpy2D(dst, dst_stride, src, pitch, (size_t)L.w, (size_t)L.h,
-                       hipMemcpyDeviceToHost));
+  ORBX_TRY(hipMemcpy2DAsync(dst, dst_stride, src, pitch, (size_t)L.w, (size_t)L.h,
+                            hipMemcpyDeviceToHost, e->plan->stream));
+  ORBX_TRY(hipStreamSynchronize(e->plan->stream));
   return ORBX_OK;
 }

@@ -15,6 +15,7 @@ __global__ void k_match_candidates(const MProblem*, const MNodePair*, int, int, 
                                    int2*);
 template <int NJ>
 __global__ void k_match_cand_lds(const MProblem*, const MNodePair*, uint2*, int4*, int2*);
+template <int NW>
 __global__ void k_match_cand_rows(const MProblem*, const MNodePair*, const uint4*, const uint32_t*,
                                   uint2*, int4*, int2*);
 __global__ void k_match_gather2(const MProblem*, const MNodePair*, uint4*, uint32_t*);
@@ -34,28 +35,17 @@ using namespace orbx;
 
 namespace {
 
-// RAII device buffers for one synchronous call
-struct DevBufs {
-  std::vector<void*> ptrs;
-  ~DevBufs() {
-    for (void* p : ptrs) hipFree(p);
+// bytes 24..31 of every descriptor zero (orbx descriptors with the
+// reference's pattern): the candidate kernel may skip dwords 6-7 exactly
+bool upper_bytes_zero(const uint8_t* d, int n) {
+  uint64_t acc = 0;
+  for (int i = 0; i < n; ++i) {
+    uint64_t w;
+    memcpy(&w, d + (size_t)i * 32 + 24, 8);
+    acc |= w;
   }
-  template <typename T>
-  T* alloc(size_t n) {
-    void* p = nullptr;
-    if (hipMalloc(&p, std::max<size_t>(n, 1) * sizeof(T)) != hipSuccess) return nullptr;
-    ptrs.push_back(p);
-    return (T*)p;
-  }
-  template <typename T>
-  T* upload(const T* src, size_t n, hipStream_t s) {
-    T* d = alloc<T>(n);
-    if (!d) return nullptr;
-    if (n && src && hipMemcpyAsync(d, src, n * sizeof(T), hipMemcpyHostToDevice, s) != hipSuccess)
-      return nullptr;
-    return d;
-  }
-};
+  return acc == 0;
+}
 
 int check_frame(const orbx_bow_frame* k) {
   if (!k || k->n < 0 || k->nnodes < 0) return ORBX_ERR_ARG;
@@ -74,7 +64,14 @@ int check_frame(const orbx_bow_frame* k) {
 void launch_match(const MProblem* d_probs, int nprob, const MNodePair* d_nps, int nnp, int nrows,
                   int sequential, int max_n1, int max_n2, int max_bitmap_n2, uint4* d_gdesc2,
                   uint32_t* d_gval2, uint2* d_cand, int4* d_rowinfo, int2* d_ev, int* d_last,
-                  const int* d_last_off, hipStream_t s, StageTimer* timer) {
+                  const int* d_last_off, hipStream_t s, StageTimer* timer, bool six_words) {
+  {
+    int dev = 0;
+    hipGetDevice(&dev);
+    set_max_dynamic_lds((const void*)k_match_cand_lds<32>, dev);
+    set_max_dynamic_lds((const void*)k_match_resolve_spec, dev);
+    set_max_dynamic_lds((const void*)k_match_resolve, dev);
+  }
   if (timer) timer->begin(ORBX_STAGE_MCAND, s);
   if (nrows > 0 && nnp > 0) {
     if (max_n2 <= ORBM_MAX_N2 && nnp <= 65535 && d_gdesc2) {
@@ -83,13 +80,15 @@ void launch_match(const MProblem* d_probs, int nprob, const MNodePair* d_nps, in
       if (max_n2 > 0)
         hipLaunchKernelGGL(k_match_gather2, dim3((max_n2 + 127) / 128, nnp), dim3(256), 0, s, d_probs,
                            d_nps, d_gdesc2, d_gval2);
-      hipLaunchKernelGGL(k_match_cand_rows, dim3((max_n1 + 127) / 128, nnp), dim3(256), 0, s,
-                         d_probs, d_nps, d_gdesc2, d_gval2, d_cand, d_rowinfo, d_ev);
+      if (six_words)
+        hipLaunchKernelGGL(k_match_cand_rows<6>, dim3((max_n1 + 127) / 128, nnp), dim3(256), 0, s,
+                           d_probs, d_nps, d_gdesc2, d_gval2, d_cand, d_rowinfo, d_ev);
+      else
+        hipLaunchKernelGGL(k_match_cand_rows<8>, dim3((max_n1 + 127) / 128, nnp), dim3(256), 0, s,
+                           d_probs, d_nps, d_gdesc2, d_gval2, d_cand, d_rowinfo, d_ev);
     } else if (max_n2 <= 64 * 32 && nnp <= 65535) {
       // list2 staged in LDS, distances in registers (32 per lane)
       const size_t lds = (size_t)std::max(max_n2, 1) * 32;
-      hipFuncSetAttribute((const void*)k_match_cand_lds<32>,
-                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
       hipLaunchKernelGGL(k_match_cand_lds<32>, dim3((max_n1 + 63) / 64, nnp), dim3(256), lds, s,
                          d_probs, d_nps, d_cand, d_rowinfo, d_ev);
     } else {
@@ -104,15 +103,11 @@ void launch_match(const MProblem* d_probs, int nprob, const MNodePair* d_nps, in
     // speculative 64-row chunks; LDS = vbMatched2 bitmap + claim table
     const int n2cap = std::max(max_bitmap_n2, 32);
     const size_t lds = (size_t)((n2cap + 31) / 32) * 4 + (size_t)n2cap * 4;
-    hipFuncSetAttribute((const void*)k_match_resolve_spec,
-                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     hipLaunchKernelGGL(k_match_resolve_spec, dim3(units), dim3(64), lds, s, d_probs, d_nps, units,
                        d_cand, d_rowinfo, d_ev, n2cap);
   } else if (nrows > 0 && units > 0) {
     if (max_bitmap_n2 > 16384) {
       const size_t lds = (size_t)((max_bitmap_n2 + 31) / 32) * 4;
-      hipFuncSetAttribute((const void*)k_match_resolve, hipFuncAttributeMaxDynamicSharedMemorySize,
-                          (int)lds);
       hipLaunchKernelGGL(k_match_resolve, dim3(units), dim3(64), lds, s, d_probs, d_nps, units,
                          sequential, d_cand, d_rowinfo, d_ev);
     } else {
@@ -189,66 +184,83 @@ extern "C" int orbm_search_by_bow(const orbx_bow_frame* kf1, const orbx_bow_fram
     return ORBX_OK;
   }
   ORBX_TRY(hipSetDevice(device));
-  hipStream_t s;
-  ORBX_TRY(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
-  int result = ORBX_OK;
-  {
-    DevBufs B;
-    const uint32_t nf1 = kf1->nnodes ? kf1->node_off[kf1->nnodes] : 0;
-    const uint32_t nf2 = kf2->nnodes ? kf2->node_off[kf2->nnodes] : 0;
-    MProblem P;
-    memset(&P, 0, sizeof(P));
-    P.desc1 = B.upload(kf1->desc, (size_t)kf1->n * 32, s);
-    P.desc2 = B.upload(kf2->desc, (size_t)kf2->n * 32, s);
-    P.ang1 = B.upload(kf1->angle, (size_t)kf1->n, s);
-    P.ang2 = B.upload(kf2->angle, (size_t)kf2->n, s);
-    P.valid1 = kf1->valid ? B.upload(kf1->valid, (size_t)kf1->n, s) : nullptr;
-    P.valid2 = kf2->valid ? B.upload(kf2->valid, (size_t)kf2->n, s) : nullptr;
-    P.feat1 = B.upload(kf1->feat, nf1, s);
-    P.feat2 = B.upload(kf2->feat, nf2, s);
-    P.match12 = B.alloc<int32_t>(kf1->n);
-    P.nmatches = B.alloc<int>(1);
-    P.ang_stride = 1;
-    P.n1 = kf1->n;
-    P.n2 = kf2->n;
-    P.np_begin = 0;
-    P.np_end = (int)nps.size();
-    P.row_begin = 0;
-    P.row_end = rows;
-    P.check_ori = check_ori ? 1 : 0;
-    P.nnratio = nnratio;
-    P.sequential = sequential;
-    P.dcap = orbm_dcap(nnratio);
-    P.pad = 0;
-    MProblem* d_prob = B.upload(&P, 1, s);
-    MNodePair* d_nps = B.upload(nps.data(), nps.size(), s);
-    uint2* d_cand = B.alloc<uint2>((size_t)rows * ORBM_T);
-    int4* d_rowinfo = B.alloc<int4>(rows);
-    int2* d_ev = B.alloc<int2>(rows);
-    int* d_last = B.alloc<int>(kf1->n);
-    uint4* d_gdesc2 = B.alloc<uint4>((size_t)g2 * 2);
-    uint32_t* d_gval2 = kf2->valid ? B.alloc<uint32_t>((size_t)g2) : nullptr;
-    const int zero = 0;
-    int* d_last_off = B.upload(&zero, 1, s);
-    if (!P.desc1 || !P.desc2 || !P.ang1 || !P.ang2 || !P.feat1 || !P.feat2 || !P.match12 ||
-        !P.nmatches || !d_prob || !d_nps || !d_cand || !d_rowinfo || !d_ev || !d_last ||
-        !d_last_off || !d_gdesc2 || (kf1->valid && !P.valid1) ||
-        (kf2->valid && (!P.valid2 || !d_gval2))) {
-      result = ORBX_ERR_HIP;
-    } else {
-      launch_match(d_prob, 1, d_nps, (int)nps.size(), rows, sequential, max_n1, max_n2, kf2->n,
-                   d_gdesc2, d_gval2, d_cand, d_rowinfo, d_ev, d_last, d_last_off, s, nullptr);
-      if (hipGetLastError() != hipSuccess ||
-          hipMemcpyAsync(match12, P.match12, sizeof(int32_t) * (size_t)kf1->n,
-                         hipMemcpyDeviceToHost, s) != hipSuccess ||
-          hipMemcpyAsync(nmatches, P.nmatches, sizeof(int), hipMemcpyDeviceToHost, s) !=
-              hipSuccess ||
-          hipStreamSynchronize(s) != hipSuccess)
-        result = ORBX_ERR_HIP;
-    }
-  }
-  hipStreamDestroy(s);
-  return result;
+  WsLease L(device);
+  CallWs* w = L.w;
+  if (!w) return ORBX_ERR_HIP;
+  hipStream_t s = w->stream;
+  // one arena: inputs [0, in_end) go up in one copy from pinned staging,
+  // outputs [in_end, out_end) come back in one copy, scratch after them
+  const uint32_t nf1 = kf1->nnodes ? kf1->node_off[kf1->nnodes] : 0;
+  const uint32_t nf2 = kf2->nnodes ? kf2->node_off[kf2->nnodes] : 0;
+  const size_t n1 = (size_t)kf1->n, n2 = (size_t)kf2->n, nnp = nps.size();
+  Carve C;
+  const size_t o_desc1 = C.take(n1 * 32), o_desc2 = C.take(n2 * 32);
+  const size_t o_ang1 = C.take(n1 * 4), o_ang2 = C.take(n2 * 4);
+  const size_t o_val1 = kf1->valid ? C.take(n1) : 0, o_val2 = kf2->valid ? C.take(n2) : 0;
+  const size_t o_feat1 = C.take((size_t)nf1 * 4), o_feat2 = C.take((size_t)nf2 * 4);
+  const size_t o_prob = C.take(sizeof(MProblem)), o_nps = C.take(nnp * sizeof(MNodePair));
+  const size_t o_loff = C.take(sizeof(int));
+  const size_t in_end = C.off;
+  const size_t o_m12 = C.take(n1 * 4), o_nm = C.take(sizeof(int));
+  const size_t out_end = C.off;
+  const size_t o_cand = C.take((size_t)rows * ORBM_T * sizeof(uint2));
+  const size_t o_rowinfo = C.take((size_t)rows * sizeof(int4)), o_ev = C.take((size_t)rows * sizeof(int2));
+  const size_t o_last = C.take(n1 * 4), o_g2 = C.take((size_t)g2 * 2 * sizeof(uint4));
+  const size_t o_gv2 = kf2->valid ? C.take((size_t)g2 * 4) : 0;
+  int rc2 = w->reserve(C.off, out_end);
+  if (rc2) return rc2;
+  uint8_t* d = w->d;
+  uint8_t* h = w->h;
+  memcpy(h + o_desc1, kf1->desc, n1 * 32);
+  memcpy(h + o_desc2, kf2->desc, n2 * 32);
+  memcpy(h + o_ang1, kf1->angle, n1 * 4);
+  memcpy(h + o_ang2, kf2->angle, n2 * 4);
+  if (kf1->valid) memcpy(h + o_val1, kf1->valid, n1);
+  if (kf2->valid) memcpy(h + o_val2, kf2->valid, n2);
+  if (nf1) memcpy(h + o_feat1, kf1->feat, (size_t)nf1 * 4);
+  if (nf2) memcpy(h + o_feat2, kf2->feat, (size_t)nf2 * 4);
+  MProblem P;
+  memset(&P, 0, sizeof(P));
+  P.desc1 = d + o_desc1;
+  P.desc2 = d + o_desc2;
+  P.ang1 = reinterpret_cast<const float*>(d + o_ang1);
+  P.ang2 = reinterpret_cast<const float*>(d + o_ang2);
+  P.valid1 = kf1->valid ? d + o_val1 : nullptr;
+  P.valid2 = kf2->valid ? d + o_val2 : nullptr;
+  P.feat1 = reinterpret_cast<const uint32_t*>(d + o_feat1);
+  P.feat2 = reinterpret_cast<const uint32_t*>(d + o_feat2);
+  P.match12 = reinterpret_cast<int32_t*>(d + o_m12);
+  P.nmatches = reinterpret_cast<int*>(d + o_nm);
+  P.ang_stride = 1;
+  P.n1 = kf1->n;
+  P.n2 = kf2->n;
+  P.np_begin = 0;
+  P.np_end = (int)nnp;
+  P.row_begin = 0;
+  P.row_end = rows;
+  P.check_ori = check_ori ? 1 : 0;
+  P.nnratio = nnratio;
+  P.sequential = sequential;
+  P.dcap = orbm_dcap(nnratio);
+  P.pad = 0;
+  memcpy(h + o_prob, &P, sizeof(P));
+  if (nnp) memcpy(h + o_nps, nps.data(), nnp * sizeof(MNodePair));
+  memset(h + o_loff, 0, sizeof(int));
+  ORBX_TRY(hipMemcpyAsync(d, h, in_end, hipMemcpyHostToDevice, s));
+  launch_match(reinterpret_cast<MProblem*>(d + o_prob), 1, reinterpret_cast<MNodePair*>(d + o_nps),
+               (int)nnp, rows, sequential, max_n1, max_n2, kf2->n,
+               reinterpret_cast<uint4*>(d + o_g2),
+               kf2->valid ? reinterpret_cast<uint32_t*>(d + o_gv2) : nullptr,
+               reinterpret_cast<uint2*>(d + o_cand), reinterpret_cast<int4*>(d + o_rowinfo),
+               reinterpret_cast<int2*>(d + o_ev), reinterpret_cast<int*>(d + o_last),
+               reinterpret_cast<const int*>(d + o_loff), s, nullptr,
+               upper_bytes_zero(kf1->desc, kf1->n) && upper_bytes_zero(kf2->desc, kf2->n));
+  if (hipGetLastError() != hipSuccess) return ORBX_ERR_HIP;
+  ORBX_TRY(hipMemcpyAsync(h + in_end, d + in_end, out_end - in_end, hipMemcpyDeviceToHost, s));
+  ORBX_TRY(hipStreamSynchronize(s));
+  memcpy(match12, h + o_m12, n1 * 4);
+  memcpy(nmatches, h + o_nm, sizeof(int));
+  return ORBX_OK;
 }
 
 extern "C" int orbm_descriptor_distance_batch(const uint8_t* a, int na, const uint8_t* b, int nb,
@@ -262,30 +274,32 @@ extern "C" int orbm_descriptor_distance_batch(const uint8_t* a, int na, const ui
   if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev)
     return ORBX_ERR_NO_DEVICE;
   ORBX_TRY(hipSetDevice(device));
-  hipStream_t s;
-  ORBX_TRY(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
-  int result = ORBX_OK;
-  {
-    DevBufs B;
-    const uint8_t* da = B.upload(a, (size_t)na * 32, s);
-    const uint8_t* db = B.upload(b, (size_t)nb * 32, s);
-    const int32_t* dia = B.upload(ia, (size_t)npairs, s);
-    const int32_t* dib = B.upload(ib, (size_t)npairs, s);
-    int32_t* dd = B.alloc<int32_t>(npairs);
-    if (!da || !db || !dia || !dib || !dd) {
-      result = ORBX_ERR_HIP;
-    } else {
-      hipLaunchKernelGGL(k_hamming_pairs, dim3((npairs + 255) / 256), dim3(256), 0, s, da, db,
-                         dia, dib, npairs, dd);
-      if (hipGetLastError() != hipSuccess ||
-          hipMemcpyAsync(dist, dd, sizeof(int32_t) * (size_t)npairs, hipMemcpyDeviceToHost, s) !=
-              hipSuccess ||
-          hipStreamSynchronize(s) != hipSuccess)
-        result = ORBX_ERR_HIP;
-    }
-  }
-  hipStreamDestroy(s);
-  return result;
+  WsLease L(device);
+  CallWs* w = L.w;
+  if (!w) return ORBX_ERR_HIP;
+  hipStream_t s = w->stream;
+  Carve C;
+  const size_t o_a = C.take((size_t)na * 32), o_b = C.take((size_t)nb * 32);
+  const size_t o_ia = C.take((size_t)npairs * 4), o_ib = C.take((size_t)npairs * 4);
+  const size_t in_end = C.off, o_d = C.take((size_t)npairs * 4), out_end = C.off;
+  int rc = w->reserve(out_end, out_end);
+  if (rc) return rc;
+  uint8_t* h = w->h;
+  uint8_t* d = w->d;
+  memcpy(h + o_a, a, (size_t)na * 32);
+  memcpy(h + o_b, b, (size_t)nb * 32);
+  memcpy(h + o_ia, ia, (size_t)npairs * 4);
+  memcpy(h + o_ib, ib, (size_t)npairs * 4);
+  ORBX_TRY(hipMemcpyAsync(d, h, in_end, hipMemcpyHostToDevice, s));
+  hipLaunchKernelGGL(k_hamming_pairs, dim3((npairs + 255) / 256), dim3(256), 0, s, d + o_a, d + o_b,
+                     reinterpret_cast<const int32_t*>(d + o_ia),
+                     reinterpret_cast<const int32_t*>(d + o_ib), npairs,
+                     reinterpret_cast<int32_t*>(d + o_d));
+  if (hipGetLastError() != hipSuccess) return ORBX_ERR_HIP;
+  ORBX_TRY(hipMemcpyAsync(h + o_d, d + o_d, (size_t)npairs * 4, hipMemcpyDeviceToHost, s));
+  ORBX_TRY(hipStreamSynchronize(s));
+  memcpy(dist, h + o_d, (size_t)npairs * 4);
+  return ORBX_OK;
 }
 
 // ---------------------------------------------------------------------------
@@ -338,6 +352,9 @@ __global__ void k_match_setup(MProblem* probs, MNodePair* nps, int npairs,
 
 struct orbm_plan {
   int device = 0, max_pairs = 0, kcap = 0, topn = 0;
+  /* frames come from orbx_plan_extract, whose descriptors have bytes 24..31
+   * zero (static_assert on the pattern in kernels_extract.hip) */
+  bool six_words = true;
   MProblem* d_probs = nullptr;
   MNodePair* d_nps = nullptr;
   uint32_t* d_sel = nullptr;
@@ -427,6 +444,6 @@ extern "C" int orbm_plan_match_frames(orbm_plan* m, int npairs, const orbx_keypo
   m->timer.end(ORBX_STAGE_MSELECT, s);
   launch_match(m->d_probs, npairs, m->d_nps, npairs, npairs * m->topn, 0, m->topn, m->topn,
                m->kcap, m->d_gdesc2, nullptr, m->d_cand, m->d_rowinfo, m->d_ev, m->d_last,
-               m->d_last_off, s, &m->timer);
+               m->d_last_off, s, &m->timer, m->six_words);
   return hipGetLastError() == hipSuccess ? ORBX_OK : ORBX_ERR_HIP;
 }

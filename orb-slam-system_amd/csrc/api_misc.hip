@@ -35,24 +35,26 @@ extern "C" int orbm_compute_distinctive_descriptors(const uint8_t* desc, const i
     if (off[m + 1] < off[m] || off[m + 1] - off[m] > (1 << 20)) return ORBX_ERR_ARG;
   int rc = check_device(device);
   if (rc) return rc;
-  uint8_t* d_desc = nullptr;
-  int32_t *d_off = nullptr, *d_best = nullptr;
-  rc = ORBX_ERR_HIP;
-  if (hipMalloc((void**)&d_desc, std::max(total, 1) * (size_t)32) == hipSuccess &&
-      hipMalloc((void**)&d_off, (nmp + 1) * sizeof(int32_t)) == hipSuccess &&
-      hipMalloc((void**)&d_best, nmp * sizeof(int32_t)) == hipSuccess &&
-      (total == 0 || hipMemcpy(d_desc, desc, (size_t)total * 32, hipMemcpyHostToDevice) == hipSuccess) &&
-      hipMemcpy(d_off, off, (nmp + 1) * sizeof(int32_t), hipMemcpyHostToDevice) == hipSuccess) {
-    hipLaunchKernelGGL(k_distinctive, dim3((nmp + 3) / 4), dim3(256), 0, 0, d_desc, d_off, nmp,
-                       d_best);
-    if (hipGetLastError() == hipSuccess &&
-        hipMemcpy(best, d_best, nmp * sizeof(int32_t), hipMemcpyDeviceToHost) == hipSuccess)
-      rc = ORBX_OK;
-  }
-  if (d_desc) hipFree(d_desc);
-  if (d_off) hipFree(d_off);
-  if (d_best) hipFree(d_best);
-  return rc;
+  WsLease L(device);
+  CallWs* w = L.w;
+  if (!w) return ORBX_ERR_HIP;
+  Carve C;
+  const size_t o_desc = C.take((size_t)total * 32), o_off = C.take((size_t)(nmp + 1) * 4);
+  const size_t in_end = C.off, o_best = C.take((size_t)nmp * 4);
+  rc = w->reserve(C.off, C.off);
+  if (rc) return rc;
+  if (total) memcpy(w->h + o_desc, desc, (size_t)total * 32);
+  memcpy(w->h + o_off, off, (size_t)(nmp + 1) * 4);
+  ORBX_TRY(hipMemcpyAsync(w->d, w->h, in_end, hipMemcpyHostToDevice, w->stream));
+  hipLaunchKernelGGL(k_distinctive, dim3((nmp + 3) / 4), dim3(256), 0, w->stream, w->d + o_desc,
+                     reinterpret_cast<const int32_t*>(w->d + o_off), nmp,
+                     reinterpret_cast<int32_t*>(w->d + o_best));
+  if (hipGetLastError() != hipSuccess) return ORBX_ERR_HIP;
+  ORBX_TRY(hipMemcpyAsync(w->h + o_best, w->d + o_best, (size_t)nmp * 4, hipMemcpyDeviceToHost,
+                          w->stream));
+  ORBX_TRY(hipStreamSynchronize(w->stream));
+  memcpy(best, w->h + o_best, (size_t)nmp * 4);
+  return ORBX_OK;
 }
 
 extern "C" int orbx_undistort_keypoints(const orbx_keypoint* kps, int n, const float* K,
@@ -76,17 +78,24 @@ extern "C" int orbx_undistort_keypoints(const orbx_keypoint* kps, int n, const f
   A.ifx = 1. / A.fx;
   A.ify = 1. / A.fy;
   for (int j = 0; j < ndist; ++j) A.k[j] = dist[j];
-  orbx_keypoint *d_in = nullptr, *d_out = nullptr;
-  rc = ORBX_ERR_HIP;
-  if (hipMalloc((void**)&d_in, n * sizeof(orbx_keypoint)) == hipSuccess &&
-      hipMalloc((void**)&d_out, n * sizeof(orbx_keypoint)) == hipSuccess &&
-      hipMemcpy(d_in, kps, n * sizeof(orbx_keypoint), hipMemcpyHostToDevice) == hipSuccess) {
-    hipLaunchKernelGGL(k_undistort, dim3((n + 255) / 256), dim3(256), 0, 0, d_in, n, A, d_out);
-    if (hipGetLastError() == hipSuccess &&
-        hipMemcpy(out, d_out, n * sizeof(orbx_keypoint), hipMemcpyDeviceToHost) == hipSuccess)
-      rc = ORBX_OK;
-  }
-  if (d_in) hipFree(d_in);
-  if (d_out) hipFree(d_out);
-  return rc;
+  WsLease L(device);
+  CallWs* w = L.w;
+  if (!w) return ORBX_ERR_HIP;
+  Carve C;
+  const size_t o_in = C.take((size_t)n * sizeof(orbx_keypoint));
+  const size_t o_out = C.take((size_t)n * sizeof(orbx_keypoint));
+  rc = w->reserve(C.off, C.off);
+  if (rc) return rc;
+  memcpy(w->h + o_in, kps, (size_t)n * sizeof(orbx_keypoint));
+  ORBX_TRY(hipMemcpyAsync(w->d + o_in, w->h + o_in, (size_t)n * sizeof(orbx_keypoint),
+                          hipMemcpyHostToDevice, w->stream));
+  hipLaunchKernelGGL(k_undistort, dim3((n + 255) / 256), dim3(256), 0, w->stream,
+                     reinterpret_cast<const orbx_keypoint*>(w->d + o_in), n, A,
+                     reinterpret_cast<orbx_keypoint*>(w->d + o_out));
+  if (hipGetLastError() != hipSuccess) return ORBX_ERR_HIP;
+  ORBX_TRY(hipMemcpyAsync(w->h + o_out, w->d + o_out, (size_t)n * sizeof(orbx_keypoint),
+                          hipMemcpyDeviceToHost, w->stream));
+  ORBX_TRY(hipStreamSynchronize(w->stream));
+  memcpy(out, w->h + o_out, (size_t)n * sizeof(orbx_keypoint));
+  return ORBX_OK;
 }

@@ -2,6 +2,8 @@
 // (query form, /root/reference/src/ORBmatcher.cc:19-61,732-818,820-894).
 #include <hip/hip_runtime.h>
 
+#include <string.h>
+
 #include <algorithm>
 #include <vector>
 
@@ -29,22 +31,6 @@ using namespace orbx;
 #define PJ_MAXN 8192
 #define PG_CELLS (64 * 48)
 
-namespace {
-struct Bufs {
-  std::vector<void*> p;
-  ~Bufs() {
-    for (void* x : p) hipFree(x);
-  }
-  template <typename T>
-  T* get(size_t n) {
-    void* x = nullptr;
-    if (hipMalloc(&x, std::max<size_t>(n, 1) * sizeof(T)) != hipSuccess) return nullptr;
-    p.push_back(x);
-    return (T*)x;
-  }
-};
-}  // namespace
-
 extern "C" int orbm_search_by_projection(int mode, const orbx_proj_frame* F,
                                          const orbx_query_proj* q, const uint8_t* qdesc, int nq,
                                          float nnratio, int th_dist, int check_ori, int device,
@@ -60,29 +46,43 @@ extern "C" int orbm_search_by_projection(int mode, const orbx_proj_frame* F,
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) return ORBX_ERR_NO_DEVICE;
   ORBX_TRY(hipSetDevice(device));
-  Bufs B;
-  orbx_keypoint* d_keys = B.get<orbx_keypoint>(n);
-  uint8_t* d_desc = B.get<uint8_t>((size_t)n * 32);
-  float* d_ur = F->uright ? B.get<float>(n) : nullptr;
-  uint8_t* d_occ = F->occupied ? B.get<uint8_t>(n) : nullptr;
-  int* d_off = B.get<int>(PG_CELLS + 1);
-  int* d_feat = B.get<int>(n);
-  orbx_query_proj* d_q = B.get<orbx_query_proj>(nq);
-  uint8_t* d_qd = B.get<uint8_t>((size_t)nq * 32);
-  uint32_t* d_cand = B.get<uint32_t>((size_t)nq * PJ_T);
-  int* d_nc = B.get<int>(nq);
-  int32_t* d_match = B.get<int32_t>(n);
-  int* d_nm = B.get<int>(1);
-  if (!d_keys || !d_desc || (F->uright && !d_ur) || (F->occupied && !d_occ) || !d_off || !d_feat ||
-      !d_q || !d_qd || !d_cand || !d_nc || !d_match || !d_nm)
-    return ORBX_ERR_HIP;
-  hipStream_t s = nullptr;
-  ORBX_TRY(hipMemcpyAsync(d_keys, F->keys, n * sizeof(orbx_keypoint), hipMemcpyHostToDevice, s));
-  ORBX_TRY(hipMemcpyAsync(d_desc, F->desc, (size_t)n * 32, hipMemcpyHostToDevice, s));
-  if (d_ur) ORBX_TRY(hipMemcpyAsync(d_ur, F->uright, n * sizeof(float), hipMemcpyHostToDevice, s));
-  if (d_occ) ORBX_TRY(hipMemcpyAsync(d_occ, F->occupied, n, hipMemcpyHostToDevice, s));
-  ORBX_TRY(hipMemcpyAsync(d_q, q, nq * sizeof(orbx_query_proj), hipMemcpyHostToDevice, s));
-  ORBX_TRY(hipMemcpyAsync(d_qd, qdesc, (size_t)nq * 32, hipMemcpyHostToDevice, s));
+  WsLease L(device);
+  CallWs* w = L.w;
+  if (!w) return ORBX_ERR_HIP;
+  hipStream_t s = w->stream;
+  set_max_dynamic_lds((const void*)k_grid_build, device);
+  set_max_dynamic_lds((const void*)k_proj_resolve, device);
+  Carve C;
+  const size_t o_keys = C.take((size_t)n * sizeof(orbx_keypoint)), o_desc = C.take((size_t)n * 32);
+  const size_t o_ur = F->uright ? C.take((size_t)n * 4) : 0, o_occ = F->occupied ? C.take(n) : 0;
+  const size_t o_q = C.take((size_t)nq * sizeof(orbx_query_proj)), o_qd = C.take((size_t)nq * 32);
+  const size_t in_end = C.off;
+  const size_t o_match = C.take((size_t)n * 4), o_nm = C.take(4), out_end = C.off;
+  const size_t o_off = C.take((PG_CELLS + 1) * 4), o_feat = C.take((size_t)n * 4);
+  const size_t o_cand = C.take((size_t)nq * PJ_T * 4), o_nc = C.take((size_t)nq * 4);
+  int rc = w->reserve(C.off, out_end);
+  if (rc) return rc;
+  uint8_t* h = w->h;
+  uint8_t* d = w->d;
+  memcpy(h + o_keys, F->keys, (size_t)n * sizeof(orbx_keypoint));
+  memcpy(h + o_desc, F->desc, (size_t)n * 32);
+  if (F->uright) memcpy(h + o_ur, F->uright, (size_t)n * 4);
+  if (F->occupied) memcpy(h + o_occ, F->occupied, n);
+  memcpy(h + o_q, q, (size_t)nq * sizeof(orbx_query_proj));
+  memcpy(h + o_qd, qdesc, (size_t)nq * 32);
+  ORBX_TRY(hipMemcpyAsync(d, h, in_end, hipMemcpyHostToDevice, s));
+  orbx_keypoint* d_keys = reinterpret_cast<orbx_keypoint*>(d + o_keys);
+  uint8_t* d_desc = d + o_desc;
+  float* d_ur = F->uright ? reinterpret_cast<float*>(d + o_ur) : nullptr;
+  uint8_t* d_occ = F->occupied ? d + o_occ : nullptr;
+  int* d_off = reinterpret_cast<int*>(d + o_off);
+  int* d_feat = reinterpret_cast<int*>(d + o_feat);
+  orbx_query_proj* d_q = reinterpret_cast<orbx_query_proj*>(d + o_q);
+  uint8_t* d_qd = d + o_qd;
+  uint32_t* d_cand = reinterpret_cast<uint32_t*>(d + o_cand);
+  int* d_nc = reinterpret_cast<int*>(d + o_nc);
+  int32_t* d_match = reinterpret_cast<int32_t*>(d + o_match);
+  int* d_nm = reinterpret_cast<int*>(d + o_nm);
   ProjFrame PF;
   PF.n = n;
   PF.minX = F->min_x;
@@ -100,8 +100,9 @@ extern "C" int orbm_search_by_projection(int mode, const orbx_proj_frame* F,
                      d_off, d_feat, d_q, d_qd, nq, mode, nnratio, th_dist, check_ori, d_cand,
                      d_nc, d_match, d_nm);
   if (hipGetLastError() != hipSuccess) return ORBX_ERR_HIP;
-  ORBX_TRY(hipMemcpyAsync(match, d_match, n * sizeof(int32_t), hipMemcpyDeviceToHost, s));
-  ORBX_TRY(hipMemcpyAsync(nmatches, d_nm, sizeof(int), hipMemcpyDeviceToHost, s));
+  ORBX_TRY(hipMemcpyAsync(h + in_end, d + in_end, out_end - in_end, hipMemcpyDeviceToHost, s));
   ORBX_TRY(hipStreamSynchronize(s));
+  memcpy(match, h + o_match, (size_t)n * 4);
+  memcpy(nmatches, h + o_nm, sizeof(int));
   return ORBX_OK;
 }

@@ -1,0 +1,97 @@
+// api_ws.hip -- pooled per-call workspaces and one-time kernel attributes
+// for the synchronous drop-in entry points (api_common.h).
+#include <hip/hip_runtime.h>
+
+#include <map>
+#include <mutex>
+#include <utility>
+#include <vector>
+
+#include "api_common.h"
+
+namespace orbx {
+
+namespace {
+std::mutex g_pool_mu;
+std::map<int, std::vector<CallWs*>>* g_pool = nullptr;  // never freed: process lifetime
+std::mutex g_attr_mu;
+std::map<std::pair<const void*, int>, int>* g_attr = nullptr;
+}  // namespace
+
+int CallWs::reserve(size_t dbytes, size_t hbytes) {
+  if (dbytes > dcap) {
+    if (d) {
+      if (hipStreamSynchronize(stream) != hipSuccess) return ORBX_ERR_HIP;
+      hipFree(d);
+      d = nullptr;
+      dcap = 0;
+    }
+    const size_t n = dbytes + dbytes / 2 + 4096;
+    if (hipMalloc((void**)&d, n) != hipSuccess) return ORBX_ERR_HIP;
+    dcap = n;
+  }
+  if (hbytes > hcap) {
+    if (h) {
+      if (hipStreamSynchronize(stream) != hipSuccess) return ORBX_ERR_HIP;
+      hipHostFree(h);
+      h = nullptr;
+      hcap = 0;
+    }
+    const size_t n = hbytes + hbytes / 2 + 4096;
+    if (hipHostMalloc((void**)&h, n, hipHostMallocDefault) != hipSuccess) return ORBX_ERR_HIP;
+    hcap = n;
+  }
+  return ORBX_OK;
+}
+
+CallWs* ws_acquire(int device) {
+  {
+    std::lock_guard<std::mutex> g(g_pool_mu);
+    if (!g_pool) g_pool = new std::map<int, std::vector<CallWs*>>();
+    std::vector<CallWs*>& v = (*g_pool)[device];
+    if (!v.empty()) {
+      CallWs* w = v.back();
+      v.pop_back();
+      return w;
+    }
+  }
+  CallWs* w = new CallWs();
+  w->device = device;
+  if (hipStreamCreateWithFlags(&w->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete w;
+    return nullptr;
+  }
+  return w;
+}
+
+void ws_release(CallWs* w) {
+  std::lock_guard<std::mutex> g(g_pool_mu);
+  (*g_pool)[w->device].push_back(w);
+}
+
+int set_max_dynamic_lds(const void* kernel, int device) {
+  std::lock_guard<std::mutex> g(g_attr_mu);
+  if (!g_attr) g_attr = new std::map<std::pair<const void*, int>, int>();
+  auto key = std::make_pair(kernel, device);
+  auto it = g_attr->find(key);
+  if (it != g_attr->end()) return it->second;
+  int lds = 0, optin = 0;
+  int rc = ORBX_OK;
+  if (hipDeviceGetAttribute(&lds, hipDeviceAttributeMaxSharedMemoryPerBlock, device) != hipSuccess)
+    rc = ORBX_ERR_HIP;
+  if (hipDeviceGetAttribute(&optin, hipDeviceAttributeSharedMemPerBlockOptin, device) == hipSuccess &&
+      optin > lds)
+    lds = optin;
+  // the dynamic maximum excludes the kernel's static __shared__ arrays
+  hipFuncAttributes fa;
+  if (rc == ORBX_OK && hipFuncGetAttributes(&fa, kernel) != hipSuccess) rc = ORBX_ERR_HIP;
+  if (rc == ORBX_OK &&
+      hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          lds - (int)fa.sharedSizeBytes) != hipSuccess)
+    rc = ORBX_ERR_HIP;
+  if (rc != ORBX_OK) (void)hipGetLastError(); /* do not leave a sticky error for the caller */
+  (*g_attr)[key] = rc;
+  return rc;
+}
+
+}  // namespace orbx

@@ -328,10 +328,16 @@ __device__ __forceinline__ void topk_insert(uint32_t (&L)[ORBM_T], uint32_t k) {
   L[0] = min(L[0], k);
 }
 
+// NW: descriptor dwords that can differ.  8 in general; 6 when both sides'
+// bytes 24..31 are zero -- always so for orbx descriptors with the
+// reference's 728-entry pattern (pairs 182..255 degenerate),
+// checked by the host before choosing it: the same distances, 25 % fewer ops.
+template <int NW>
 __global__ __launch_bounds__(256) void k_match_cand_rows(
     const MProblem* __restrict__ probs, const MNodePair* __restrict__ nps,
     const uint4* __restrict__ gdesc2, const uint32_t* __restrict__ gval2,
     uint2* __restrict__ cand, int4* __restrict__ rowinfo, int2* __restrict__ ev) {
+  static_assert(NW == 6 || NW == 8, "6 or 8 live descriptor dwords");
   __shared__ uint4 sdesc[2][2 * MC_CHUNK];        // 2 x 16 KB; the merge area aliases it
   __shared__ uint32_t sval[2][MC_CHUNK];          // per-position invalid masks (validity arrays only)
   const int tid = threadIdx.x, lane = tid & 63;
@@ -415,7 +421,7 @@ __global__ __launch_bounds__(256) void k_match_cand_rows(
       for (int u = 0; u < 4; ++u) hi[u] = sd[2 * (j0 + u) + 1];
       uint32_t acc[2][4];
 #pragma unroll
-      for (int k = 0; k < 8; ++k) {
+      for (int k = 0; k < NW; ++k) {
         uint32_t t[2][4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
@@ -514,6 +520,11 @@ __global__ __launch_bounds__(256) void k_match_cand_rows(
     }
   }
 }
+
+template __global__ void k_match_cand_rows<8>(const MProblem*, const MNodePair*, const uint4*,
+                                              const uint32_t*, uint2*, int4*, int2*);
+template __global__ void k_match_cand_rows<6>(const MProblem*, const MNodePair*, const uint4*,
+                                              const uint32_t*, uint2*, int4*, int2*);
 
 // ---------------------------------------------------------------------------
 // k_match_resolve: greedy, in list order.  unit = node pair (parallel mode)

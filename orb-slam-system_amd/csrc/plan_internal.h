@@ -27,6 +27,7 @@ struct orbx_plan {
   uint32_t *d_slots = nullptr, *d_ccount = nullptr, *d_qkeys = nullptr, *d_qout = nullptr;
   int32_t* d_qnode = nullptr;
   int *d_lcount = nullptr, *d_err = nullptr;
+  int* h_err = nullptr; /* pinned: orbx_plan_check reads the error word without a blocking copy */
   size_t pyr_stride = 0, blur_stride = 0, slot_stride = 0, qk_stride = 0, qout_stride = 0;
   size_t qt_lds = 0;
   BriefArgs bargs;
@@ -45,6 +46,9 @@ struct orbx_extractor {
   orbx_keypoint* d_kps = nullptr;
   uint8_t* d_desc = nullptr;
   int* d_count = nullptr;
+  /* pinned result staging: [count | kps rows | desc rows] (kcap rows each) */
+  uint8_t* h_res = nullptr;
+  int last_k = 0; /* keypoints of the previous call: sizes the speculative copy */
   bool have_frame = false;
   void* stereo = nullptr; /* orbs_plan of orbx_stereo_match (api_stereo.hip) */
 };

@@ -459,6 +459,23 @@ def undistort_keypoints(kps, K, dist, device=0):
 
 
 # --------------------------------------------------------------------------- batched device path
+def _check_dev(t, itemsize, rows, name, tail=None):
+    """Validate a caller-supplied cuda tensor before its pointer crosses the C
+    ABI: cuda device, contiguous, element size, >= rows leading entries and
+    the expected trailing shape (the kernels trust these)."""
+    if not getattr(t, "is_cuda", False):
+        raise OrbxError(ERR_ARG, "%s: cuda tensor expected" % name)
+    if not t.is_contiguous():
+        raise OrbxError(ERR_ARG, "%s: contiguous tensor expected" % name)
+    if itemsize is not None and t.element_size() != itemsize:
+        raise OrbxError(ERR_ARG, "%s: element size %d expected" % (name, itemsize))
+    if t.dim() < 1 or t.shape[0] < rows:
+        raise OrbxError(ERR_ARG, "%s: at least %d rows expected" % (name, rows))
+    if tail is not None and tuple(t.shape[1:]) != tuple(tail):
+        raise OrbxError(ERR_ARG, "%s: shape [*, %s] expected, got %s"
+                        % (name, ", ".join(map(str, tail)), tuple(t.shape)))
+
+
 def _stream_handle(stream):
     if stream is None:
         import torch
@@ -496,7 +513,10 @@ class Plan:
         assert frames.dtype.itemsize == 1 and frames.is_contiguous()
         assert frames.shape[1] == self.H and frames.shape[2] == self.W and B <= self.max_batch
         kps, desc, counts = out if out is not None else (self.kps, self.desc, self.counts)
-        assert kps.shape[1] == self.kcap and desc.shape[1] == self.kcap
+        _check_dev(frames, None, B, "frames")
+        _check_dev(kps, 1, B, "kps", (self.kcap, 28))
+        _check_dev(desc, 1, B, "desc", (self.kcap, 32))
+        _check_dev(counts, 4, B, "counts")
         _check(_lib.orbx_plan_extract(self._h, frames.data_ptr(), B, self.W * self.H, self.W,
                                       kps.data_ptr(), desc.data_ptr(), counts.data_ptr(),
                                       _stream_handle(stream)), "orbx_plan_extract")
@@ -547,6 +567,14 @@ class MatchPlan:
 
     def match(self, npairs, kps_a, desc_a, cnt_a, kps_b, desc_b, cnt_b, nnratio=0.6,
               check_ori=True, stream=None, out_offset=0):
+        if npairs < 1 or out_offset < 0 or npairs + out_offset > self.max_pairs:
+            raise OrbxError(ERR_ARG, "MatchPlan.match: npairs %d + out_offset %d > max_pairs %d"
+                            % (npairs, out_offset, self.max_pairs))
+        for t, name, shape in ((kps_a, "kps_a", (self.kcap, 28)), (desc_a, "desc_a", (self.kcap, 32)),
+                               (kps_b, "kps_b", (self.kcap, 28)), (desc_b, "desc_b", (self.kcap, 32))):
+            _check_dev(t, 1, npairs, name, shape)
+        _check_dev(cnt_a, 4, npairs, "cnt_a")
+        _check_dev(cnt_b, 4, npairs, "cnt_b")
         m = self.match12[out_offset:]
         nm = self.nmatches[out_offset:]
         _check(_lib.orbm_plan_match_frames(self._h, npairs, kps_a.data_ptr(), desc_a.data_ptr(),
@@ -590,8 +618,17 @@ class StereoPlan:
               stream=None):
         """frames_*: the cuda [B, H, W] tensors the plans last extracted.  Async."""
         B = frames_l.shape[0]
+        if B > self.max_batch or frames_r.shape[0] < B:
+            raise OrbxError(ERR_ARG, "StereoPlan.match: batch %d > max_batch %d" % (B, self.max_batch))
+        _check_dev(frames_l, 1, B, "frames_l", (left.H, left.W))
+        _check_dev(frames_r, 1, B, "frames_r", (left.H, left.W))
         kl, dl, cl = left_out if left_out is not None else (left.kps, left.desc, left.counts)
         kr, dr, cr = right_out if right_out is not None else (right.kps, right.desc, right.counts)
+        for t, name, shape in ((kl, "kps_l", (self.kcap, 28)), (dl, "desc_l", (self.kcap, 32)),
+                               (kr, "kps_r", (self.kcap, 28)), (dr, "desc_r", (self.kcap, 32))):
+            _check_dev(t, 1, B, name, shape)
+        _check_dev(cl, 4, B, "counts_l")
+        _check_dev(cr, 4, B, "counts_r")
         _check(_lib.orbs_plan_match(self._h, B, left._h, right._h, frames_l.data_ptr(),
                                     frames_r.data_ptr(), left.W * left.H, left.W, kl.data_ptr(),
                                     dl.data_ptr(), cl.data_ptr(), kr.data_ptr(), dr.data_ptr(),

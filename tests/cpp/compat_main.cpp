@@ -1,0 +1,151 @@
+// Call sites shaped like the reference's, compiled against
+// orb-slam-system_amd/cpp/orbslam2_compat.hpp (ORB_SLAM2::ORBextractor /
+// ORBmatcher with the reference signatures, cv:: subset):
+//   * Frame::ExtractORB (src/Frame.cc:227-233) called from the two stereo
+//     threads of Frame::Frame (src/Frame.cc:58-61),
+//   * concurrently with LoopClosing's SearchByBoW(KF, KF) (src/LoopClosing.cc:149)
+//     on a third thread,
+// repeated; every repetition must give identical outputs.  The first one is
+// written for tests/test_cpp_adapter.py to check against the oracle.
+//   compat_main left.raw right.raw c.raw d.raw W H nfeatures reps out.bin
+#include <stdio.h>
+#include <stdlib.h>
+
+#include <map>
+#include <thread>
+#include <vector>
+
+#include "orbslam2_compat.hpp"
+
+using namespace ORB_SLAM2;
+
+// test stand-ins for the out-of-scope map classes: only the members
+// ORBmatcher::SearchByBoW reads (KeyFrame.h / MapPoint.h)
+struct TMapPoint {
+  bool bad = false;
+  bool isBad() { return bad; }
+};
+struct TKeyFrame {
+  std::vector<TMapPoint*> mvpMapPoints;
+  std::vector<cv::KeyPoint> mvKeysUn;
+  std::map<unsigned int, std::vector<unsigned int>> mFeatVec;  // DBoW2::FeatureVector
+  cv::Mat mDescriptors;
+  std::vector<TMapPoint*> GetMapPointMatches() { return mvpMapPoints; }
+};
+
+// shaped like the reference's Frame (src/Frame.cc:41-97, 227-233)
+struct TFrame {
+  ORBextractor *mpORBextractorLeft, *mpORBextractorRight;
+  std::vector<cv::KeyPoint> mvKeys, mvKeysRight;
+  cv::Mat mDescriptors, mDescriptorsRight;
+  int N = 0;
+  void ExtractORB(int flag, const cv::Mat& im) {
+    if (flag == 0)
+      (*mpORBextractorLeft)(im, cv::Mat(), mvKeys, mDescriptors);
+    else
+      (*mpORBextractorRight)(im, cv::Mat(), mvKeysRight, mDescriptorsRight);
+  }
+  TFrame(const cv::Mat& imLeft, const cv::Mat& imRight, ORBextractor* l, ORBextractor* r)
+      : mpORBextractorLeft(l), mpORBextractorRight(r) {
+    std::thread threadLeft(&TFrame::ExtractORB, this, 0, imLeft);
+    std::thread threadRight(&TFrame::ExtractORB, this, 1, imRight);
+    threadLeft.join();
+    threadRight.join();
+    N = (int)mvKeys.size();
+  }
+};
+
+static std::vector<uint8_t> load(const char* p, size_t n) {
+  std::vector<uint8_t> v(n);
+  FILE* f = fopen(p, "rb");
+  if (!f || fread(v.data(), 1, n, f) != n) { fprintf(stderr, "read %s\n", p); exit(2); }
+  fclose(f);
+  return v;
+}
+
+static void make_kf(ORBextractor& ex, const cv::Mat& im, TKeyFrame& kf, std::vector<TMapPoint>& store) {
+  ex(im, cv::Mat(), kf.mvKeysUn, kf.mDescriptors);
+  const size_t n = kf.mvKeysUn.size();
+  store.resize(n);
+  kf.mvpMapPoints.assign(n, nullptr);
+  for (size_t i = 0; i < n; ++i) {
+    store[i].bad = (i % 11) == 5;
+    if (i % 7 != 3) kf.mvpMapPoints[i] = &store[i];
+    kf.mFeatVec[(unsigned)(4 * (i % 5) + 3)].push_back((unsigned)i);  // 5 vocabulary nodes
+  }
+}
+
+int main(int argc, char** argv) {
+  if (argc != 10) return 2;
+  const int W = atoi(argv[5]), H = atoi(argv[6]), nf = atoi(argv[7]), reps = atoi(argv[8]);
+  std::vector<uint8_t> bl = load(argv[1], (size_t)W * H), br = load(argv[2], (size_t)W * H),
+                       bc = load(argv[3], (size_t)W * H), bd = load(argv[4], (size_t)W * H);
+  cv::Mat L(H, W, CV_8UC1, bl.data()), R(H, W, CV_8UC1, br.data()), C(H, W, CV_8UC1, bc.data()),
+      D(H, W, CV_8UC1, bd.data());
+  // Tracking::Tracking (src/Tracking.cc:76-79)
+  ORBextractor* left = new ORBextractor(nf, 1.2f, 8, 20, 7);
+  ORBextractor* right = new ORBextractor(nf, 1.2f, 8, 20, 7);
+  ORBextractor kfex(nf, 1.2f, 8, 20, 7);
+  TKeyFrame kf1, kf2;
+  std::vector<TMapPoint> mp1, mp2;
+  make_kf(kfex, C, kf1, mp1);
+  make_kf(kfex, D, kf2, mp2);
+  std::vector<cv::KeyPoint> k0L, k0R;
+  std::vector<uint8_t> d0L, d0R;
+  std::vector<int> m0;
+  int nm0 = -1;
+  for (int rep = 0; rep < reps; ++rep) {
+    std::vector<TMapPoint*> matches;
+    int nm = -1;
+    // LoopClosing thread: SearchByBoW while the stereo frame is extracted
+    std::thread loop([&] {
+      ORBmatcher matcher(0.75, true);  // LoopClosing.cc:129
+      for (int i = 0; i < 3; ++i) nm = matcher.SearchByBoW(&kf1, &kf2, matches);
+    });
+    TFrame frame(L, R, left, right);
+    loop.join();
+    std::vector<int> m(matches.size(), -1);
+    for (size_t i = 0; i < matches.size(); ++i)
+      if (matches[i]) m[i] = (int)(matches[i] - mp2.data());
+    auto flat = [](const cv::Mat& d) {
+      return d.empty() ? std::vector<uint8_t>() : std::vector<uint8_t>(d.data, d.data + (size_t)d.rows * 32);
+    };
+    if (rep == 0) {
+      k0L = frame.mvKeys;
+      k0R = frame.mvKeysRight;
+      d0L = flat(frame.mDescriptors);
+      d0R = flat(frame.mDescriptorsRight);
+      m0 = m;
+      nm0 = nm;
+    } else if (frame.mvKeys.size() != k0L.size() || frame.mvKeysRight.size() != k0R.size() ||
+               memcmp(frame.mvKeys.data(), k0L.data(), k0L.size() * sizeof(cv::KeyPoint)) ||
+               memcmp(frame.mvKeysRight.data(), k0R.data(), k0R.size() * sizeof(cv::KeyPoint)) ||
+               flat(frame.mDescriptors) != d0L || flat(frame.mDescriptorsRight) != d0R || m != m0 ||
+               nm != nm0) {
+      fprintf(stderr, "repetition %d differs\n", rep);
+      return 3;
+    }
+  }
+  // DescriptorDistance (static, cv::Mat rows) as Frame.cc:521 calls it
+  const int dist = ORBmatcher::DescriptorDistance(cv::Mat(1, 32, CV_8U, d0L.data()),
+                                                  cv::Mat(1, 32, CV_8U, d0R.data()));
+  const std::vector<float> sc = left->GetScaleFactors();
+  FILE* o = fopen(argv[9], "wb");
+  int hdr[5] = {(int)k0L.size(), (int)k0R.size(), (int)m0.size(), nm0, dist};
+  fwrite(hdr, sizeof(int), 5, o);
+  fwrite(k0L.data(), sizeof(cv::KeyPoint), k0L.size(), o);
+  fwrite(d0L.data(), 1, d0L.size(), o);
+  fwrite(k0R.data(), sizeof(cv::KeyPoint), k0R.size(), o);
+  fwrite(d0R.data(), 1, d0R.size(), o);
+  fwrite(m0.data(), sizeof(int), m0.size(), o);
+  fwrite(sc.data(), sizeof(float), sc.size(), o);
+  const cv::Mat& top = left->mvImagePyramid[7];
+  int tw[2] = {top.cols, top.rows};
+  fwrite(tw, sizeof(int), 2, o);
+  for (int r = 0; r < top.rows; ++r) fwrite(top.ptr(r), 1, top.cols, o);
+  fclose(o);
+  delete left;
+  delete right;
+  printf("compat ok: %d reps, L=%zu R=%zu matches=%d\n", reps, k0L.size(), k0R.size(), nm0);
+  return 0;
+}

@@ -141,3 +141,74 @@ def test_cpp_vocab_adapter_matches_oracle(gpu, oracle, tmp_path):
     kf2 = dict(desc=d2, angle=k2["angle"], valid=None, **rfv2)
     rm, rnm = oracle.search_by_bow(kf1, kf2, 0.75, True)
     assert nm == rnm and np.array_equal(m12, rm)
+
+
+def _build_compat(tmp_path):
+    exe = tmp_path / "compat_main"
+    subprocess.check_call(["g++", "-O2", "-std=c++17", "-Wall", "-pthread", "-I",
+                           os.path.join(PKG, "cpp"), os.path.join(ROOT, "tests", "cpp", "compat_main.cpp"),
+                           "-o", str(exe), "-L", PKG, "-lorbx", "-Wl,-rpath," + PKG])
+    return exe
+
+
+def test_reference_shaped_call_sites_compile(tmp_path):
+    """Frame::ExtractORB / Frame::Frame's stereo threads / LoopClosing's
+    SearchByBoW / DescriptorDistance(cv::Mat, cv::Mat) written as in the
+    reference compile against cpp/orbslam2_compat.hpp."""
+    assert _build_compat(tmp_path).exists()
+
+
+def _compat_featvec(n):
+    nodes = [4 * j + 3 for j in range(5)]
+    feat, off = [], [0]
+    for j in range(5):
+        feat.extend(i for i in range(n) if i % 5 == j)
+        off.append(len(feat))
+    return np.array(nodes, np.uint32), np.array(off, np.uint32), np.array(feat, np.uint32)
+
+
+@pytest.mark.gpu
+def test_reference_shaped_concurrent_call_sites(gpu, oracle, tmp_path):
+    """Two ORB_SLAM2::ORBextractor instances on the two stereo threads of a
+    Frame-shaped constructor, concurrently with SearchByBoW(KF, KF) on a third
+    thread, 6 repetitions (each identical to the first, checked in C++), all
+    bit-exact against the oracle."""
+    exe = _build_compat(tmp_path)
+    W, H, nf = 752, 480, 1200
+    L, R = synth.stereo_pair(W, H, 70)
+    c, d = synth.frame(W, H, 80, "pan"), synth.frame(W, H, 81, "pan")
+    paths = []
+    for name, im in (("l", L), ("r", R), ("c", c), ("d", d)):
+        (tmp_path / (name + ".raw")).write_bytes(np.ascontiguousarray(im).tobytes())
+        paths.append(str(tmp_path / (name + ".raw")))
+    out = tmp_path / "out.bin"
+    subprocess.check_call([str(exe)] + paths + [str(W), str(H), str(nf), "6", str(out)], timeout=120)
+    raw = out.read_bytes()
+    nl, nr, n1, nm, dist = np.frombuffer(raw[:20], np.int32).tolist()
+    off = 20
+    kl = np.frombuffer(raw[off:off + 28 * nl], oracle.KEYPOINT_DTYPE); off += 28 * nl
+    dl = np.frombuffer(raw[off:off + 32 * nl], np.uint8).reshape(nl, 32); off += 32 * nl
+    kr = np.frombuffer(raw[off:off + 28 * nr], oracle.KEYPOINT_DTYPE); off += 28 * nr
+    dr = np.frombuffer(raw[off:off + 32 * nr], np.uint8).reshape(nr, 32); off += 32 * nr
+    m12 = np.frombuffer(raw[off:off + 4 * n1], np.int32); off += 4 * n1
+    sc = np.frombuffer(raw[off:off + 32], np.float32); off += 32
+    tw, th = np.frombuffer(raw[off:off + 8], np.int32).tolist(); off += 8
+    top = np.frombuffer(raw[off:off + tw * th], np.uint8).reshape(th, tw)
+    e = oracle.Extractor(nf, 1.2, 8, 20, 7)
+    rkr, rdr = e.extract(R)
+    rkl, rdl = e.extract(L)
+    assert np.array_equal(top, e.level(7))  # mvImagePyramid after the left frame
+    assert np.array_equal(kl.view(np.uint8), rkl.view(np.uint8)) and np.array_equal(dl, rdl)
+    assert np.array_equal(kr.view(np.uint8), rkr.view(np.uint8)) and np.array_equal(dr, rdr)
+    assert np.array_equal(sc, e.tables()["scale"])
+    assert dist == oracle.descriptor_distance(rdl[0], rdr[0])
+    kc, dc = e.extract(c)
+    kd, dd = e.extract(d)
+
+    def kf(k, dsc):
+        n = len(k)
+        ids, offs, feat = _compat_featvec(n)
+        valid = np.array([(i % 7 != 3) and (i % 11 != 5) for i in range(n)], np.uint8)
+        return dict(desc=dsc, angle=k["angle"], valid=valid, node_id=ids, off=offs, feat=feat)
+    rm, rnm = oracle.search_by_bow(kf(kc, dc), kf(kd, dd), 0.75, True)
+    assert nm == rnm and nm > 0 and np.array_equal(m12, rm)
