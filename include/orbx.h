@@ -160,6 +160,10 @@ int orbx_synth_frames(uint8_t* d_frames, int width, int height, size_t frame_str
  * the (sin, cos) k_orient_brief uses for angle x[i] -- glibc sincosf
  * (ORBextractor.cc:58-59) wherever it moves a BRIEF sample (orbx_sincos.h). */
 int orbx_selftest_sincos(const float* d_x, int n, float* d_sc, void* stream);
+/* Same (sin, cos) for the n consecutive float bit patterns first_bits ..
+ * first_bits + n - 1, lane-parallel, into host memory sc[2n] (synchronous):
+ * the exhaustive device check of every reachable BRIEF angle. */
+int orbx_selftest_sincos_range(uint32_t first_bits, int n, float* sc, int device);
 
 /* ---------------------------------------------------------------------------
  * ORBmatcher drop-in.

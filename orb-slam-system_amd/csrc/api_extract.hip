@@ -28,6 +28,7 @@ __global__ void k_orient_brief(const uint8_t*, size_t, size_t, const uint8_t*, s
                                orbx_keypoint*, uint8_t*, int*, int);
 __global__ void k_synth(uint8_t*, int, int, size_t, int, int);
 __global__ void k_selftest_sincos(const float*, int, float*);
+__global__ void k_selftest_sincos_range(uint32_t, int, float*);
 }  // namespace orbx
 
 using namespace orbx;
@@ -363,6 +364,25 @@ extern "C" int orbx_selftest_sincos(const float* d_x, int n, float* d_sc, void* 
   if (n == 0) return ORBX_OK;
   hipLaunchKernelGGL(k_selftest_sincos, dim3(n), dim3(64), 0, (hipStream_t)stream, d_x, n, d_sc);
   return hipGetLastError() == hipSuccess ? ORBX_OK : ORBX_ERR_HIP;
+}
+
+extern "C" int orbx_selftest_sincos_range(uint32_t first_bits, int n, float* sc, int device) {
+  if (n < 0 || (n > 0 && !sc)) return ORBX_ERR_ARG;
+  if (n == 0) return ORBX_OK;
+  if (device < 0 || device >= orbx_device_count()) return ORBX_ERR_NO_DEVICE;
+  ORBX_TRY(hipSetDevice(device));
+  WsLease L(device);
+  CallWs* w = L.w;
+  if (!w) return ORBX_ERR_HIP;
+  const size_t bytes = (size_t)n * 8;
+  int rc = w->reserve(bytes, 0);
+  if (rc) return rc;
+  hipLaunchKernelGGL(k_selftest_sincos_range, dim3((n + 255) / 256), dim3(256), 0, w->stream,
+                     first_bits, n, reinterpret_cast<float*>(w->d));
+  if (hipGetLastError() != hipSuccess) return ORBX_ERR_HIP;
+  ORBX_TRY(hipMemcpyAsync(sc, w->d, bytes, hipMemcpyDeviceToHost, w->stream));
+  ORBX_TRY(hipStreamSynchronize(w->stream));
+  return ORBX_OK;
 }
 
 // ---------------------------------------------------------------------------

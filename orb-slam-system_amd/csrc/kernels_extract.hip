@@ -1345,4 +1345,28 @@ __global__ __launch_bounds__(64) void k_selftest_sincos(const float* __restrict_
   }
 }
 
+// k_selftest_sincos_range: the BRIEF sin/cos of consecutive float bit
+// patterns, lane-parallel (orbx_sincos_core + the exception table, looked up
+// by binary search -- the same table brief_sincos consults by ballot), for
+// the exhaustive device check over every reachable angle
+// (tests/test_sincos_gpu.py::test_device_sincos_exhaustive).
+__global__ __launch_bounds__(256) void k_selftest_sincos_range(uint32_t first, int n,
+                                                               float* __restrict__ sc) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t b = first + (uint32_t)i;
+  float s, c;
+  orbx_sincos_core(orbx_u2f(b), &s, &c);
+  int lo = 0, hi = ORBX_SINCOS_NEXC;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (ORBX_SINCOS_EXC[mid][0] < b) lo = mid + 1; else hi = mid;
+  }
+  if (lo < ORBX_SINCOS_NEXC && ORBX_SINCOS_EXC[lo][0] == b) {
+    s = orbx_u2f(ORBX_SINCOS_EXC[lo][1]);
+    c = orbx_u2f(ORBX_SINCOS_EXC[lo][2]);
+  }
+  reinterpret_cast<float2*>(sc)[i] = make_float2(s, c);
+}
+
 }  // namespace orbx

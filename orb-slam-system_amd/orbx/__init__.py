@@ -56,6 +56,7 @@ EXPORTED = [
     "orbv_vocab_load_text", "orbv_vocab_create", "orbv_vocab_destroy", "orbv_vocab_info",
     "orbv_transform", "orbv_transform_batch", "orbv_check", "orbm_search_by_projection",
     "orbm_compute_distinctive_descriptors", "orbx_undistort_keypoints", "orbx_selftest_sincos",
+    "orbx_selftest_sincos_range",
 ]
 
 
@@ -151,6 +152,7 @@ _sig = {
     "orbm_compute_distinctive_descriptors": (I, [P, P, I, I, P]),
     "orbx_undistort_keypoints": (I, [P, I, P, P, I, I, P]),
     "orbx_selftest_sincos": (I, [P, I, P, P]),
+    "orbx_selftest_sincos_range": (I, [ctypes.c_uint32, I, P, I]),
 }
 for _n, (_r, _a) in _sig.items():
     _f = getattr(_lib, _n)

@@ -109,3 +109,38 @@ def test_device_sincos_matches_table_and_core(gpu):
             want = tuple(map(_bits, sincos_core(np.uint32(b).view(np.float32))))
         assert (int(got[i, 0]), int(got[i, 1])) == want, \
             "x=0x%08x: device (0x%08x, 0x%08x) vs (0x%08x, 0x%08x)" % (b, got[i, 0], got[i, 1], *want)
+
+
+def _build_exhaustive(tmp_path):
+    import subprocess
+    exe = tmp_path / "sincos_exhaustive"
+    pkg = os.path.join(ROOT, "orb-slam-system_amd")
+    subprocess.check_call(["g++", "-O2", "-std=c++17", "-pthread", "-ffp-contract=off", "-I",
+                           os.path.join(ROOT, "include"),
+                           os.path.join(ROOT, "tests", "cpp", "sincos_exhaustive.cpp"), "-o", str(exe),
+                           "-L", pkg, "-lorbx", "-Wl,-rpath," + pkg])
+    return exe
+
+
+def test_exhaustive_checker_compiles(tmp_path):
+    assert _build_exhaustive(tmp_path).exists()
+
+
+@pytest.mark.gpu
+def test_device_sincos_exhaustive(gpu, tmp_path):
+    """Every float angle in [0, f32(360*factorPI)] (1.09e9 inputs): the device
+    (sin, cos) gives the same 364 live BRIEF sample positions as this host's
+    glibc sincosf.  Summary -> gpurun_out/ when run on the
+    GPU box (committed under profiles/)."""
+    import json
+    import subprocess
+    exe = _build_exhaustive(tmp_path)
+    out = tmp_path / "sincos.json"
+    r = subprocess.run([str(exe), str(out), "16"], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout + r.stderr
+    res = json.loads(out.read_text())
+    assert res["inputs"] == 0x40c90fdb + 1 and res["position_changing"] == 0
+    dst = os.path.join(ROOT, "gpurun_out")
+    if os.path.isdir(dst):
+        with open(os.path.join(dst, "sincos_exhaustive.json"), "w") as f:
+            f.write(out.read_text())
