@@ -1005,12 +1005,40 @@ __device__ __forceinline__ void brief_sincos(float x, uint32_t exk0, uint32_t ex
   }
 }
 
+// 7-tap Gaussian (OpenCV 8U fixed point, sigma 2): [18,34,48,56,48,34,18]
+__device__ constexpr uint32_t kb_tap(int i) {
+  return i == 0 || i == 6 ? 18u : i == 1 || i == 5 ? 34u : i == 2 || i == 4 ? 48u : 56u;
+}
+// weight dword d (bytes 4d..4d+3 of a 12-byte window) with k0..k6 at bytes
+// m+1..m+7: the horizontal pass's output column 4q+m over dwords q-1..q+1
+__device__ constexpr uint32_t kb_w(int m, int d) {
+  uint32_t w = 0;
+  for (int b = 0; b < 4; ++b) {
+    const int i = 4 * d + b - (m + 1);
+    if (i >= 0 && i <= 6) w |= kb_tap(i) << (8 * b);
+  }
+  return w;
+}
+// vertical pairs (lo = first row, hi = second row) for taps starting at the
+// low half (E) or the high half (O) of the first row pair
+#define KV_PAIR(a, b) ((uint32_t)(a) | ((uint32_t)(b) << 16))
+#define KV_E0 KV_PAIR(18, 34)
+#define KV_E1 KV_PAIR(48, 56)
+#define KV_E2 KV_PAIR(48, 34)
+#define KV_E3 KV_PAIR(18, 0)
+#define KV_O0 KV_PAIR(0, 18)
+#define KV_O1 KV_PAIR(34, 48)
+#define KV_O2 KV_PAIR(56, 48)
+#define KV_O3 KV_PAIR(34, 18)
+
 // Keypoint patch: rows y-21..y+21, 48 columns from (x-21) & ~3 (a multiple of
 // 4 in level coordinates; the row addresses need not be dword aligned);
 // covers IC_Angle's radius-15 disk and every blur tap of the radius-18 samples.
 #define KP_R 21
 #define KP_ROWS 43
 #define KP_COLS 48
+#define KP_HCOLS 44  /* hblur columns: patch columns 0..43 (samples use cc-18..cc+18 <= 42) */
+#define KP_HPAIRS 22 /* hblur row pairs: rows 0..43 (row 43 never weighted) */
 
 // One keypoint of the frame's level-major output list: where its level
 // lives and where its patch starts (all wave-uniform).
@@ -1089,6 +1117,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OB_WPE))) v
     orbx_keypoint* __restrict__ kps, uint8_t* __restrict__ desc, int* __restrict__ counts,
     int dbg) {
   __shared__ uint32_t patch[4][KP_ROWS][KP_COLS / 4];
+  // horizontally blurred patch, column-major: hblur[w][patch col][row pair]
+  // = (H(row 2k), H(row 2k+1)) as u16 pair, H = sum_i k_i p (7 taps)
+  __shared__ uint32_t hblur[4][KP_HCOLS][KP_HPAIRS];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int f = blockIdx.y;
   const int g = blockIdx.x * 4 + wave;
@@ -1201,16 +1232,37 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OB_WPE))) v
   const float factorPI = (float)(3.1415926535897932384626433832795 / 180.f);
   float sn, cs;
   brief_sincos(angle * factorPI, exk0, exk1, &sn, &cs);
-  // BRIEF (:57-73) on GaussianBlur(7x7, sigma 2) evaluated at each sample:
-  // out = (sum_j k_j * (sum_i k_i p) + 32768) >> 16, rows via v_dot4_u32_u8
-  const uint32_t K0 = 18u | (34u << 8) | (48u << 16) | (56u << 24), K1 = 48u | (34u << 8) | (18u << 16);
-  // Only pairs 0..181 carry information: the reference table has 728
-  // initialisers (ORBextractor.cc:75-113), so pairs 182..255 are {0,0,0,0},
-  // compare the centre with itself and give 0 bits.  Rounds of 64 pairs
-  // needed: 3 (pairs 182..191 of round 2 still evaluate to 0); round 3
-  // (bytes 24..31) is the constant 0 and is not evaluated.
-  static_assert(ORBX_BRIEF_INITIALISED_INTS <= 3 * 64 * 4,
-                "pattern has live pairs past 191: evaluate all four rounds");
+  // BRIEF (:57-73) on GaussianBlur(7x7, sigma 2): separable and exact,
+  // out = (sum_j k_j H(r+j-3) + 32768) >> 16 with H = sum_i k_i p(c+i-3)
+  // (OpenCV's fixed-point 8U path, [18,34,48,56,48,34,18]).  The horizontal
+  // pass runs once per keypoint over the patch (hblur, column-major, row
+  // pairs packed as u16 x 2); each of the 364 live samples is then 4 dword
+  // reads + 4 v_dot2_u32_u16 down its hblur column -- 64 LDS ops per keypoint
+  // instead of 21 dword reads per sample (126).
+  {
+    // task = (row pair rp, 4-column group q): patch columns 4q..4q+3, rows
+    // 2rp, 2rp+1; the 7-byte windows c-3..c+3 lie in dwords q-1..q+1
+    const int qlo = (cc - 18) >> 2, qhi = (cc + 18) >> 2, nq = qhi - qlo + 1;
+    const int ntask = KP_HPAIRS * nq;
+    for (int t = lane; t < ntask; t += 64) {
+      const int rp = t / nq, q = qlo + t - rp * nq;
+      const int r0 = 2 * rp, r1 = min(2 * rp + 1, KP_ROWS - 1);
+      const int d0 = max(q - 1, 0);  // q == 0: the weights of dword q-1 are 0 for the columns used
+      const uint32_t a0 = P[r0][d0], a1 = P[r0][q], a2 = P[r0][q + 1];
+      const uint32_t b0 = P[r1][d0], b1 = P[r1][q], b2 = P[r1][q + 1];
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        // taps k0..k6 at window bytes m+1..m+7 of the 12 bytes a0|a1|a2
+        const uint32_t W0 = kb_w(m, 0), W1 = kb_w(m, 1), W2 = kb_w(m, 2);
+        const uint32_t h0 = __builtin_amdgcn_udot4(a2, W2, __builtin_amdgcn_udot4(a1, W1, __builtin_amdgcn_udot4(a0, W0, 0u, false), false), false);
+        const uint32_t h1 = __builtin_amdgcn_udot4(b2, W2, __builtin_amdgcn_udot4(b1, W1, __builtin_amdgcn_udot4(b0, W0, 0u, false), false), false);
+        hblur[wave][4 * q + m][rp] = h0 | (h1 << 16);
+      }
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   uint64_t words[4] = {0, 0, 0, 0};
 #pragma unroll
   for (int rr = 0; rr < 3; ++rr) {
@@ -1223,26 +1275,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OB_WPE))) v
       const float ya = fy * cs, yb = fy * sn;
       const int row = (int)__builtin_rintf(__builtin_fmaf(fx, sn, ya));
       const int col = (int)__builtin_rintf(__builtin_fmaf(fx, cs, -yb));
-      const int r0 = cr + row - 3, c0 = cc + col - 3;
-      const int qd = c0 >> 2, sh = c0 & 3;  // window = bytes sh..sh+6 of dwords qd..qd+2
-      const uint32_t* prow = &P[0][0] + __mul24(r0, KP_COLS / 4) + qd;  // |r0| < 64: 24-bit multiply
-      // the 7 taps shifted to the window's byte offset: three weight words
-      // over the three aligned dwords (no v_alignbyte); rows j and 6-j share
-      // their vertical weight, so their horizontal sums chain into one dot4
-      // accumulation: 21 v_dot4 + 4 multiplies per sample instead of
-      // 14 v_alignbyte + 14 v_dot4 + 7 multiplies
-      const uint64_t Kw = (((uint64_t)K1 << 32) | K0) << (8 * sh);
-      const uint32_t K0s = (uint32_t)Kw, K1s = (uint32_t)(Kw >> 32);
-      const uint32_t K2s = (uint32_t)(((uint64_t)K1 << (8 * sh)) >> 32);
-      auto hrow = [&](int jj, uint32_t a) {
-        a = __builtin_amdgcn_udot4(prow[jj * (KP_COLS / 4)], K0s, a, false);
-        a = __builtin_amdgcn_udot4(prow[jj * (KP_COLS / 4) + 1], K1s, a, false);
-        return __builtin_amdgcn_udot4(prow[jj * (KP_COLS / 4) + 2], K2s, a, false);
-      };
-      uint32_t acc = __umul24(hrow(3, 0u), 56u);
-      acc = __umul24(hrow(6, hrow(0, 0u)), 18u) + acc;
-      acc = __umul24(hrow(5, hrow(1, 0u)), 34u) + acc;
-      acc = __umul24(hrow(4, hrow(2, 0u)), 48u) + acc;
+      const int rt = cr + row - 3;  // first vertical tap (patch row)
+      const uint32_t* hc = &hblur[wave][cc + col][rt >> 1];
+      const uint32_t v0 = hc[0], v1 = hc[1], v2 = hc[2], v3 = hc[3];
+      // row pairs (2k, 2k+1): taps rt..rt+6 start at the pair's low half
+      // (rt even) or high half (rt odd)
+      const bool odd = rt & 1;
+      uint32_t acc = __builtin_amdgcn_udot2(as_us2(v0), as_us2(odd ? KV_O0 : KV_E0), 0u, false);
+      acc = __builtin_amdgcn_udot2(as_us2(v1), as_us2(odd ? KV_O1 : KV_E1), acc, false);
+      acc = __builtin_amdgcn_udot2(as_us2(v2), as_us2(odd ? KV_O2 : KV_E2), acc, false);
+      acc = __builtin_amdgcn_udot2(as_us2(v3), as_us2(odd ? KV_O3 : KV_E3), acc, false);
       t[e] = (int)min((acc + 32768u) >> 16, 255u);
     }
     words[rr] = __ballot(t[0] < t[1]);

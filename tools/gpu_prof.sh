@@ -4,4 +4,3 @@ cd $GRAFT_REPO_ROOT
 TAG=${1:-run}
 bash tools/profile.sh $TAG || exit $?
 bash tools/pmc_sq.sh $TAG || exit $?
-python3 tools/pmc_traffic.py gpurun_out/prof_$TAG gpurun_out/prof_$TAG/traffic.json > /dev/null

@@ -25,6 +25,9 @@ STAGE_OF = {
     "k_match_resolve_spec": "match_resolve",
     "k_match_resolve": "match_resolve",
     "k_match_finalize": "match_finalize",
+    "k_stereo_rows": "stereo_rows",
+    "k_stereo_match": "stereo_match",
+    "k_stereo_filter": "stereo_filter",
 }
 
 
