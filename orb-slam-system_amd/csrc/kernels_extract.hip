@@ -989,6 +989,18 @@ __device__ __forceinline__ float fast_atan2(float y, float x) {
   return a;
 }
 
+// Sum over the wave, returned wave-uniform: inclusive row scans by DPP
+// row_shr 1/2/4/8 (16-lane rows, out-of-row sources read 0), then the four
+// row totals (lanes 15, 31, 47, 63) by readlane -- no ds_bpermute round trips.
+__device__ __forceinline__ int wave_sum_dpp(int x) {
+  x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, true);
+  x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, true);
+  x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xf, true);
+  x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xf, true);
+  return __builtin_amdgcn_readlane(x, 15) + __builtin_amdgcn_readlane(x, 31) +
+         __builtin_amdgcn_readlane(x, 47) + __builtin_amdgcn_readlane(x, 63);
+}
+
 // x is wave-uniform.  The exception keys live in two VGPRs per lane
 // (entries lane and lane + 64, loaded once per wave), so the lookup is two
 // compares and a ballot -- no chain of dependent scalar loads; the rare hit
@@ -1151,7 +1163,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OB_WPE))) v
   // keypoint's patch (vmcnt stays exact; nothing waits on it early).
   auto locate = [&](int o) {
     const int l = __builtin_amdgcn_readfirstlane(__popcll(__ballot(lane < nlevels && incl <= o)));
-    const int i = o - __builtin_amdgcn_readfirstlane(__shfl(excl, l, 64));
+    const int i = o - __builtin_amdgcn_readlane(excl, l);  // l is uniform
     const uint32_t key = __builtin_amdgcn_readfirstlane(Q[A.kout_off[l] + i]);
     BriefKp k;
     k.l = l;
@@ -1191,6 +1203,36 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OB_WPE))) v
     brief_issue(cur, R, lane);
   }
   const int l = me.l, x = me.x, score = me.score, px0 = me.px0;
+  // BRIEF (:57-73) on GaussianBlur(7x7, sigma 2): separable and exact,
+  // out = (sum_j k_j H(r+j-3) + 32768) >> 16 with H = sum_i k_i p(c+i-3)
+  // (OpenCV's fixed-point 8U path, [18,34,48,56,48,34,18]).  The horizontal
+  // pass runs once per keypoint over the patch (hblur, column-major, row
+  // pairs packed as u16 x 2); each of the 364 live samples is then 4 dword
+  // reads + 4 v_dot2_u32_u16 down its hblur column -- 64 LDS ops per keypoint
+  // instead of 21 dword reads per sample (126).  It runs before IC_Angle so
+  // its LDS writes drain while the angle and sin/cos are computed.
+  {
+    // task = (row pair rp, 4-column group q): patch columns 4q..4q+3, rows
+    // 2rp, 2rp+1; the 7-byte windows c-3..c+3 lie in dwords q-1..q+1
+    const int cc = me.x - me.px0;
+    const int qlo = (cc - 18) >> 2, qhi = (cc + 18) >> 2, nq = qhi - qlo + 1;
+    const int ntask = KP_HPAIRS * nq;
+    for (int t = lane; t < ntask; t += 64) {
+      const int rp = t / nq, q = qlo + t - rp * nq;
+      const int r0 = 2 * rp, r1 = min(2 * rp + 1, KP_ROWS - 1);
+      const int d0 = max(q - 1, 0);  // q == 0: the weights of dword q-1 are 0 for the columns used
+      const uint32_t a0 = P[r0][d0], a1 = P[r0][q], a2 = P[r0][q + 1];
+      const uint32_t b0 = P[r1][d0], b1 = P[r1][q], b2 = P[r1][q + 1];
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        // taps k0..k6 at window bytes m+1..m+7 of the 12 bytes a0|a1|a2
+        const uint32_t W0 = kb_w(m, 0), W1 = kb_w(m, 1), W2 = kb_w(m, 2);
+        const uint32_t h0 = __builtin_amdgcn_udot4(a2, W2, __builtin_amdgcn_udot4(a1, W1, __builtin_amdgcn_udot4(a0, W0, 0u, false), false), false);
+        const uint32_t h1 = __builtin_amdgcn_udot4(b2, W2, __builtin_amdgcn_udot4(b1, W1, __builtin_amdgcn_udot4(b0, W0, 0u, false), false), false);
+        hblur[wave][4 * q + m][rp] = h0 | (h1 << 16);
+      }
+    }
+  }
   // IC_Angle (:21-48) on the unblurred level (integer sums: order-free).
   // Lane (< 62) = patch row v = lane/2 - 15, half = lane & 1: five dwords of
   // the row (columns 4..23 or 24..43; the disk spans cc-15..cc+15 <= 39).
@@ -1221,45 +1263,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OB_WPE))) v
     m10 = (int)m - 19 * (int)s;
     m01 = __mul24(v, (int)s);
   }
-#pragma unroll
-  for (int d = 32; d >= 1; d >>= 1) {
-    m10 += __shfl_xor(m10, d, 64);
-    m01 += __shfl_xor(m01, d, 64);
-  }
-  m10 = __builtin_amdgcn_readfirstlane(m10);  // uniform: scalar angle / sincos table
-  m01 = __builtin_amdgcn_readfirstlane(m01);
+  // wave sums (uniform: scalar angle / sincos table) without LDS round trips
+  m10 = wave_sum_dpp(m10);
+  m01 = wave_sum_dpp(m01);
   const float angle = fast_atan2((float)m01, (float)m10);
   const float factorPI = (float)(3.1415926535897932384626433832795 / 180.f);
   float sn, cs;
   brief_sincos(angle * factorPI, exk0, exk1, &sn, &cs);
-  // BRIEF (:57-73) on GaussianBlur(7x7, sigma 2): separable and exact,
-  // out = (sum_j k_j H(r+j-3) + 32768) >> 16 with H = sum_i k_i p(c+i-3)
-  // (OpenCV's fixed-point 8U path, [18,34,48,56,48,34,18]).  The horizontal
-  // pass runs once per keypoint over the patch (hblur, column-major, row
-  // pairs packed as u16 x 2); each of the 364 live samples is then 4 dword
-  // reads + 4 v_dot2_u32_u16 down its hblur column -- 64 LDS ops per keypoint
-  // instead of 21 dword reads per sample (126).
-  {
-    // task = (row pair rp, 4-column group q): patch columns 4q..4q+3, rows
-    // 2rp, 2rp+1; the 7-byte windows c-3..c+3 lie in dwords q-1..q+1
-    const int qlo = (cc - 18) >> 2, qhi = (cc + 18) >> 2, nq = qhi - qlo + 1;
-    const int ntask = KP_HPAIRS * nq;
-    for (int t = lane; t < ntask; t += 64) {
-      const int rp = t / nq, q = qlo + t - rp * nq;
-      const int r0 = 2 * rp, r1 = min(2 * rp + 1, KP_ROWS - 1);
-      const int d0 = max(q - 1, 0);  // q == 0: the weights of dword q-1 are 0 for the columns used
-      const uint32_t a0 = P[r0][d0], a1 = P[r0][q], a2 = P[r0][q + 1];
-      const uint32_t b0 = P[r1][d0], b1 = P[r1][q], b2 = P[r1][q + 1];
-#pragma unroll
-      for (int m = 0; m < 4; ++m) {
-        // taps k0..k6 at window bytes m+1..m+7 of the 12 bytes a0|a1|a2
-        const uint32_t W0 = kb_w(m, 0), W1 = kb_w(m, 1), W2 = kb_w(m, 2);
-        const uint32_t h0 = __builtin_amdgcn_udot4(a2, W2, __builtin_amdgcn_udot4(a1, W1, __builtin_amdgcn_udot4(a0, W0, 0u, false), false), false);
-        const uint32_t h1 = __builtin_amdgcn_udot4(b2, W2, __builtin_amdgcn_udot4(b1, W1, __builtin_amdgcn_udot4(b0, W0, 0u, false), false), false);
-        hblur[wave][4 * q + m][rp] = h0 | (h1 << 16);
-      }
-    }
-  }
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
