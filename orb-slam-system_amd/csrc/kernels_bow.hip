@@ -16,6 +16,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "wave_ops.h"
+
 namespace orbx {
 
 struct BowRes {
@@ -138,12 +140,7 @@ __global__ __launch_bounds__(BA_THREADS) void k_bow_assemble(
   __shared__ int s_scan[BA_THREADS / 64 + 1];
   {
     const int lane = tid & 63, wave = tid >> 6;
-    int incl = heads;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      const int t = __shfl_up(incl, d, 64);
-      if (lane >= d) incl += t;
-    }
+    const int incl = orbx::wave_incl_scan(heads);
     if (lane == 63) s_scan[wave] = incl;
     atomicAdd(&s_cnt[0], valid);
     __syncthreads();
@@ -194,12 +191,7 @@ __global__ __launch_bounds__(BA_THREADS) void k_bow_assemble(
   int q0;
   {
     const int lane = tid & 63, wave = tid >> 6;
-    int incl = heads;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      const int t = __shfl_up(incl, d, 64);
-      if (lane >= d) incl += t;
-    }
+    const int incl = orbx::wave_incl_scan(heads);
     __syncthreads();
     if (lane == 63) s_scan[wave] = incl;
     __syncthreads();

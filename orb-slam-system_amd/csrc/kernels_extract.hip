@@ -15,6 +15,7 @@
 #include "../../include/orbx.h"
 #include "orbx_internal.h"
 #include "orbx_sincos.h"
+#include "wave_ops.h"
 
 #define ORBX_BRIEF_STORAGE static __constant__ const
 #include "brief_pattern.inc"
@@ -404,13 +405,8 @@ __device__ __forceinline__ bool fast_even_test(const uint8_t* t, int tw, int th)
 }
 
 __device__ __forceinline__ int wave_excl_scan(int n, int lane, int* total) {
-  int incl = n;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const int t = __shfl_up(incl, d, 64);
-    if (lane >= d) incl += t;
-  }
-  *total = __shfl(incl, 63, 64);
+  const int incl = wave_incl_scan(n);  // all 64 lanes active
+  *total = lane_value(incl, 63);
   return incl - n;
 }
 
@@ -507,7 +503,7 @@ __global__ __launch_bounds__(FS_NT) void k_fast_strips(
     const unsigned long long bal = __ballot(corner);
     int b = 0;
     if (lane == 0 && bal) b = atomicAdd(&ncorner, __popcll(bal));
-    b = __shfl(b, 0, 64);
+    b = __builtin_amdgcn_readfirstlane(b);
     const int q = b + __popcll(bal & lt);
     if (corner && q < FS_CCAP) clist[q] = (uint16_t)e;
   };
@@ -707,12 +703,7 @@ __device__ int block_scan_excl(int* a, int n, int* wtmp) {
   const int b = tid * chunk, e = min(n, b + chunk);
   int s = 0;
   for (int i = b; i < e; ++i) s += a[i];
-  int incl = s;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    int t = __shfl_up(incl, d, 64);
-    if (lane >= d) incl += t;
-  }
+  const int incl = wave_incl_scan(s);
   if (lane == 63) wtmp[wave] = incl;
   __syncthreads();
   int woff = 0;
@@ -989,18 +980,6 @@ __device__ __forceinline__ float fast_atan2(float y, float x) {
   return a;
 }
 
-// Sum over the wave, returned wave-uniform: inclusive row scans by DPP
-// row_shr 1/2/4/8 (16-lane rows, out-of-row sources read 0), then the four
-// row totals (lanes 15, 31, 47, 63) by readlane -- no ds_bpermute round trips.
-__device__ __forceinline__ int wave_sum_dpp(int x) {
-  x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, true);
-  x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, true);
-  x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xf, true);
-  x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xf, true);
-  return __builtin_amdgcn_readlane(x, 15) + __builtin_amdgcn_readlane(x, 31) +
-         __builtin_amdgcn_readlane(x, 47) + __builtin_amdgcn_readlane(x, 63);
-}
-
 // x is wave-uniform.  The exception keys live in two VGPRs per lane
 // (entries lane and lane + 64, loaded once per wave), so the lookup is two
 // compares and a ballot -- no chain of dependent scalar loads; the rare hit
@@ -1138,13 +1117,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OB_WPE))) v
   const int nlevels = A.nlevels, kcap = A.kcap;
   // per-level counts of this frame: one vector load + wave prefix
   const int lcv = lane < nlevels ? lcount[(size_t)f * nlevels + lane] : 0;
-  int incl = lcv;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const int t = __shfl_up(incl, d, 64);
-    if (lane >= d) incl += t;
-  }
-  const int total = __shfl(incl, 63, 64);  // all lanes active here
+  const int incl = wave_incl_scan(lcv);
+  const int total = lane_value(incl, 63);  // all lanes active here
   if (blockIdx.x == 0 && threadIdx.x == 0) counts[f] = total;
   const int excl = incl - lcv;
   const uint32_t* Q = qout + (size_t)f * qout_stride;
@@ -1264,8 +1238,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OB_WPE))) v
     m01 = __mul24(v, (int)s);
   }
   // wave sums (uniform: scalar angle / sincos table) without LDS round trips
-  m10 = wave_sum_dpp(m10);
-  m01 = wave_sum_dpp(m01);
+  m10 = wave_sum(m10);
+  m01 = wave_sum(m01);
   const float angle = fast_atan2((float)m01, (float)m10);
   const float factorPI = (float)(3.1415926535897932384626433832795 / 180.f);
   float sn, cs;

@@ -19,6 +19,7 @@
 
 #include "../../include/orbx.h"
 #include "match_internal.h"
+#include "wave_ops.h"
 
 namespace orbx {
 
@@ -117,12 +118,7 @@ __global__ __launch_bounds__(256) void k_match_candidates(
   int h[5], hs = 0;
 #pragma unroll
   for (int k = 0; k < 5; ++k) { h[k] = hist[wave][5 * lane + k]; hs += h[k]; }
-  int incl = hs;
-#pragma unroll
-  for (int s = 1; s < 64; s <<= 1) {
-    const int t = __shfl_up(incl, s, 64);
-    if (lane >= s) incl += t;
-  }
+  const int incl = wave_incl_scan(hs);
   const int excl = incl - hs;
   const uint64_t reach = __ballot(incl >= ORBM_T);
   int D = 1 << 20, cntLess = nvalid;  // nvalid < T: take everything
@@ -136,8 +132,8 @@ __global__ __launch_bounds__(256) void k_match_candidates(
         cum += h[k];
       }
     }
-    D = __shfl(dd, L0, 64);
-    cntLess = __shfl(cl, L0, 64);
+    D = lane_value(dd, L0);
+    cntLess = lane_value(cl, L0);
   }
   const uint64_t nz = __ballot(hs > 0);
   int minD = 1 << 20;
@@ -147,7 +143,7 @@ __global__ __launch_bounds__(256) void k_match_candidates(
     if (lane == L1) {
       for (int k = 4; k >= 0; --k) if (h[k] > 0) md = 5 * lane + k;
     }
-    minD = __shfl(md, L1, 64);
+    minD = lane_value(md, L1);
   }
   // ordered compaction: all entries with d < D, then the first (T - cntLess) with d == D
   const int needEq = ORBM_T - cntLess;
@@ -582,8 +578,8 @@ __global__ __launch_bounds__(256) void k_match_resolve(
         const int l = __ffsll((unsigned long long)feas) - 1;
         feas &= feas - 1;
         const int r = NP.row_base + base + l;
-        const int idx1 = __shfl(inf.w, l, 64);
-        const int nvalid2 = __shfl(inf.y, l, 64);
+        const int idx1 = lane_value(inf.w, l);
+        const int nvalid2 = lane_value(inf.y, l);
         const uint2 c = lane < ORBM_T ? scand[wave][l * ORBM_T + lane] : make_uint2(0xFFFFFFFFu, 0u);
         const uint32_t key = c.x;
         const int idx2 = (int)c.y;
@@ -593,10 +589,10 @@ __global__ __launch_bounds__(256) void k_match_resolve(
         if (__popcll(m) >= 2 || nvalid2 <= ORBM_T) {
           if (m) {
             const int l1 = __ffsll((unsigned long long)m) - 1;
-            best1 = (int)(__shfl(key, l1, 64) >> 16);
-            bidx2 = __shfl(idx2, l1, 64);
+            best1 = (int)(lane_value(key, l1) >> 16);
+            bidx2 = lane_value(idx2, l1);
             const uint64_t m2 = m & (m - 1);
-            if (m2) best2 = (int)(__shfl(key, __ffsll((unsigned long long)m2) - 1, 64) >> 16);
+            if (m2) best2 = (int)(lane_value(key, __ffsll((unsigned long long)m2) - 1) >> 16);
           }
         } else {  // candidates exhausted: exact rescan of the node's list
           const uint32_t* q1 = reinterpret_cast<const uint32_t*>(P.desc1 + (size_t)idx1 * 32);
@@ -744,7 +740,7 @@ __global__ __launch_bounds__(64) void k_match_resolve_spec(
 #ifdef RS_STATS
         st_hard++;
 #endif
-        const int idx1 = __shfl(inf.w, bnd, 64);
+        const int idx1 = lane_value(inf.w, bnd);
         const uint32_t* q1 = reinterpret_cast<const uint32_t*>(P.desc1 + (size_t)idx1 * 32);
         uint32_t d1[8];
 #pragma unroll

@@ -13,6 +13,7 @@
 #include <stdint.h>
 
 #include "../../include/orbx.h"
+#include "wave_ops.h"
 
 namespace orbx {
 
@@ -277,10 +278,10 @@ __global__ __launch_bounds__(64) void k_proj_resolve(
     if (nfree >= 2 || complete) {
       if (nfree >= 1) {
         const int l1 = __ffsll(fb) - 1;
-        k1 = __shfl(e, l1, 64);
+        k1 = lane_value(e, l1);
         if (nfree >= 2) {
           const int l2 = __ffsll(fb & (fb - 1)) - 1;
-          d2 = (uint32_t)__shfl(e, l2, 64) >> 16;
+          d2 = lane_value(e, l2) >> 16;
         }
       }
     } else {

@@ -14,6 +14,7 @@
 
 #include "../../include/orbx.h"
 #include "orbx_internal.h"
+#include "wave_ops.h"
 
 namespace orbx {
 
@@ -26,12 +27,7 @@ __device__ int stereo_block_scan(int* a, int n, int* wsum) {
   const int b = min(n, tid * chunk), e = min(n, b + chunk);
   int s = 0;
   for (int i = b; i < e; ++i) s += a[i];
-  int incl = s;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const int t = __shfl_up(incl, d, 64);
-    if (lane >= d) incl += t;
-  }
+  const int incl = orbx::wave_incl_scan(s);
   if (lane == 63) wsum[wave] = incl;
   __syncthreads();
   if (tid == 0) {

@@ -1,0 +1,43 @@
+// wave_ops.h -- wave64 reductions and scans on DPP / v_readlane (CDNA4).
+// __shfl / __shfl_up compile to ds_bpermute: an LDS round trip per step.
+// These use DPP row shifts and row broadcasts (gfx9 DPP: row_shr:n =
+// 0x110 + n, row_bcast:15 = 0x142, row_bcast:31 = 0x143) and readlane, so a
+// 64-lane scan is 6 VALU ops.  Callers keep all 64 lanes active (DPP reads
+// inactive lanes' stale registers).
+#ifndef ORBX_WAVE_OPS_H
+#define ORBX_WAVE_OPS_H
+
+#include <hip/hip_runtime.h>
+
+namespace orbx {
+
+// inclusive prefix sum over the 64 lanes
+__device__ __forceinline__ int wave_incl_scan(int x) {
+  x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, true);  // row_shr:1
+  x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, true);  // row_shr:2
+  x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xf, true);  // row_shr:4
+  x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xf, true);  // row_shr:8
+  x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xa, 0xf, false);  // row_bcast:15 -> rows 1, 3
+  x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xc, 0xf, false);  // row_bcast:31 -> rows 2, 3
+  return x;
+}
+
+// sum over the 64 lanes, wave-uniform
+__device__ __forceinline__ int wave_sum(int x) {
+  x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, true);
+  x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, true);
+  x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xf, true);
+  x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xf, true);
+  return __builtin_amdgcn_readlane(x, 15) + __builtin_amdgcn_readlane(x, 31) +
+         __builtin_amdgcn_readlane(x, 47) + __builtin_amdgcn_readlane(x, 63);
+}
+
+// value of lane l (l wave-uniform)
+__device__ __forceinline__ int lane_value(int x, int l) { return __builtin_amdgcn_readlane(x, l); }
+__device__ __forceinline__ uint32_t lane_value(uint32_t x, int l) {
+  return (uint32_t)__builtin_amdgcn_readlane((int)x, l);
+}
+
+}  // namespace orbx
+
+#endif
