@@ -338,8 +338,10 @@ __global__ __launch_bounds__(256) void k_match_cand_rows(
   __shared__ uint32_t sval[2][MC_CHUNK];          // per-position invalid masks (validity arrays only)
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const MNodePair NP = nps[blockIdx.y];
-  const int a0 = blockIdx.x * 128;
+  int bx, np;
+  frame_unit(bx, np);  // a node pair's row chunks share one L2 (its list2)
+  const MNodePair NP = nps[np];
+  const int a0 = bx * 128;
   if (a0 >= NP.n1) return;  // workgroup-uniform
   const MProblem P = probs[NP.prob];
   const uint32_t* f2 = P.feat2 + NP.off2;

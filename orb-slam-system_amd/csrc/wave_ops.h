@@ -38,6 +38,28 @@ __device__ __forceinline__ uint32_t lane_value(uint32_t x, int l) {
   return (uint32_t)__builtin_amdgcn_readlane((int)x, l);
 }
 
+#ifndef ORBX_XCD_FRAMES
+#define ORBX_XCD_FRAMES 1
+#endif
+// (unit, frame) of a workgroup of a grid (units, frames).  Workgroups are
+// dispatched round-robin over the 8 XCDs in linear-id order, so with
+// ORBX_XCD_FRAMES every unit of frame f runs on XCD f % 8, in unit order:
+// strips / tiles / keypoint groups / row chunks that share 128-B lines, ring
+// rows or a whole descriptor set of one frame meet in one L2 instead of being
+// fetched from HBM by several XCDs (falls back to the plain grid when the
+// frame count is not a multiple of 8).
+__device__ __forceinline__ void frame_unit(int& unit, int& f) {
+  if (ORBX_XCD_FRAMES && (gridDim.y & 7) == 0) {
+    const int L = (int)(blockIdx.x + blockIdx.y * gridDim.x), k = L >> 3;
+    const int q = k / (int)gridDim.x;
+    unit = k - q * (int)gridDim.x;
+    f = (L & 7) + 8 * q;
+  } else {
+    unit = (int)blockIdx.x;
+    f = (int)blockIdx.y;
+  }
+}
+
 }  // namespace orbx
 
 #endif
