@@ -19,7 +19,7 @@ __global__ void k_pyramid(const uint8_t*, size_t, size_t, uint8_t*, size_t, cons
                           const int4*, const int4*, const uint4*, const int*, int);
 __global__ void k_fast_strips(const uint8_t*, size_t, size_t, const uint8_t*, size_t,
                               const LevelArgs, const CellInfo*, const StripInfo*, uint32_t*,
-                              size_t, uint32_t*, int, int, int, int, int, int, int, int);
+                              size_t, uint32_t*, int, int, int, int, int, int, int);
 __global__ void k_quadtree(const LevelInfo*, const CellInfo*, const uint32_t*, size_t,
                            const uint32_t*, int, uint32_t*, int32_t*, size_t, uint32_t*, size_t,
                            int*, int, int, int, int*);
@@ -206,16 +206,9 @@ extern "C" int orbx_plan_create(const orbx_params* prm, int width, int height, i
     p->fs_mcells = std::max(P.strip_max_cells, 1);
     /* tile + band-row strength map + counts; the NMS masks reuse the tile
      * when they fit (k_fast_strips) */
-    /* strength map pitch: 4 x the most 4-pixel groups a band spans (tile
-     * lead 0..15 by the level's alignment) */
-    int max_ng = 1;
-    for (const StripInfo& st : P.strips)
-      for (int lead = 0; lead < 16; ++lead)
-        max_ng = std::max(max_ng, ((lead + st.w) >> 2) - ((lead + 3) >> 2));
-    p->fs_apitch = 4 * max_ng;
     const size_t tile = (size_t)p->fs_tpitch * p->fs_tmaxh;
     const size_t masks = 16 * (size_t)p->fs_mcells * (p->fs_tmaxh - 6);
-    p->fs_lds = tile + (size_t)p->fs_apitch * (p->fs_tmaxh - 6) + 4 * (size_t)((p->fs_mcells + 3) & ~3) +
+    p->fs_lds = tile + (size_t)p->fs_tpitch * (p->fs_tmaxh - 6) + 4 * (size_t)((p->fs_mcells + 3) & ~3) +
                 (masks <= tile ? 0 : masks);
 #ifdef FS_LDS_PAD  // profiling variant: occupancy sensitivity of k_fast_strips
     p->fs_lds += FS_LDS_PAD;
@@ -310,7 +303,7 @@ extern "C" int orbx_plan_extract(orbx_plan* p, const uint8_t* frames, int nframe
     hipLaunchKernelGGL(k_fast_strips, dim3((unsigned)P.strips.size(), n), dim3(FS_NT), p->fs_lds, s,
                        frames, fstride, rstride, p->d_pyr, p->pyr_stride, p->largs, p->d_cells,
                        p->d_strips, p->d_slots, p->slot_stride, p->d_ccount, P.ncells, P.ini_th,
-                       P.min_th, p->fs_tpitch, p->fs_apitch, p->fs_tmaxh, p->fs_mcells, p->dbg);
+                       P.min_th, p->fs_tpitch, p->fs_tmaxh, p->fs_mcells, p->dbg);
   }
   p->timer.end(ORBX_STAGE_FAST, s);
   if (p->dbg && p->dbg < 20) return ORBX_OK; /* phase probe: later stages would read partial results */

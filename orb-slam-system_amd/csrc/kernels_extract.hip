@@ -334,6 +334,27 @@ __device__ __forceinline__ int fast_strength(const uint8_t* t, int tw) {
   return max3i(0, Mb - v, v - Md);
 }
 
+__device__ __forceinline__ int nms_keep(const uint8_t* amap, int bw, int bh, int bx, int by,
+                                        int th) {
+  const int a = amap[by * bw + bx];
+  if (a <= th) return 0;
+  const int s = a - 1;
+#pragma unroll
+  for (int dy = -1; dy <= 1; ++dy)
+#pragma unroll
+    for (int dx = -1; dx <= 1; ++dx) {
+      if (dx == 0 && dy == 0) continue;
+      const int qx = bx + dx, qy = by + dy;
+      int nb = 0;
+      if (qx >= 0 && qx < bw && qy >= 0 && qy < bh) {
+        const int aq = amap[qy * bw + qx];
+        nb = aq > th ? aq - 1 : 0;
+      }
+      if (!(s > nb)) return 0;
+    }
+  return 1;
+}
+
 // ---------------------------------------------------------------------------
 // k_fast_strips: one workgroup per (strip of cells, frame).
 //  1. the strip tile (cells + 3-px rings) is staged in LDS with dword loads;
@@ -346,6 +367,25 @@ __device__ __forceinline__ int fast_strength(const uint8_t* t, int tw) {
 //  5. each (cell, row) writes its kept pixels at the cell's raster offset.
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ int tbyte(const uint32_t* dw, int i) { return (dw[i >> 2] >> ((i & 3) * 8)) & 0xFF; }
+
+__device__ __forceinline__ bool nms_keep_tile(const uint8_t* amap, int tpitch, int r, int c, int a,
+                                              int th, int bh, int cb0, int cb1) {
+  bool keep = true;
+#pragma unroll
+  for (int dy = -1; dy <= 1; ++dy)
+#pragma unroll
+    for (int dx = -1; dx <= 1; ++dx) {
+      if (!dx && !dy) continue;
+      const int rr = r + dy, cc = c + dx;
+      int nb = 0;
+      if (rr >= 3 && rr < 3 + bh && cc >= cb0 && cc < cb1) {
+        const int aq = amap[rr * tpitch + cc];
+        nb = aq > th ? aq - 1 : 0;
+      }
+      keep = keep && (a - 1 > nb);
+    }
+  return keep;
+}
 
 // 4 cyclically consecutive points of {0,2,..,14} all brighter (darker) than
 // v +- t: necessary for a 9-arc (any 9 contiguous circle points contain 4
@@ -383,9 +423,9 @@ __device__ __forceinline__ void wave_sync_lds() {
 #ifndef FS_L1FLUSH
 #define FS_L1FLUSH 64 /* stage B runs once a wave's L1 holds this many entries */
 #endif
-#define FS_L1CAP (FS_L1FLUSH + 128) /* per-wave cardinal survivors: < FS_L1FLUSH carried + <= 2 x 64 new */
+#define FS_L1CAP (FS_L1FLUSH + 256) /* per-wave cardinal survivors: < FS_L1FLUSH carried + <= 256 new */
 #define FS_L2CAP 128 /* per-wave even-test survivors: < 64 carried + <= 64 new */
-#define FS_CCAP 512 /* per-strip corner list (overflow falls back to a map scan) */
+#define FS_CCAP 1024 /* per-strip corner list (overflow falls back to a map scan) */
 
 
 __global__ __launch_bounds__(FS_NT) void k_fast_strips(
@@ -393,16 +433,16 @@ __global__ __launch_bounds__(FS_NT) void k_fast_strips(
     const uint8_t* __restrict__ pyr, size_t pstride, const LevelArgs LA,
     const CellInfo* __restrict__ cells, const StripInfo* __restrict__ strips,
     uint32_t* __restrict__ slots, size_t slot_stride, uint32_t* __restrict__ ccount, int ncells,
-    int ini_th, int min_th, int tpitch, int apitch, int tmax_h, int mcells, int dbg) {
+    int ini_th, int min_th, int tpitch, int tmax_h, int mcells, int dbg) {
   // LDS (occupancy is LDS-bound and the kernel is latency-bound: +12 KB per
   // workgroup measured +38 % time): tile | strength map of the band rows only
   // | per-cell counts; the NMS row masks reuse the tile, which is dead after
   // pass 1 (fs_lds in api_extract.hip mirrors this layout)
   extern __shared__ __align__(16) uint32_t sm[];
   uint8_t* tile = reinterpret_cast<uint8_t*>(sm);                    // tpitch * tmax_h
-  // strength map: apitch (>= 4 * the band's 4-pixel groups) x band rows
-  uint8_t* amap_mem = tile + tpitch * tmax_h;
-  int* cnt = reinterpret_cast<int*>(amap_mem + apitch * (tmax_h - 6));  // mcells
+  uint8_t* amap_mem = tile + tpitch * tmax_h;                         // tpitch * (tmax_h - 6)
+  uint8_t* amap = amap_mem - 3 * tpitch;                              // indexed by tile row 3 .. 3+bh
+  int* cnt = reinterpret_cast<int*>(amap_mem + tpitch * (tmax_h - 6));  // mcells
   const bool masks_in_tile = 16 * mcells * (tmax_h - 6) <= tpitch * tmax_h;
   unsigned long long* mask = masks_in_tile ? reinterpret_cast<unsigned long long*>(tile)
                                            : reinterpret_cast<unsigned long long*>(cnt + ((mcells + 3) & ~3));
@@ -455,7 +495,6 @@ __global__ __launch_bounds__(FS_NT) void k_fast_strips(
   // only wave-level LDS ordering is needed.
   const int g0 = c0 >> 2, g1 = (c1 + 3) >> 2, ng = g1 - g0;
   const int ntask = ng * bh;
-  uint8_t* const amap = amap_mem - 3 * apitch - 4 * g0;  // indexed by tile (row 3 .. 3+bh, col)
   uint16_t* L1 = wlist1[wave];
   uint16_t* L2 = wlist2[wave];
   int n1 = 0, n2 = 0;  // wave-uniform list lengths
@@ -466,7 +505,7 @@ __global__ __launch_bounds__(FS_NT) void k_fast_strips(
       const int rr = e >> 9, cc = e & 511;
       const int a = fast_strength(tile + rr * tpitch + cc, tpitch);
       corner = a > t_lo;
-      amap[rr * apitch + cc] = (uint8_t)(corner ? a : 0);
+      amap[rr * tpitch + cc] = (uint8_t)(corner ? a : 0);
     }
     const unsigned long long bal = __ballot(corner);
     int b = 0;
@@ -526,7 +565,7 @@ __global__ __launch_bounds__(FS_NT) void k_fast_strips(
           const uint32_t x = as_u32(db) | as_u32(dd);
           if (h) chi = x; else clo = x;
         }
-        reinterpret_cast<uint32_t*>(amap + __mul24(r, apitch))[g] = 0u;
+        reinterpret_cast<uint32_t*>(amap + ro)[g] = 0u;
 #ifdef FAST_PAD
         // profiling only: FAST_PAD dependent VALU ops per group (issue-bound probe)
         uint32_t pz = clo;
@@ -537,14 +576,12 @@ __global__ __launch_bounds__(FS_NT) void k_fast_strips(
 #endif
       }
 #ifdef FAST_NO_APPEND  // profiling only: stage A without the list appends
-      if (it < ntask) reinterpret_cast<uint32_t*>(amap + r * apitch)[g] = (clo | chi) & 0x01000000u;
+      if (it < ntask) reinterpret_cast<uint32_t*>(amap + r * tpitch)[g] = (clo | chi) & 0x01000000u;
 #else
       // append: the ballot is the compare's SGPR result, the lane's slot is
       // mbcnt of it, only survivors store (stores of every lane to a dummy
       // slot measured 13 % slower).  Columns outside [c0, c1) are appended
       // too and rejected in stage B.
-      // L1 is flushed after every second position, so it holds at most
-      // FS_L1FLUSH - 1 + 128 entries (LDS sets FAST's occupancy)
       const uint32_t ebase = ((uint32_t)r << 9) | (uint32_t)(4 * g);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
@@ -555,18 +592,18 @@ __global__ __launch_bounds__(FS_NT) void k_fast_strips(
                                                        __builtin_amdgcn_mbcnt_lo((uint32_t)bal, (uint32_t)n1));
         if (k) L1[pos] = (uint16_t)(ebase + (uint32_t)j);
         n1 += __popcll(bal);
-        if ((j & 1) && n1 >= FS_L1FLUSH) {  // wave-uniform
-          wave_sync_lds();
-          while (n1 >= 64) {
-            n1 -= 64;
-#ifndef FAST_SKIP_B  // profiling only: drop the cardinal survivors
-            even_batch(L1[n1 + lane], true);
-#endif
-          }
-          wave_sync_lds();
-        }
       }
 #endif
+      if (n1 >= FS_L1FLUSH) {  // wave-uniform
+        wave_sync_lds();
+        while (n1 >= 64) {
+          n1 -= 64;
+#ifndef FAST_SKIP_B  // profiling only: drop the cardinal survivors
+          even_batch(L1[n1 + lane], true);
+#endif
+        }
+        wave_sync_lds();
+      }
       r += dr;
       g += dg;
       if (g >= g1) { g -= ng; ++r; }
@@ -599,7 +636,7 @@ __global__ __launch_bounds__(FS_NT) void k_fast_strips(
         if (!dx && !dy) continue;
         const int rr = r + dy, cc = c + dx;
         int aq = 0;
-        if (rr >= 3 && rr < 3 + bh && cc >= cb0 && cc < cb1) aq = amap[rr * apitch + cc];
+        if (rr >= 3 && rr < 3 + bh && cc >= cb0 && cc < cb1) aq = amap[rr * tpitch + cc];
         nbm = max(nbm, aq > min_th ? aq - 1 : 0);
         nbi = max(nbi, aq > ini_th ? aq - 1 : 0);
       }
@@ -615,13 +652,13 @@ __global__ __launch_bounds__(FS_NT) void k_fast_strips(
     for (int q = tid; q < nc; q += FS_NT) {
       const int e = clist[q];
       const int r = e >> 9, c = e & 511;
-      nms_pixel(r, c, amap[r * apitch + c]);
+      nms_pixel(r, c, amap[r * tpitch + c]);
     }
   } else {  // list overflow: scan the strength map
     const int dr = FS_NT / ng, dg = FS_NT - dr * ng;
     int r = 3 + tid / ng, g = g0 + tid % ng;
     for (; r < 3 + bh;) {
-      const uint32_t w4 = reinterpret_cast<const uint32_t*>(amap + r * apitch)[g];
+      const uint32_t w4 = reinterpret_cast<const uint32_t*>(amap + r * tpitch)[g];
       if (w4) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -656,7 +693,7 @@ __global__ __launch_bounds__(FS_NT) void k_fast_strips(
         const int c = cb0 + b;
         const int gx = xal + c - ORBX_MINB;
         fslots[so + off++] =
-            orbx_pack_key((uint32_t)gx, (uint32_t)gy, (uint32_t)amap[(3 + br) * apitch + c] - 1u);
+            orbx_pack_key((uint32_t)gx, (uint32_t)gy, (uint32_t)amap[(3 + br) * tpitch + c] - 1u);
       }
       carry += tot;
     }

@@ -17,7 +17,7 @@ struct orbx_plan {
   LevelInfo* d_lv = nullptr;
   CellInfo* d_cells = nullptr;
   StripInfo* d_strips = nullptr;
-  int fs_tpitch = 0, fs_apitch = 0, fs_tmaxh = 0, fs_qcap = 0, fs_mcells = 0;
+  int fs_tpitch = 0, fs_tmaxh = 0, fs_qcap = 0, fs_mcells = 0;
   size_t fs_lds = 0;
   int32_t *d_xofs = nullptr, *d_xofs1 = nullptr, *d_yofs = nullptr;
   int32_t *d_pyr_xs = nullptr, *d_pyr_ys = nullptr, *d_pyr_bo = nullptr;
