@@ -772,7 +772,12 @@ __global__ __launch_bounds__(256) void k_quadtree(
     uint32_t* __restrict__ qout, size_t qout_stride, int* __restrict__ lcount, int nlevels,
     int smax, int maxcells, int* __restrict__ err) {
   extern __shared__ __align__(16) int smem[];
-  const int l = blockIdx.x, f = blockIdx.y, tid = threadIdx.x;
+  // grid (levels, frames): the plain linear order would put level l of
+  // every frame on XCD l (dispatch is round-robin over 8 XCDs), i.e. all
+  // level-0 trees on one XCD; frame_unit spreads frames, not levels
+  int l, f;
+  frame_unit(l, f);
+  const int tid = threadIdx.x;
   const LevelInfo L = lv[l];
   const LevelInfo U = lv[L.unique];
   int* cell_off = smem;                       // maxcells + 1
