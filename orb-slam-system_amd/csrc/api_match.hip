@@ -19,6 +19,12 @@ template <int NW>
 __global__ void k_match_cand_rows(const MProblem*, const MNodePair*, const uint4*, const uint32_t*,
                                   uint2*, int4*, int2*);
 __global__ void k_match_gather2(const MProblem*, const MNodePair*, uint4*, uint32_t*);
+typedef int v4i_ __attribute__((ext_vector_type(4)));
+template <int NK>
+__global__ void k_match_expand2(const MNodePair*, const uint4*, v4i_*);
+template <int NK>
+__global__ void k_match_cand_mfma(const MProblem*, const MNodePair*, const v4i_*, uint2*, int4*,
+                                  int2*);
 __global__ void k_match_resolve(const MProblem*, const MNodePair*, int, int, const uint2*,
                                 const int4*, int2*);
 __global__ void k_match_resolve_spec(const MProblem*, const MNodePair*, int, const uint2*,
@@ -32,6 +38,10 @@ __global__ void k_hamming_pairs(const uint8_t*, const uint8_t*, const int32_t*, 
 }  // namespace orbx
 
 using namespace orbx;
+
+#ifndef ORBM_MFMA
+#define ORBM_MFMA 1 /* 0: VALU distances everywhere (profiling variant) */
+#endif
 
 namespace {
 
@@ -63,8 +73,9 @@ int check_frame(const orbx_bow_frame* k) {
 
 void launch_match(const MProblem* d_probs, int nprob, const MNodePair* d_nps, int nnp, int nrows,
                   int sequential, int max_n1, int max_n2, int max_bitmap_n2, uint4* d_gdesc2,
-                  uint32_t* d_gval2, uint2* d_cand, int4* d_rowinfo, int2* d_ev, int* d_last,
-                  const int* d_last_off, hipStream_t s, StageTimer* timer, bool six_words) {
+                  uint32_t* d_gval2, void* d_gx2, uint2* d_cand, int4* d_rowinfo, int2* d_ev,
+                  int* d_last, const int* d_last_off, hipStream_t s, StageTimer* timer,
+                  bool six_words) {
   {
     int dev = 0;
     hipGetDevice(&dev);
@@ -80,7 +91,21 @@ void launch_match(const MProblem* d_probs, int nprob, const MNodePair* d_nps, in
       if (max_n2 > 0)
         hipLaunchKernelGGL(k_match_gather2, dim3((max_n2 + 127) / 128, nnp), dim3(256), 0, s, d_probs,
                            d_nps, d_gdesc2, d_gval2);
-      if (six_words)
+      if (ORBM_MFMA && d_gx2 && !d_gval2 && max_n2 > 0) {
+        // distances on the matrix cores (no validity masks on this path)
+        v4i_* gx2 = reinterpret_cast<v4i_*>(d_gx2);
+        if (six_words) {
+          hipLaunchKernelGGL(k_match_expand2<6>, dim3((max_n2 * 6 + 255) / 256, nnp), dim3(256), 0, s,
+                             d_nps, d_gdesc2, gx2);
+          hipLaunchKernelGGL(k_match_cand_mfma<6>, dim3((max_n1 + 127) / 128, nnp), dim3(256), 0, s,
+                             d_probs, d_nps, gx2, d_cand, d_rowinfo, d_ev);
+        } else {
+          hipLaunchKernelGGL(k_match_expand2<8>, dim3((max_n2 * 8 + 255) / 256, nnp), dim3(256), 0, s,
+                             d_nps, d_gdesc2, gx2);
+          hipLaunchKernelGGL(k_match_cand_mfma<8>, dim3((max_n1 + 127) / 128, nnp), dim3(256), 0, s,
+                             d_probs, d_nps, gx2, d_cand, d_rowinfo, d_ev);
+        }
+      } else if (six_words)
         hipLaunchKernelGGL(k_match_cand_rows<6>, dim3((max_n1 + 127) / 128, nnp), dim3(256), 0, s,
                            d_probs, d_nps, d_gdesc2, d_gval2, d_cand, d_rowinfo, d_ev);
       else
@@ -207,6 +232,7 @@ extern "C" int orbm_search_by_bow(const orbx_bow_frame* kf1, const orbx_bow_fram
   const size_t o_rowinfo = C.take((size_t)rows * sizeof(int4)), o_ev = C.take((size_t)rows * sizeof(int2));
   const size_t o_last = C.take(n1 * 4), o_g2 = C.take((size_t)g2 * 2 * sizeof(uint4));
   const size_t o_gv2 = kf2->valid ? C.take((size_t)g2 * 4) : 0;
+  const size_t o_gx2 = kf2->valid ? 0 : C.take((size_t)g2 * 256);  /* +-1 bytes for the MFMA path */
   int rc2 = w->reserve(C.off, out_end);
   if (rc2) return rc2;
   uint8_t* d = w->d;
@@ -251,7 +277,7 @@ extern "C" int orbm_search_by_bow(const orbx_bow_frame* kf1, const orbx_bow_fram
                (int)nnp, rows, sequential, max_n1, max_n2, kf2->n,
                reinterpret_cast<uint4*>(d + o_g2),
                kf2->valid ? reinterpret_cast<uint32_t*>(d + o_gv2) : nullptr,
-               reinterpret_cast<uint2*>(d + o_cand), reinterpret_cast<int4*>(d + o_rowinfo),
+               kf2->valid ? nullptr : d + o_gx2, reinterpret_cast<uint2*>(d + o_cand), reinterpret_cast<int4*>(d + o_rowinfo),
                reinterpret_cast<int2*>(d + o_ev), reinterpret_cast<int*>(d + o_last),
                reinterpret_cast<const int*>(d + o_loff), s, nullptr,
                upper_bytes_zero(kf1->desc, kf1->n) && upper_bytes_zero(kf2->desc, kf2->n));
@@ -360,6 +386,7 @@ struct orbm_plan {
   uint32_t* d_sel = nullptr;
   uint2* d_cand = nullptr;
   uint4* d_gdesc2 = nullptr;
+  void* d_gx2 = nullptr; /* list2 as +-1 bytes, 256 B per position */
   int4* d_rowinfo = nullptr;
   int2* d_ev = nullptr;
   int *d_last = nullptr, *d_last_off = nullptr;
@@ -369,8 +396,8 @@ struct orbm_plan {
 static void mplan_free(orbm_plan* m) {
   if (!m) return;
   hipSetDevice(m->device);
-  void* b[] = {m->d_probs, m->d_nps, m->d_sel, m->d_cand, m->d_gdesc2, m->d_rowinfo, m->d_ev,
-               m->d_last, m->d_last_off};
+  void* b[] = {m->d_probs, m->d_nps, m->d_sel, m->d_cand, m->d_gdesc2, m->d_gx2, m->d_rowinfo,
+               m->d_ev, m->d_last, m->d_last_off};
   for (void* p : b)
     if (p) hipFree(p);
   m->timer.release();
@@ -396,6 +423,7 @@ extern "C" int orbm_plan_create(int max_pairs, int kcap, int topn, int device, o
       hipMalloc((void**)&m->d_sel, P * 2 * topn * sizeof(uint32_t)) != hipSuccess ||
       hipMalloc((void**)&m->d_cand, rows * ORBM_T * sizeof(uint2)) != hipSuccess ||
       hipMalloc((void**)&m->d_gdesc2, rows * 2 * sizeof(uint4)) != hipSuccess ||
+      hipMalloc(&m->d_gx2, rows * 256) != hipSuccess ||
       hipMalloc((void**)&m->d_rowinfo, rows * sizeof(int4)) != hipSuccess ||
       hipMalloc((void**)&m->d_ev, rows * sizeof(int2)) != hipSuccess ||
       hipMalloc((void**)&m->d_last, P * kcap * sizeof(int)) != hipSuccess ||
@@ -443,7 +471,7 @@ extern "C" int orbm_plan_match_frames(orbm_plan* m, int npairs, const orbx_keypo
                      kps_a, count_a, kps_b, count_b, m->kcap, m->topn, m->d_sel);
   m->timer.end(ORBX_STAGE_MSELECT, s);
   launch_match(m->d_probs, npairs, m->d_nps, npairs, npairs * m->topn, 0, m->topn, m->topn,
-               m->kcap, m->d_gdesc2, nullptr, m->d_cand, m->d_rowinfo, m->d_ev, m->d_last,
+               m->kcap, m->d_gdesc2, nullptr, m->d_gx2, m->d_cand, m->d_rowinfo, m->d_ev, m->d_last,
                m->d_last_off, s, &m->timer, m->six_words);
   return hipGetLastError() == hipSuccess ? ORBX_OK : ORBX_ERR_HIP;
 }

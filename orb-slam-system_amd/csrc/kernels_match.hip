@@ -525,6 +525,170 @@ template __global__ void k_match_cand_rows<6>(const MProblem*, const MNodePair*,
                                               const uint32_t*, uint2*, int4*, int2*);
 
 // ---------------------------------------------------------------------------
+// Distances on the matrix cores.  With bits as +-1 bytes the i8 MFMA's dot
+// product of a position's a' = 2a - 1 and a row's b' = 1 - 2b is
+// sum_k -(+1 if a_k == b_k else -1) = 2 h - K (h = Hamming distance), so an
+// accumulator started at K ends at 2 h and the candidate key
+// (h << 16 | position) is (C << 15) + position.  k_match_expand2 writes the
+// gathered list2 as such bytes; k_match_cand_mfma computes 32 positions x
+// 32 rows per wave step (v_mfma_i32_32x32x32_i8, K = 32 bits per step) and
+// keeps the VALU for the top-T insertion only.
+// ---------------------------------------------------------------------------
+typedef int v4i_ __attribute__((ext_vector_type(4)));
+typedef int v16i_ __attribute__((ext_vector_type(16)));
+
+// 4 bits -> 4 bytes of 0 / 1 (bit t -> byte t; the shifted copies never overlap)
+__device__ __forceinline__ uint32_t nib_bytes(uint32_t n) { return (n * 0x00204081u) & 0x01010101u; }
+
+// 16 bits -> 16 bytes: +1 / -1 for bit set / clear (pos = true), or the reverse
+__device__ __forceinline__ v4i_ pm1_bytes(uint32_t bits, bool pos) {
+  const uint32_t base = pos ? 0xFFFFFFFFu : 0x01010101u;  // x * 0xFE flips 0xFF <-> 0x01 per set bit
+  v4i_ r;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) r[q] = (int)(base ^ (nib_bytes((bits >> (4 * q)) & 15u) * 0xFEu));
+  return r;
+}
+
+// gx2[(g2 + j) * 2 * NK + 2 * s + h] = bits 16h .. 16h+15 of dword s of
+// position j's gathered descriptor, as +-1 bytes (a' = 2a - 1)
+template <int NK>
+__global__ __launch_bounds__(256) void k_match_expand2(const MNodePair* __restrict__ nps,
+                                                       const uint4* __restrict__ gdesc2,
+                                                       v4i_* __restrict__ gx2) {
+  const MNodePair NP = nps[blockIdx.y];
+  const int i = blockIdx.x * 256 + threadIdx.x;  // (position, dword)
+  const int j = i / NK, s = i - j * NK;
+  if (j >= NP.n2) return;
+  const uint32_t w = reinterpret_cast<const uint32_t*>(gdesc2 + (size_t)(NP.g2 + j) * 2)[s];
+  v4i_* o = gx2 + ((size_t)(NP.g2 + j) * NK + s) * 2;
+  o[0] = pm1_bytes(w & 0xFFFFu, true);
+  o[1] = pm1_bytes(w >> 16, true);
+}
+template __global__ void k_match_expand2<6>(const MNodePair*, const uint4*, v4i_*);
+template __global__ void k_match_expand2<8>(const MNodePair*, const uint4*, v4i_*);
+
+// 128 rows per workgroup, 32 per wave: lane l holds row a0 + 32w + (l & 31)
+// as the B operand (K bits of its half h = l >> 5 per step), and gets back
+// C[position][row] for the 16 positions (i&3) + 8(i>>2) + 4h of each 32-
+// position tile (gfx950 32x32 C layout).  Each lane half keeps its own
+// sorted top-T list of the row; the halves merge through LDS at the end.
+// Positions are read as A fragments straight from gx2 (L1/L2: the 4 waves
+// of a workgroup and the node pair's other workgroups read the same tiles),
+// one tile ahead.  Validity arrays are not supported (k_match_cand_rows).
+template <int NK>
+__global__ __launch_bounds__(256) void k_match_cand_mfma(
+    const MProblem* __restrict__ probs, const MNodePair* __restrict__ nps,
+    const v4i_* __restrict__ gx2, uint2* __restrict__ cand, int4* __restrict__ rowinfo,
+    int2* __restrict__ ev) {
+  static_assert(NK == 6 || NK == 8, "6 or 8 live descriptor dwords");
+  __shared__ uint32_t ml[4][ORBM_T][32];  // upper halves' lists
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int h = lane >> 5, c = lane & 31;
+  int bx, np;
+  frame_unit(bx, np);  // a node pair's row chunks share one L2 (its list2)
+  const MNodePair NP = nps[np];
+  const int a0 = bx * 128;
+  if (a0 >= NP.n1) return;  // workgroup-uniform
+  const MProblem P = probs[NP.prob];
+  const uint32_t* f2 = P.feat2 + NP.off2;
+  const int n2 = NP.n2;
+  const int a = a0 + 32 * wave + c;
+  const bool act = a < NP.n1;
+  int idx1 = 0;
+  bool v1 = false;
+  v4i_ bf[NK];
+  {
+    uint4 q0 = make_uint4(0, 0, 0, 0), q1 = q0;
+    if (act) {
+      idx1 = (int)P.feat1[NP.off1 + a];
+      v1 = !(P.valid1 && !P.valid1[idx1]);
+      q0 = reinterpret_cast<const uint4*>(P.desc1 + (size_t)idx1 * 32)[0];
+      q1 = reinterpret_cast<const uint4*>(P.desc1 + (size_t)idx1 * 32)[1];
+    }
+    const uint32_t dw[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
+#pragma unroll
+    for (int s = 0; s < NK; ++s) bf[s] = pm1_bytes((dw[s] >> (16 * h)) & 0xFFFFu, false);
+  }
+  const uint32_t sent = (uint32_t)P.dcap << 16;
+  uint32_t L[ORBM_T];
+#pragma unroll
+  for (int t = 0; t < ORBM_T; ++t) L[t] = sent;
+  uint32_t posv[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) posv[i] = (uint32_t)((i & 3) + 8 * (i >> 2) + 4 * h) + ((uint32_t)(32 * NK) << 15);
+  const v4i_* gx = gx2 + (size_t)NP.g2 * NK * 2 + h;
+  v4i_ af[NK], an[NK];
+#pragma unroll
+  for (int s = 0; s < NK; ++s) af[s] = n2 > 0 ? gx[(size_t)min(c, n2 - 1) * NK * 2 + 2 * s] : v4i_{0, 0, 0, 0};
+  for (int t0 = 0; t0 < n2; t0 += 32) {  // wave-uniform
+    const bool more = t0 + 32 < n2;
+    const int pn = min(t0 + 32 + c, n2 - 1);
+#pragma unroll
+    for (int s = 0; s < NK; ++s) an[s] = gx[(size_t)pn * NK * 2 + 2 * s];  // next tile (clamped)
+    // accumulate from 0 (an inline-constant C operand, no per-tile init):
+    // C = 2h - K, and K << 15 is folded into the position offsets
+    v16i_ C = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[0], bf[0], v16i_{}, 0, 0, 0);
+#pragma unroll
+    for (int s = 1; s < NK; ++s) C = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[s], bf[s], C, 0, 0, 0);
+    uint32_t k[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) k[i] = ((uint32_t)C[i] << 15) + posv[i] + (uint32_t)t0;
+    if (!more) {  // last tile: positions past the list
+#pragma unroll
+      for (int i = 0; i < 16; ++i)
+        if ((posv[i] & 0x7FFFu) + (uint32_t)t0 >= (uint32_t)n2) k[i] = 0xFFFFFFFFu;
+    }
+    uint32_t m = min(min(min(k[0], k[1]), min(k[2], k[3])), min(min(k[4], k[5]), min(k[6], k[7])));
+    m = min(m, min(min(min(k[8], k[9]), min(k[10], k[11])), min(min(k[12], k[13]), min(k[14], k[15]))));
+    if (__ballot(m < L[ORBM_T - 1])) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i)
+        if (__ballot(k[i] < L[ORBM_T - 1])) topk_insert(L, k[i]);
+    }
+#pragma unroll
+    for (int s = 0; s < NK; ++s) af[s] = an[s];
+  }
+  // merge the two halves' lists of each row (keys unique: position inside)
+  if (h) {
+#pragma unroll
+    for (int t = 0; t < ORBM_T; ++t) ml[wave][t][c] = L[t];
+  }
+  __syncthreads();
+  if (h) return;
+#pragma unroll
+  for (int t = 0; t < ORBM_T; ++t) {
+    const uint32_t kk = ml[wave][t][c];
+    if (__ballot(kk < L[ORBM_T - 1])) topk_insert(L, kk);
+  }
+  const bool full = L[ORBM_T - 1] < sent;
+#pragma unroll
+  for (int t = 0; t < ORBM_T; ++t)
+    if (L[t] >= sent) L[t] = 0xFFFFFFFFu;
+  if (!act) return;
+  const int r = NP.row_base + a;
+  ev[r] = make_int2(-1, 0);
+  if (!v1) {
+    rowinfo[r] = make_int4(0, 0, 0, idx1);
+    return;
+  }
+  const int minD = L[0] != 0xFFFFFFFFu ? (int)(L[0] >> 16) : (1 << 20);
+  rowinfo[r] = make_int4(1, full ? ORBM_T + 1 : 0, minD, idx1);
+  if (minD >= ORBM_TH_LOW) return;
+  uint4* out = reinterpret_cast<uint4*>(cand + (size_t)r * ORBM_T);
+#pragma unroll
+  for (int t = 0; t < ORBM_T / 2; ++t) {
+    const uint32_t ka = L[2 * t], kb = L[2 * t + 1];
+    out[t] = make_uint4(ka, ka != 0xFFFFFFFFu ? f2[ka & 0xFFFFu] : 0u, kb,
+                        kb != 0xFFFFFFFFu ? f2[kb & 0xFFFFu] : 0u);
+  }
+}
+template __global__ void k_match_cand_mfma<6>(const MProblem*, const MNodePair*, const v4i_*, uint2*,
+                                              int4*, int2*);
+template __global__ void k_match_cand_mfma<8>(const MProblem*, const MNodePair*, const v4i_*, uint2*,
+                                              int4*, int2*);
+
+// ---------------------------------------------------------------------------
 // k_match_resolve: greedy, in list order.  unit = node pair (parallel mode)
 // or problem (sequential mode: all its node pairs, one bitmap).
 // ---------------------------------------------------------------------------
