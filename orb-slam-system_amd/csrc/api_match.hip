@@ -25,6 +25,7 @@ __global__ void k_match_expand2(const MNodePair*, const uint4*, v4i_*);
 template <int NK>
 __global__ void k_match_cand_mfma(const MProblem*, const MNodePair*, const v4i_*, uint2*, int4*,
                                   int2*);
+
 __global__ void k_match_resolve(const MProblem*, const MNodePair*, int, int, const uint2*,
                                 const int4*, int2*);
 __global__ void k_match_resolve_spec(const MProblem*, const MNodePair*, int, const uint2*,
@@ -42,6 +43,7 @@ using namespace orbx;
 #ifndef ORBM_MFMA
 #define ORBM_MFMA 1 /* 0: VALU distances everywhere (profiling variant) */
 #endif
+
 
 namespace {
 

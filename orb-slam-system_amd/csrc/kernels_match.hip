@@ -567,6 +567,42 @@ __global__ __launch_bounds__(256) void k_match_expand2(const MNodePair* __restri
 template __global__ void k_match_expand2<6>(const MNodePair*, const uint4*, v4i_*);
 template __global__ void k_match_expand2<8>(const MNodePair*, const uint4*, v4i_*);
 
+// one 32-position x 32-row tile: distances on the MFMA, keys and top-T
+// insertions of the lane's 16 (row, position) values on the VALU
+// hoff = 4h + (K << 15): the lane half's position offset and the K bias;
+// value i of the tile is position t0 + (i & 3) + 8 (i >> 2) + 4h
+template <int NK>
+__device__ __forceinline__ void mfma_tile(const v4i_ (&af)[NK], const v4i_ (&bf)[NK], uint32_t t0,
+                                          int n2, uint32_t hoff, uint32_t (&L)[ORBM_T]) {
+  // accumulate from 0 (an inline-constant C operand, no per-tile init):
+  // C = 2h - K, and K << 15 is folded into the position offsets
+  v16i_ C = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[0], bf[0], v16i_{}, 0, 0, 0);
+#pragma unroll
+  for (int s = 1; s < NK; ++s) C = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[s], bf[s], C, 0, 0, 0);
+  uint32_t k[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) k[i] = ((uint32_t)C[i] << 15) + hoff + (t0 + (uint32_t)((i & 3) + 8 * (i >> 2)));
+  if (t0 + 32 > (uint32_t)n2) {  // last tile: positions past the list
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+      if ((hoff & 0x7FFFu) + t0 + (uint32_t)((i & 3) + 8 * (i >> 2)) >= (uint32_t)n2) k[i] = 0xFFFFFFFFu;
+  }
+  uint32_t m = min(min(min(k[0], k[1]), min(k[2], k[3])), min(min(k[4], k[5]), min(k[6], k[7])));
+  m = min(m, min(min(min(k[8], k[9]), min(k[10], k[11])), min(min(k[12], k[13]), min(k[14], k[15]))));
+  if (__ballot(m < L[ORBM_T - 1])) {
+    // the 16 tests against the tile-start threshold, all issued before the
+    // first insertion (an insertion of a key >= the current last entry is
+    // a no-op, so a stale threshold only adds no-op insertions)
+    const uint32_t l7 = L[ORBM_T - 1];
+    unsigned long long bm[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) bm[i] = __ballot(k[i] < l7);
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+      if (bm[i]) topk_insert(L, k[i]);
+  }
+}
+
 // 128 rows per workgroup, 32 per wave: lane l holds row a0 + 32w + (l & 31)
 // as the B operand (K bits of its half h = l >> 5 per step), and gets back
 // C[position][row] for the 16 positions (i&3) + 8(i>>2) + 4h of each 32-
@@ -614,38 +650,16 @@ __global__ __launch_bounds__(256) void k_match_cand_mfma(
   uint32_t L[ORBM_T];
 #pragma unroll
   for (int t = 0; t < ORBM_T; ++t) L[t] = sent;
-  uint32_t posv[16];
-#pragma unroll
-  for (int i = 0; i < 16; ++i) posv[i] = (uint32_t)((i & 3) + 8 * (i >> 2) + 4 * h) + ((uint32_t)(32 * NK) << 15);
+  const uint32_t hoff = (uint32_t)(4 * h) + ((uint32_t)(32 * NK) << 15);
   const v4i_* gx = gx2 + (size_t)NP.g2 * NK * 2 + h;
   v4i_ af[NK], an[NK];
 #pragma unroll
   for (int s = 0; s < NK; ++s) af[s] = n2 > 0 ? gx[(size_t)min(c, n2 - 1) * NK * 2 + 2 * s] : v4i_{0, 0, 0, 0};
   for (int t0 = 0; t0 < n2; t0 += 32) {  // wave-uniform
-    const bool more = t0 + 32 < n2;
     const int pn = min(t0 + 32 + c, n2 - 1);
 #pragma unroll
     for (int s = 0; s < NK; ++s) an[s] = gx[(size_t)pn * NK * 2 + 2 * s];  // next tile (clamped)
-    // accumulate from 0 (an inline-constant C operand, no per-tile init):
-    // C = 2h - K, and K << 15 is folded into the position offsets
-    v16i_ C = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[0], bf[0], v16i_{}, 0, 0, 0);
-#pragma unroll
-    for (int s = 1; s < NK; ++s) C = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[s], bf[s], C, 0, 0, 0);
-    uint32_t k[16];
-#pragma unroll
-    for (int i = 0; i < 16; ++i) k[i] = ((uint32_t)C[i] << 15) + posv[i] + (uint32_t)t0;
-    if (!more) {  // last tile: positions past the list
-#pragma unroll
-      for (int i = 0; i < 16; ++i)
-        if ((posv[i] & 0x7FFFu) + (uint32_t)t0 >= (uint32_t)n2) k[i] = 0xFFFFFFFFu;
-    }
-    uint32_t m = min(min(min(k[0], k[1]), min(k[2], k[3])), min(min(k[4], k[5]), min(k[6], k[7])));
-    m = min(m, min(min(min(k[8], k[9]), min(k[10], k[11])), min(min(k[12], k[13]), min(k[14], k[15]))));
-    if (__ballot(m < L[ORBM_T - 1])) {
-#pragma unroll
-      for (int i = 0; i < 16; ++i)
-        if (__ballot(k[i] < L[ORBM_T - 1])) topk_insert(L, k[i]);
-    }
+    mfma_tile<NK>(af, bf, (uint32_t)t0, n2, hoff, L);
 #pragma unroll
     for (int s = 0; s < NK; ++s) af[s] = an[s];
   }
