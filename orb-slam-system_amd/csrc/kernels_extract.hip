@@ -1201,11 +1201,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OB_WPE))) v
   {
     // task = (row pair rp, 4-column group q): patch columns 4q..4q+3, rows
     // 2rp, 2rp+1; the 7-byte windows c-3..c+3 lie in dwords q-1..q+1
+    // cc = x - px0 is 21..24, so the columns cc-18..cc+18 always span the 10
+    // groups qlo..qlo+9 (qlo = 0 for cc = 21, else 1): a constant task grid,
+    // stepped per round without a division
     const int cc = me.x - me.px0;
-    const int qlo = (cc - 18) >> 2, qhi = (cc + 18) >> 2, nq = qhi - qlo + 1;
-    const int ntask = KP_HPAIRS * nq;
-    for (int t = lane; t < ntask; t += 64) {
-      const int rp = t / nq, q = qlo + t - rp * nq;
+    const int qlo = (cc - 18) >> 2;
+    constexpr int NQ = 10, NTASK = KP_HPAIRS * NQ;
+    int rp = lane / NQ, qq = lane - (lane / NQ) * NQ;
+    for (int t = lane; t < NTASK; t += 64) {
+      const int q = qlo + qq;
       const int r0 = 2 * rp, r1 = min(2 * rp + 1, KP_ROWS - 1);
       const int d0 = max(q - 1, 0);  // q == 0: the weights of dword q-1 are 0 for the columns used
       const uint32_t a0 = P[r0][d0], a1 = P[r0][q], a2 = P[r0][q + 1];
@@ -1218,6 +1222,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OB_WPE))) v
         const uint32_t h1 = __builtin_amdgcn_udot4(b2, W2, __builtin_amdgcn_udot4(b1, W1, __builtin_amdgcn_udot4(b0, W0, 0u, false), false), false);
         hblur[wave][4 * q + m][rp] = h0 | (h1 << 16);
       }
+      rp += 64 / NQ;
+      qq += 64 % NQ;
+      if (qq >= NQ) { qq -= NQ; ++rp; }
     }
   }
   // IC_Angle (:21-48) on the unblurred level (integer sums: order-free).
