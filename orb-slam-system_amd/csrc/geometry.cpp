@@ -287,7 +287,12 @@ static bool build_blobs(Plan& P, const std::vector<int>& lev, PyrSeg& g, const s
           if (cf[0] < 0 || cf[0] > 4095 || cf[1] < 0 || cf[1] > 4095) return false;
           if (isx && ((d - b) & 3) == 0) glo = lo;
           if (isx && hi - glo > 7) return false;
-          P.pyr_blob.push_back((uint32_t)(lo - origin) | ((uint32_t)(hi - origin) << 16));
+          if (!isx)
+            P.pyr_blob.push_back((uint32_t)(lo - origin) | ((uint32_t)(hi - origin) << 16));
+          else if (((d - b) & 3) == 0) /* group column 0: s0 | (sx1 - s0) << 16 */
+            P.pyr_blob.push_back((uint32_t)(lo - origin) | ((uint32_t)(hi - lo) << 16));
+          else /* columns 1..3: k_pyramid's v_perm selector, bytes relative to s0 */
+            P.pyr_blob.push_back((uint32_t)(lo - glo) | 0x0C00u | ((uint32_t)(hi - glo) << 16) | 0x0C000000u);
           P.pyr_blob.push_back((uint32_t)(uint16_t)cf[0] | ((uint32_t)(uint16_t)cf[1] << 16));
           ++n;
         }

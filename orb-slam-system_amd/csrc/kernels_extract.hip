@@ -207,26 +207,34 @@ __global__ __launch_bounds__(256) void k_pyramid(const uint8_t* __restrict__ fra
     const int nrows = max(Y.y - Y.x, 0);
     const int dpitch = 4 * ncg;
     if (ncg > 0 && nrows > 0) {
-      const int R = 256 / ncg;
+      // tid / ncg and 256 / ncg through the float reciprocal: exact for
+      // integers <= 256.5 (relative error ~1e-7 against a margin >= 0.5 / ncg)
+      const float rcp = __builtin_amdgcn_rcpf((float)ncg);
+      const int R = (int)(256.5f * rcp);
       if (tid < R * ncg) {
-        const int cg = tid % ncg, r0 = tid / ncg;
+        const int r0 = (int)(((float)tid + 0.5f) * rcp), cg = tid - r0 * ncg;
         // the 4 columns' source bytes lie in an 8-byte window from sx[0]
         // (scale < 2: sx1[3] - sx[0] <= 7, checked by the planner): two
         // v_alignbyte of three LDS dwords per source row, then one v_perm
         // (bytes sx, sx1 -> u16 pair) and one v_dot2_u32_u16 with the
         // (a0, a1) pair per column: D = S[sx]*a0 + S[sx1]*a1
+        // blob (geometry.cpp build_blobs): column 0 of the group holds
+        // s0 | (sx1 - s0) << 16, columns 1..3 their v_perm selectors
+        // relative to s0; .y = a0 | a1 << 16, both in [0, 2048]
         uint32_t hsel[4], hcoef[4];
         int hbase, hsh;
         {
-          const int s0 = (int)(xl[xo + 4 * cg].x & 0xFFFF);
+          const uint2 e0 = xl[xo + 4 * cg];
+          const int s0 = (int)(e0.x & 0xFFFF);
           hbase = s0 & ~3;
           hsh = s0 & 3;
+          hsel[0] = (e0.x & 0xFFFF0000u) | 0x0C000C00u;
+          hcoef[0] = e0.y;
 #pragma unroll
-          for (int k = 0; k < 4; ++k) {
+          for (int k = 1; k < 4; ++k) {
             const uint2 e = xl[xo + 4 * cg + k];
-            const uint32_t o0 = (e.x & 0xFFFF) - (uint32_t)s0, o1 = (e.x >> 16) - (uint32_t)s0;
-            hsel[k] = o0 | 0x0C00u | (o1 << 16) | 0x0C000000u;
-            hcoef[k] = e.y;  // a0 | a1 << 16, both in [0, 2048]
+            hsel[k] = e.x;
+            hcoef[k] = e.y;
           }
         }
         const int gx0 = dax + 4 * cg;
@@ -271,7 +279,7 @@ __global__ __launch_bounds__(256) void k_pyramid(const uint8_t* __restrict__ fra
             const int y = Y.x + r;
             *reinterpret_cast<uint32_t*>(nxt + r * dpitch + 4 * cg) = packed[u];
             if (y >= Y.z && y < Y.w && any_x) {
-              uint8_t* o = gdst + (size_t)y * gp + gx0;
+              uint8_t* o = gdst + (uint32_t)(y * gp + gx0);  // a level is < 4 GB
               if (in_x) {
                 *reinterpret_cast<uint32_t*>(o) = packed[u];  // pyr offsets/pitches are 16-B multiples
               } else {

@@ -75,7 +75,12 @@ int main(int argc, char** argv) {
             }
             for (int c = dax; c < dax + dpitch; ++c) {
               const uint32_t* xe = &P.pyr_blob[2 * (xb + xo + c - dax)];
-              const int sx = xe[0] & 0xFFFF, sx1 = xe[0] >> 16;
+              // x entries per 4-column group: column 0 = s0 | (sx1 - s0) << 16,
+              // columns 1..3 = v_perm selectors (bytes 0 / 2) relative to s0
+              const uint32_t g0 = P.pyr_blob[2 * (xb + xo + ((c - dax) & ~3))];
+              const int s0 = g0 & 0xFFFF;
+              const int sx = ((c - dax) & 3) ? s0 + (int)(xe[0] & 0xFF) : s0;
+              const int sx1 = ((c - dax) & 3) ? s0 + (int)((xe[0] >> 16) & 0xFF) : s0 + (int)(xe[0] >> 16);
               const int a0 = (int16_t)(xe[1] & 0xFFFF), a1 = (int16_t)(xe[1] >> 16);
               auto rd = [&](int rr, int cc) {
                 if (rr < 0 || rr >= cy1 - cay || cc < 0 || cc >= cpitch) fail("oob", rr, cc);
