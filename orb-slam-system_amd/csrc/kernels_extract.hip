@@ -633,8 +633,10 @@ __global__ __launch_bounds__(FS_NT) void k_fast_strips(
   // thresholds in one scan: iniThFAST into mask (+ per-cell counts) and
   // minThFAST into mask2, used for cells left empty at iniThFAST (:293-296)
   const int wcell = st.wcell;
+  // (c - c0) / wcell through the float reciprocal (exact: c - c0 < 512)
+  const float rwcell = __builtin_amdgcn_rcpf((float)wcell);
   auto nms_pixel = [&](int r, int c, int a) {
-    const int k = min((c - c0) / wcell, st.ncells - 1);
+    const int k = min((int)(((float)(c - c0) + 0.5f) * rwcell), st.ncells - 1);
     const int cb0 = c0 + k * wcell, cb1 = (k == st.ncells - 1) ? c1 : cb0 + wcell;
     int nbm = 0, nbi = 0;  // max neighbour score at min / ini threshold (0 outside the band)
 #pragma unroll
