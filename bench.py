@@ -183,14 +183,15 @@ def roofline_entries(st, steps, by, geo, B, traffic):
             "algorithmic_bytes_per_launch": round(by[dom] / launches),
             "launches_per_step": launches, "avg_launch_ms": round(per_step[dom] / launches, 5)}
     # the north-star pass: pyramid + FAST together
-    t = per_step.get("resize", 0.0) + per_step.get("fast_cells", 0.0)
+    # (a single-level plan launches no resize kernel: its empty stage is left out)
+    pk = [k for k in ("resize", "fast_cells") if k in per_step and by.get(k, 0) > 0]
+    t = sum(per_step[k] for k in pk)
     pf = None
     if t > 0:
-        b = by["resize"] + by["fast_cells"]
+        b = sum(by[k] for k in pk)
         bmin = min_pyr_fast_bytes(geo, B)
-        trs = [traffic.get(k, {}).get("bytes_per_launch") for k in ("resize", "fast_cells")
-               if k in per_step]
-        pf = {"bound": "hbm", "kernels": [k for k in ("resize", "fast_cells") if k in per_step],
+        trs = [traffic.get(k, {}).get("bytes_per_launch") for k in pk]
+        pf = {"bound": "hbm", "kernels": pk,
               "ms_per_step": round(t, 5), "algorithmic_bytes_per_step": b,
               "achieved": round(b / (t * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
               "frac": round(b / (t * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
