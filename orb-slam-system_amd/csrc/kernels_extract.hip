@@ -21,6 +21,8 @@
 #include "brief_pattern.inc"
 #define ORBX_SINCOS_STORAGE static __constant__ const
 #include "sincos_exceptions.inc"
+#define ORBX_HTASK_STORAGE static __constant__ const
+#include "brief_htasks.inc"
 
 namespace orbx {
 
@@ -1052,6 +1054,7 @@ __device__ constexpr uint32_t kb_w(int m, int d) {
 #define KP_COLS 48
 #define KP_HCOLS 44  /* hblur columns: patch columns 0..43 (samples use cc-18..cc+18 <= 42) */
 #define KP_HPAIRS 22 /* hblur row pairs: rows 0..43 (row 43 never weighted) */
+#define KP_PSTRIDE (KP_COLS / 4) /* patch row, dwords (+1 padding: no change measured) */
 
 // One keypoint of the frame's level-major output list: where its level
 // lives and where its patch starts (all wave-uniform).
@@ -1115,7 +1118,7 @@ __device__ __forceinline__ void brief_commit(const BriefRegs& R, uint32_t* P, in
 #pragma unroll
     for (int u = 0; u < 9; ++u) {
       const int row = r0 + 5 * u;
-      if (row < KP_ROWS) P[row * (KP_COLS / 4) + c] = R.r[u];
+      if (row < KP_ROWS) P[row * KP_PSTRIDE + c] = R.r[u];
     }
   }
 }
@@ -1129,10 +1132,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OB_WPE))) v
     const uint32_t* __restrict__ qout, size_t qout_stride, const int* __restrict__ lcount,
     orbx_keypoint* __restrict__ kps, uint8_t* __restrict__ desc, int* __restrict__ counts,
     int dbg) {
-  __shared__ uint32_t patch[4][KP_ROWS][KP_COLS / 4];
+  __shared__ uint32_t patch[4][KP_ROWS][KP_PSTRIDE];
   // horizontally blurred patch, column-major: hblur[w][patch col][row pair]
   // = (H(row 2k), H(row 2k+1)) as u16 pair, H = sum_i k_i p (7 taps)
   __shared__ uint32_t hblur[4][KP_HCOLS][KP_HPAIRS];
+  // horizontal-pass tasks per keypoint column cc = 21..24 (brief_htasks.inc)
+  __shared__ uint16_t htask[4][192];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   int bx, f;
   frame_unit(bx, f);
@@ -1145,7 +1150,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OB_WPE))) v
   if (bx == 0 && threadIdx.x == 0) counts[f] = total;
   const int excl = incl - lcv;
   const uint32_t* Q = qout + (size_t)f * qout_stride;
-  uint32_t(*P)[KP_COLS / 4] = patch[wave];
+  uint32_t(*P)[KP_PSTRIDE] = patch[wave];
   // the 256 test pairs {x0, y0, x1, y1} in LDS (ds_read, not a vector load
   // that would wait behind the patch prefetch)
   // sincos exception keys, entries lane and lane + 64 (brief_sincos)
@@ -1153,6 +1158,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OB_WPE))) v
   const uint32_t exk1 = lane + 64 < ORBX_SINCOS_NEXC ? ORBX_SINCOS_EXC[lane + 64][0] : 0xFFFFFFFFu;
   __shared__ uint32_t spat[256];
   spat[threadIdx.x] = *reinterpret_cast<const uint32_t*>(ORBX_BRIEF_PATTERN[threadIdx.x]);
+  for (int i = threadIdx.x; i < 4 * 192; i += 256) (&htask[0][0])[i] = (&ORBX_HTASK[0][0])[i];
   __syncthreads();
   // output position o -> keypoint.  Everything is wave-uniform and forced
   // scalar (readfirstlane): the key and the level tables are s_loads, so the
@@ -1212,14 +1218,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OB_WPE))) v
     // task = (row pair rp, 4-column group q): patch columns 4q..4q+3, rows
     // 2rp, 2rp+1; the 7-byte windows c-3..c+3 lie in dwords q-1..q+1
     // cc = x - px0 is 21..24, so the columns cc-18..cc+18 always span the 10
-    // groups qlo..qlo+9 (qlo = 0 for cc = 21, else 1): a constant task grid,
-    // stepped per round without a division
+    // groups qlo..qlo+9 (qlo = 0 for cc = 21, else 1).  Of those 22 x 10
+    // tasks only the ones under a rotated sample's taps are computed: the
+    // live pattern points stay within a fixed radius at every angle
+    // (tools/gen_brief_htasks.py), 189-190 tasks, 3 rounds of 64 lanes
     const int cc = me.x - me.px0;
     const int qlo = (cc - 18) >> 2;
-    constexpr int NQ = 10, NTASK = KP_HPAIRS * NQ;
-    int rp = lane / NQ, qq = lane - (lane / NQ) * NQ;
-    for (int t = lane; t < NTASK; t += 64) {
-      const int q = qlo + qq;
+    const uint16_t* ht = htask[cc - 21];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const uint32_t e = ht[lane + 64 * k];
+      if (e == 0xFFFFu) continue;
+      const int rp = (int)(e >> 8), q = qlo + (int)(e & 0xFFu);
       const int r0 = 2 * rp, r1 = min(2 * rp + 1, KP_ROWS - 1);
       const int d0 = max(q - 1, 0);  // q == 0: the weights of dword q-1 are 0 for the columns used
       const uint32_t a0 = P[r0][d0], a1 = P[r0][q], a2 = P[r0][q + 1];
@@ -1232,9 +1242,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OB_WPE))) v
         const uint32_t h1 = __builtin_amdgcn_udot4(b2, W2, __builtin_amdgcn_udot4(b1, W1, __builtin_amdgcn_udot4(b0, W0, 0u, false), false), false);
         hblur[wave][4 * q + m][rp] = h0 | (h1 << 16);
       }
-      rp += 64 / NQ;
-      qq += 64 % NQ;
-      if (qq >= NQ) { qq -= NQ; ++rp; }
     }
   }
   // IC_Angle (:21-48) on the unblurred level (integer sums: order-free).
