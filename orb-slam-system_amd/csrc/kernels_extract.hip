@@ -1124,7 +1124,7 @@ __device__ __forceinline__ void brief_commit(const BriefRegs& R, uint32_t* P, in
 }
 
 #ifndef OB_WPE
-#define OB_WPE 5
+#define OB_WPE 6
 #endif
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OB_WPE))) void k_orient_brief(
     const uint8_t* __restrict__ frames, size_t fstride, size_t rstride,
