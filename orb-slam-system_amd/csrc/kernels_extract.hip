@@ -462,7 +462,8 @@ __global__ __launch_bounds__(FS_NT) void k_fast_strips(
   __shared__ uint16_t clist[FS_CCAP];  // corners at t_lo (A > t_lo), any order
   __shared__ int cslot[ORBX_STRIP_MAXCELLS];
   __shared__ int ncorner;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // uniform: list bases in SGPRs
   // plain grid: with 8 strip columns at 1080p level 0, XCD (f*S + s) % 8 is
   // a strip column, whose ring rows then meet in one L2.  Frame-grouped
   // (frame_unit) and 4..256-strip chunked mappings cut the traffic 1.66x ->
@@ -598,9 +599,12 @@ __global__ __launch_bounds__(FS_NT) void k_fast_strips(
         const uint32_t x = (j & 1) ? chi : clo;
         const bool k = ((j & 2) ? (x >> 16) : (x & 0xFFFFu)) != 0;
         const unsigned long long bal = __ballot(k);
+        // slot = mbcnt of the ballot from 0, stored at the uniform L1 + n1
+        // (no VGPR copy of n1 per append)
         const int pos = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
-                                                       __builtin_amdgcn_mbcnt_lo((uint32_t)bal, (uint32_t)n1));
-        if (k) L1[pos] = (uint16_t)(ebase + (uint32_t)j);
+                                                       __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+        uint16_t* const L1n = L1 + __builtin_amdgcn_readfirstlane(n1);
+        if (k) L1n[pos] = (uint16_t)(ebase + (uint32_t)j);
         n1 += __popcll(bal);
       }
 #endif

@@ -823,6 +823,9 @@ __global__ __launch_bounds__(256) void k_match_resolve(
 // boundary: every pending row before it is exactly what the serial walk
 // would decide, so those commit together and the rest re-decide.
 // ---------------------------------------------------------------------------
+#ifndef RS_NB
+#define RS_NB 2
+#endif
 __global__ __launch_bounds__(64) void k_match_resolve_spec(
     const MProblem* __restrict__ probs, const MNodePair* __restrict__ nps, int nunits,
     const uint2* __restrict__ cand, const int4* __restrict__ rowinfo, int2* __restrict__ ev,
@@ -839,8 +842,10 @@ __global__ __launch_bounds__(64) void k_match_resolve_spec(
   for (int w = lane; w < ((P.n2 + 31) >> 5); w += 64) bm[w] = 0u;
   for (int w = lane; w < P.n2; w += 64) claim[w] = 64;
   __builtin_amdgcn_wave_barrier();
-  // row info + candidate lists of the chunks two ahead are in flight while
-  // a chunk resolves (two register buffers, used alternately)
+  // row info + candidate lists of the RS_NB chunks ahead are in flight while
+  // a chunk resolves (RS_NB register buffers, used in turn; one wave per
+  // node pair, so registers are not what limits this kernel -- the walk is
+  // bound by the latency of these loads)
   // (unconditional loads at a clamped row: a load under a divergent branch
   // would be waited for at the branch join; rows past n1 are masked in chunk)
   auto fetch = [&](int4& inf_n, uint4 (&cv_n)[ORBM_T / 2], int base) {
@@ -866,7 +871,7 @@ __global__ __launch_bounds__(64) void k_match_resolve_spec(
     // the buffer is consumed before it is refilled, so the refill can take the
     // same registers (otherwise the loop latch copies it, waiting on vmcnt)
     __builtin_amdgcn_sched_barrier(0);
-    fetch(inf_n, cv_n, base + 128);  // unconditional (clamped rows)
+    fetch(inf_n, cv_n, base + 64 * RS_NB);  // unconditional (clamped rows)
     uint64_t pend = __ballot(feas);
     if (!pend) return;
 #ifdef RS_STATS
@@ -952,14 +957,15 @@ __global__ __launch_bounds__(64) void k_match_resolve_spec(
       }
     }
   };
-  int4 infA, infB;
-  uint4 cvA[ORBM_T / 2], cvB[ORBM_T / 2];
+  int4 inf[RS_NB];
+  uint4 cv[RS_NB][ORBM_T / 2];
   if (NP.n1 <= 0) return;
-  fetch(infA, cvA, 0);
-  fetch(infB, cvB, 64);
-  for (int base = 0; base < NP.n1; base += 128) {
-    chunk(infA, cvA, base);
-    if (base + 64 < NP.n1) chunk(infB, cvB, base + 64);
+#pragma unroll
+  for (int b = 0; b < RS_NB; ++b) fetch(inf[b], cv[b], 64 * b);
+  for (int base = 0; base < NP.n1; base += 64 * RS_NB) {
+#pragma unroll
+    for (int b = 0; b < RS_NB; ++b)
+      if (base + 64 * b < NP.n1) chunk(inf[b], cv[b], base + 64 * b);
   }
 #ifdef RS_STATS
   if (lane == 0 && unit < 4)
