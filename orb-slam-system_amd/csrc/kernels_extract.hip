@@ -1142,7 +1142,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OB_WPE))) v
   __shared__ uint32_t hblur[4][KP_HCOLS][KP_HPAIRS];
   // horizontal-pass tasks per keypoint column cc = 21..24 (brief_htasks.inc)
   __shared__ uint16_t htask[4][192];
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   int bx, f;
   frame_unit(bx, f);
   const int g = bx * 4 + wave;

@@ -133,7 +133,7 @@ __global__ __launch_bounds__(256) void k_stereo_match(
     float* __restrict__ uright, float* __restrict__ depth, int* __restrict__ sad,
     int* __restrict__ err) {
   __shared__ int part[4][128];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int f = blockIdx.y;
   const int nl = cnt_l[f];
   const orbx_keypoint* KL = kps_l + (size_t)f * A.kcap;
