@@ -542,85 +542,98 @@ __global__ __launch_bounds__(FS_NT) void k_fast_strips(
   };
   {
     const uint32_t tt = (uint32_t)t_lo * 0x00010001u;
-    const int it_first = wave * 64 + lane;
-    int r = 3 + it_first / ng, g = g0 + it_first % ng;
-    const int dr = FS_NT / ng, dg = FS_NT - dr * ng;
-    for (int it0 = wave * 64; it0 < ntask; it0 += FS_NT) {  // wave-uniform trip count
-      const int it = it0 + lane;
+    // one 4-pixel group: tile byte offset off = r * tpitch + 4 g, list entry
+    // ebase = r << 9 | 4 g; a lane with threshold 0xFF00 per 16-bit lane
+    // (padding) finds no survivors; zf: zero the group's strength-map dword
+    // (a padding lane may only repeat a group some lane of the same call
+    // zeroes: a later zero would erase strengths already written)
+    auto group = [&](uint32_t off, uint32_t ebase, uint32_t ttl, bool zf) {
+      // (g = 0: w0 is the previous row's last dword -- only pixels left of
+      // the band, rejected in stage B, read it; r >= 3 keeps it in the tile)
+      const uint32_t* row0 = reinterpret_cast<const uint32_t*>(tile + off);
+      const uint32_t w0 = row0[-1], w1 = row0[0], w2 = row0[1];
+      const uint32_t up = *reinterpret_cast<const uint32_t*>(tile + off - 3 * tpitch);
+      const uint32_t dn = *reinterpret_cast<const uint32_t*>(tile + off + 3 * tpitch);
+      const uint32_t I4 = __builtin_amdgcn_alignbyte(w2, w1, 3);   // (x+3, y)
+      const uint32_t I12 = __builtin_amdgcn_alignbyte(w1, w0, 1);  // (x-3, y)
       uint32_t clo = 0, chi = 0;  // candidate words: pixels 0,2 / 1,3 (16-bit lanes)
-      if (it < ntask) {
-        // (g = 0: w0 is the previous row's last dword -- only pixels left of
-        // the band, rejected in stage B, read it; r >= 3 keeps it in the tile)
-        const int ro = __mul24(r, tpitch);
-        const uint32_t* row0 = reinterpret_cast<const uint32_t*>(tile + ro);
-        const uint32_t w0 = row0[g - 1], w1 = row0[g], w2 = row0[g + 1];
-        const uint32_t up = reinterpret_cast<const uint32_t*>(tile + ro - 3 * tpitch)[g];
-        const uint32_t dn = reinterpret_cast<const uint32_t*>(tile + ro + 3 * tpitch)[g];
-        const uint32_t I4 = __builtin_amdgcn_alignbyte(w2, w1, 3);   // (x+3, y)
-        const uint32_t I12 = __builtin_amdgcn_alignbyte(w1, w0, 1);  // (x-3, y)
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const uint32_t sel = h ? 0x0c030c01u : 0x0c020c00u;
-          const us2 v = as_us2(__builtin_amdgcn_perm(0u, w1, sel));
-          const us2 a0 = as_us2(__builtin_amdgcn_perm(0u, dn, sel));
-          const us2 a8 = as_us2(__builtin_amdgcn_perm(0u, up, sel));
-          const us2 a4 = as_us2(__builtin_amdgcn_perm(0u, I4, sel));
-          const us2 a12 = as_us2(__builtin_amdgcn_perm(0u, I12, sel));
-          const us2 t2 = as_us2(tt);
-          const us2 mb = __builtin_elementwise_min(__builtin_elementwise_max(a0, a8),
-                                                   __builtin_elementwise_max(a4, a12));
-          const us2 md = __builtin_elementwise_max(__builtin_elementwise_min(a0, a8),
-                                                   __builtin_elementwise_min(a4, a12));
-          const us2 db = __builtin_elementwise_sub_sat(mb, v + t2);       // > 0 iff brighter arc
-          const us2 dd = __builtin_elementwise_sub_sat(__builtin_elementwise_sub_sat(v, md), t2);
-          const uint32_t x = as_u32(db) | as_u32(dd);
-          if (h) chi = x; else clo = x;
-        }
-        reinterpret_cast<uint32_t*>(amap + ro)[g] = 0u;
-#ifdef FAST_PAD
-        // profiling only: FAST_PAD dependent VALU ops per group (issue-bound probe)
-        uint32_t pz = clo;
-#pragma unroll
-        for (int z = 0; z < FAST_PAD; ++z) asm volatile("v_xor_b32 %0, %0, %1" : "+v"(pz) : "v"(chi));
-        clo |= pz & 0u;
-        asm volatile("" : "+v"(clo));
-#endif
+      for (int h = 0; h < 2; ++h) {
+        const uint32_t sel = h ? 0x0c030c01u : 0x0c020c00u;
+        const us2 v = as_us2(__builtin_amdgcn_perm(0u, w1, sel));
+        const us2 a0 = as_us2(__builtin_amdgcn_perm(0u, dn, sel));
+        const us2 a8 = as_us2(__builtin_amdgcn_perm(0u, up, sel));
+        const us2 a4 = as_us2(__builtin_amdgcn_perm(0u, I4, sel));
+        const us2 a12 = as_us2(__builtin_amdgcn_perm(0u, I12, sel));
+        const us2 t2 = as_us2(ttl);
+        const us2 mb = __builtin_elementwise_min(__builtin_elementwise_max(a0, a8),
+                                                 __builtin_elementwise_max(a4, a12));
+        const us2 md = __builtin_elementwise_max(__builtin_elementwise_min(a0, a8),
+                                                 __builtin_elementwise_min(a4, a12));
+        const us2 db = __builtin_elementwise_sub_sat(mb, v + t2);       // > 0 iff brighter arc
+        const us2 dd = __builtin_elementwise_sub_sat(__builtin_elementwise_sub_sat(v, md), t2);
+        const uint32_t x = as_u32(db) | as_u32(dd);
+        if (h) chi = x; else clo = x;
       }
-#ifdef FAST_NO_APPEND  // profiling only: stage A without the list appends
-      if (it < ntask) reinterpret_cast<uint32_t*>(amap + r * tpitch)[g] = (clo | chi) & 0x01000000u;
-#else
+      if (zf) *reinterpret_cast<uint32_t*>(amap + off) = 0u;
       // append: the ballot is the compare's SGPR result, the lane's slot is
-      // mbcnt of it, only survivors store (stores of every lane to a dummy
-      // slot measured 13 % slower).  Columns outside [c0, c1) are appended
-      // too and rejected in stage B.
-      const uint32_t ebase = ((uint32_t)r << 9) | (uint32_t)(4 * g);
+      // mbcnt of it from 0 at the uniform L1 + n1, only survivors store
+      // (stores of every lane to a dummy slot measured 13 % slower).
+      // Columns outside [c0, c1) are appended too and rejected in stage B.
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const uint32_t x = (j & 1) ? chi : clo;
         const bool k = ((j & 2) ? (x >> 16) : (x & 0xFFFFu)) != 0;
         const unsigned long long bal = __ballot(k);
-        // slot = mbcnt of the ballot from 0, stored at the uniform L1 + n1
-        // (no VGPR copy of n1 per append)
         const int pos = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
                                                        __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
         uint16_t* const L1n = L1 + __builtin_amdgcn_readfirstlane(n1);
         if (k) L1n[pos] = (uint16_t)(ebase + (uint32_t)j);
         n1 += __popcll(bal);
       }
-#endif
       if (n1 >= FS_L1FLUSH) {  // wave-uniform
         wave_sync_lds();
         while (n1 >= 64) {
           n1 -= 64;
-#ifndef FAST_SKIP_B  // profiling only: drop the cardinal survivors
           even_batch(L1[n1 + lane], true);
-#endif
         }
         wave_sync_lds();
       }
-      r += dr;
-      g += dg;
-      if (g >= g1) { g -= ng; ++r; }
+    };
+    if (ng <= 64) {
+      // row-mapped: lane = (row lr of the step, group lg); a step covers
+      // rpw = 64 / ngp rows (ngp = 16 / 32 / 64 >= ng); offsets and entries
+      // are lane constants plus a uniform row term, the loop is scalar
+      const int sh = ng <= 16 ? 4 : ng <= 32 ? 5 : 6;
+      const int rpw = 64 >> sh, lr = lane >> sh, lg = lane & ((1 << sh) - 1);
+      const bool lact = lg < ng;
+      const int g = g0 + min(lg, ng - 1);  // padding lanes repeat the last group
+      const uint32_t tl = lact ? tt : 0xFF00FF00u;
+      const uint32_t offl = (uint32_t)(__mul24(3 + lr, tpitch) + 4 * g);
+      const uint32_t el = ((uint32_t)(3 + lr) << 9) | (uint32_t)(4 * g);
+      for (int rb = wave * rpw; rb < bh; rb += FS_NW * rpw) {  // wave-uniform
+        if (rb + rpw <= bh) {
+          group(offl + (uint32_t)(rb * tpitch), el + ((uint32_t)rb << 9), tl, true);
+        } else {  // last rows: lanes past the band repeat its last row, no survivors
+          const int r = min(rb + lr, bh - 1);
+          group((uint32_t)(__mul24(3 + r, tpitch) + 4 * g), ((uint32_t)(3 + r) << 9) | (uint32_t)(4 * g),
+                rb + lr < bh ? tl : 0xFF00FF00u, true);
+        }
+      }
+    } else {
+      // flattened (row, group) tasks for bands wider than 64 groups
+      const int it_first = wave * 64 + lane;
+      int r = 3 + it_first / ng, g = g0 + it_first % ng;
+      const int dr = FS_NT / ng, dg = FS_NT - dr * ng;
+      for (int it0 = wave * 64; it0 < ntask; it0 += FS_NT) {  // wave-uniform trip count
+        const bool act = it0 + lane < ntask;
+        const int rc = act ? r : 3, gc = act ? g : g0;
+        group((uint32_t)(__mul24(rc, tpitch) + 4 * gc), ((uint32_t)rc << 9) | (uint32_t)(4 * gc),
+              act ? tt : 0xFF00FF00u, act);
+        r += dr;
+        g += dg;
+        if (g >= g1) { g -= ng; ++r; }
+      }
     }
     wave_sync_lds();
     while (n1 >= 64) {  // leftovers above one batch (FS_L1FLUSH > 64)
