@@ -22,7 +22,10 @@ __global__ void k_match_gather2(const MProblem*, const MNodePair*, uint4*, uint3
 typedef int v4i_ __attribute__((ext_vector_type(4)));
 template <int NK>
 __global__ void k_match_expand2(const MNodePair*, const uint4*, v4i_*);
-template <int NK>
+#ifndef MC_RT
+#define MC_RT 2 /* row tiles of 32 per wave in k_match_cand_mfma */
+#endif
+template <int NK, int RT>
 __global__ void k_match_cand_mfma(const MProblem*, const MNodePair*, const v4i_*, uint2*, int4*,
                                   int2*);
 
@@ -99,12 +102,12 @@ void launch_match(const MProblem* d_probs, int nprob, const MNodePair* d_nps, in
         if (six_words) {
           hipLaunchKernelGGL(k_match_expand2<6>, dim3((max_n2 * 6 + 255) / 256, nnp), dim3(256), 0, s,
                              d_nps, d_gdesc2, gx2);
-          hipLaunchKernelGGL(k_match_cand_mfma<6>, dim3((max_n1 + 127) / 128, nnp), dim3(256), 0, s,
+          hipLaunchKernelGGL((k_match_cand_mfma<6, MC_RT>), dim3((max_n1 + 128 * MC_RT - 1) / (128 * MC_RT), nnp), dim3(256), 0, s,
                              d_probs, d_nps, gx2, d_cand, d_rowinfo, d_ev);
         } else {
           hipLaunchKernelGGL(k_match_expand2<8>, dim3((max_n2 * 8 + 255) / 256, nnp), dim3(256), 0, s,
                              d_nps, d_gdesc2, gx2);
-          hipLaunchKernelGGL(k_match_cand_mfma<8>, dim3((max_n1 + 127) / 128, nnp), dim3(256), 0, s,
+          hipLaunchKernelGGL((k_match_cand_mfma<8, MC_RT>), dim3((max_n1 + 128 * MC_RT - 1) / (128 * MC_RT), nnp), dim3(256), 0, s,
                              d_probs, d_nps, gx2, d_cand, d_rowinfo, d_ev);
         }
       } else if (six_words)

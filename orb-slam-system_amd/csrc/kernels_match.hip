@@ -603,53 +603,60 @@ __device__ __forceinline__ void mfma_tile(const v4i_ (&af)[NK], const v4i_ (&bf)
   }
 }
 
-// 128 rows per workgroup, 32 per wave: lane l holds row a0 + 32w + (l & 31)
-// as the B operand (K bits of its half h = l >> 5 per step), and gets back
-// C[position][row] for the 16 positions (i&3) + 8(i>>2) + 4h of each 32-
-// position tile (gfx950 32x32 C layout).  Each lane half keeps its own
-// sorted top-T list of the row; the halves merge through LDS at the end.
-// Positions are read as A fragments straight from gx2 (L1/L2: the 4 waves
-// of a workgroup and the node pair's other workgroups read the same tiles),
-// one tile ahead.  Validity arrays are not supported (k_match_cand_rows).
-template <int NK>
+// 128 * RT rows per workgroup, 32 * RT per wave: lane l holds rows
+// a0 + 32 (RT w + t) + (l & 31), t < RT, as B operands (K bits of its half
+// h = l >> 5 per step), and gets back C[position][row] for the 16 positions
+// (i&3) + 8(i>>2) + 4h of each 32-position tile (gfx950 32x32 C layout).
+// Each lane half keeps its own sorted top-T list per row; the halves merge
+// through LDS at the end.  Positions are read as A fragments straight from
+// gx2 (L1/L2: the waves of a workgroup and the node pair's other workgroups
+// read the same tiles), one tile ahead; each fragment feeds RT MFMA chains.
+// Validity arrays are not supported (k_match_cand_rows).
+#ifndef MC_RT
+#define MC_RT 2
+#endif
+template <int NK, int RT>
 __global__ __launch_bounds__(256) void k_match_cand_mfma(
     const MProblem* __restrict__ probs, const MNodePair* __restrict__ nps,
     const v4i_* __restrict__ gx2, uint2* __restrict__ cand, int4* __restrict__ rowinfo,
     int2* __restrict__ ev) {
   static_assert(NK == 6 || NK == 8, "6 or 8 live descriptor dwords");
-  __shared__ uint32_t ml[4][ORBM_T][32];  // upper halves' lists
+  __shared__ uint32_t ml[4][RT][ORBM_T][32];  // upper halves' lists
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int h = lane >> 5, c = lane & 31;
   int bx, np;
   frame_unit(bx, np);  // a node pair's row chunks share one L2 (its list2)
   const MNodePair NP = nps[np];
-  const int a0 = bx * 128;
+  const int a0 = bx * 128 * RT;
   if (a0 >= NP.n1) return;  // workgroup-uniform
   const MProblem P = probs[NP.prob];
   const uint32_t* f2 = P.feat2 + NP.off2;
   const int n2 = NP.n2;
-  const int a = a0 + 32 * wave + c;
-  const bool act = a < NP.n1;
-  int idx1 = 0;
-  bool v1 = false;
-  v4i_ bf[NK];
-  {
+  int a[RT], idx1[RT];
+  bool act[RT], v1[RT];
+  v4i_ bf[RT][NK];
+  uint32_t L[RT][ORBM_T];
+  const uint32_t sent = (uint32_t)P.dcap << 16;
+#pragma unroll
+  for (int t = 0; t < RT; ++t) {
+    a[t] = a0 + 32 * (RT * wave + t) + c;
+    act[t] = a[t] < NP.n1;
+    idx1[t] = 0;
+    v1[t] = false;
     uint4 q0 = make_uint4(0, 0, 0, 0), q1 = q0;
-    if (act) {
-      idx1 = (int)P.feat1[NP.off1 + a];
-      v1 = !(P.valid1 && !P.valid1[idx1]);
-      q0 = reinterpret_cast<const uint4*>(P.desc1 + (size_t)idx1 * 32)[0];
-      q1 = reinterpret_cast<const uint4*>(P.desc1 + (size_t)idx1 * 32)[1];
+    if (act[t]) {
+      idx1[t] = (int)P.feat1[NP.off1 + a[t]];
+      v1[t] = !(P.valid1 && !P.valid1[idx1[t]]);
+      q0 = reinterpret_cast<const uint4*>(P.desc1 + (size_t)idx1[t] * 32)[0];
+      q1 = reinterpret_cast<const uint4*>(P.desc1 + (size_t)idx1[t] * 32)[1];
     }
     const uint32_t dw[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
 #pragma unroll
-    for (int s = 0; s < NK; ++s) bf[s] = pm1_bytes((dw[s] >> (16 * h)) & 0xFFFFu, false);
-  }
-  const uint32_t sent = (uint32_t)P.dcap << 16;
-  uint32_t L[ORBM_T];
+    for (int s = 0; s < NK; ++s) bf[t][s] = pm1_bytes((dw[s] >> (16 * h)) & 0xFFFFu, false);
 #pragma unroll
-  for (int t = 0; t < ORBM_T; ++t) L[t] = sent;
+    for (int u = 0; u < ORBM_T; ++u) L[t][u] = sent;
+  }
   const uint32_t hoff = (uint32_t)(4 * h) + ((uint32_t)(32 * NK) << 15);
   const v4i_* gx = gx2 + (size_t)NP.g2 * NK * 2 + h;
   v4i_ af[NK], an[NK];
@@ -659,48 +666,55 @@ __global__ __launch_bounds__(256) void k_match_cand_mfma(
     const int pn = min(t0 + 32 + c, n2 - 1);
 #pragma unroll
     for (int s = 0; s < NK; ++s) an[s] = gx[(size_t)pn * NK * 2 + 2 * s];  // next tile (clamped)
-    mfma_tile<NK>(af, bf, (uint32_t)t0, n2, hoff, L);
+#pragma unroll
+    for (int t = 0; t < RT; ++t) mfma_tile<NK>(af, bf[t], (uint32_t)t0, n2, hoff, L[t]);
 #pragma unroll
     for (int s = 0; s < NK; ++s) af[s] = an[s];
   }
   // merge the two halves' lists of each row (keys unique: position inside)
   if (h) {
 #pragma unroll
-    for (int t = 0; t < ORBM_T; ++t) ml[wave][t][c] = L[t];
+    for (int t = 0; t < RT; ++t)
+#pragma unroll
+      for (int u = 0; u < ORBM_T; ++u) ml[wave][t][u][c] = L[t][u];
   }
   __syncthreads();
   if (h) return;
 #pragma unroll
-  for (int t = 0; t < ORBM_T; ++t) {
-    const uint32_t kk = ml[wave][t][c];
-    if (__ballot(kk < L[ORBM_T - 1])) topk_insert(L, kk);
-  }
-  const bool full = L[ORBM_T - 1] < sent;
+  for (int t = 0; t < RT; ++t) {
+    uint32_t (&Lt)[ORBM_T] = L[t];
 #pragma unroll
-  for (int t = 0; t < ORBM_T; ++t)
-    if (L[t] >= sent) L[t] = 0xFFFFFFFFu;
-  if (!act) return;
-  const int r = NP.row_base + a;
-  ev[r] = make_int2(-1, 0);
-  if (!v1) {
-    rowinfo[r] = make_int4(0, 0, 0, idx1);
-    return;
-  }
-  const int minD = L[0] != 0xFFFFFFFFu ? (int)(L[0] >> 16) : (1 << 20);
-  rowinfo[r] = make_int4(1, full ? ORBM_T + 1 : 0, minD, idx1);
-  if (minD >= ORBM_TH_LOW) return;
-  uint4* out = reinterpret_cast<uint4*>(cand + (size_t)r * ORBM_T);
+    for (int u = 0; u < ORBM_T; ++u) {
+      const uint32_t kk = ml[wave][t][u][c];
+      if (__ballot(kk < Lt[ORBM_T - 1])) topk_insert(Lt, kk);
+    }
+    const bool full = Lt[ORBM_T - 1] < sent;
 #pragma unroll
-  for (int t = 0; t < ORBM_T / 2; ++t) {
-    const uint32_t ka = L[2 * t], kb = L[2 * t + 1];
-    out[t] = make_uint4(ka, ka != 0xFFFFFFFFu ? f2[ka & 0xFFFFu] : 0u, kb,
-                        kb != 0xFFFFFFFFu ? f2[kb & 0xFFFFu] : 0u);
+    for (int u = 0; u < ORBM_T; ++u)
+      if (Lt[u] >= sent) Lt[u] = 0xFFFFFFFFu;
+    if (!act[t]) continue;
+    const int r = NP.row_base + a[t];
+    ev[r] = make_int2(-1, 0);
+    if (!v1[t]) {
+      rowinfo[r] = make_int4(0, 0, 0, idx1[t]);
+      continue;
+    }
+    const int minD = Lt[0] != 0xFFFFFFFFu ? (int)(Lt[0] >> 16) : (1 << 20);
+    rowinfo[r] = make_int4(1, full ? ORBM_T + 1 : 0, minD, idx1[t]);
+    if (minD >= ORBM_TH_LOW) continue;
+    uint4* out = reinterpret_cast<uint4*>(cand + (size_t)r * ORBM_T);
+#pragma unroll
+    for (int u = 0; u < ORBM_T / 2; ++u) {
+      const uint32_t ka = Lt[2 * u], kb = Lt[2 * u + 1];
+      out[u] = make_uint4(ka, ka != 0xFFFFFFFFu ? f2[ka & 0xFFFFu] : 0u, kb,
+                          kb != 0xFFFFFFFFu ? f2[kb & 0xFFFFu] : 0u);
+    }
   }
 }
-template __global__ void k_match_cand_mfma<6>(const MProblem*, const MNodePair*, const v4i_*, uint2*,
-                                              int4*, int2*);
-template __global__ void k_match_cand_mfma<8>(const MProblem*, const MNodePair*, const v4i_*, uint2*,
-                                              int4*, int2*);
+template __global__ void k_match_cand_mfma<6, MC_RT>(const MProblem*, const MNodePair*, const v4i_*,
+                                                     uint2*, int4*, int2*);
+template __global__ void k_match_cand_mfma<8, MC_RT>(const MProblem*, const MNodePair*, const v4i_*,
+                                                     uint2*, int4*, int2*);
 
 // ---------------------------------------------------------------------------
 // k_match_resolve: greedy, in list order.  unit = node pair (parallel mode)
