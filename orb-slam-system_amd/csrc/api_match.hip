@@ -21,7 +21,7 @@ __global__ void k_match_cand_rows(const MProblem*, const MNodePair*, const uint4
 __global__ void k_match_gather2(const MProblem*, const MNodePair*, uint4*, uint32_t*);
 typedef int v4i_ __attribute__((ext_vector_type(4)));
 template <int NK>
-__global__ void k_match_expand2(const MNodePair*, const uint4*, v4i_*);
+__global__ void k_match_expand2(const MProblem*, const MNodePair*, v4i_*);
 #ifndef MC_RT
 #define MC_RT 2 /* row tiles of 32 per wave in k_match_cand_mfma */
 #endif
@@ -91,31 +91,35 @@ void launch_match(const MProblem* d_probs, int nprob, const MNodePair* d_nps, in
   if (timer) timer->begin(ORBX_STAGE_MCAND, s);
   if (nrows > 0 && nnp > 0) {
     if (max_n2 <= ORBM_MAX_N2 && nnp <= 65535 && d_gdesc2) {
-      // list2 descriptors gathered into node order, then two rows per lane,
-      // the 4 waves splitting the positions; descriptors stream through LDS
-      if (max_n2 > 0)
-        hipLaunchKernelGGL(k_match_gather2, dim3((max_n2 + 127) / 128, nnp), dim3(256), 0, s, d_probs,
-                           d_nps, d_gdesc2, d_gval2);
-      if (ORBM_MFMA && d_gx2 && !d_gval2 && max_n2 > 0) {
-        // distances on the matrix cores (no validity masks on this path)
+      const bool mfma = ORBM_MFMA && d_gx2 && !d_gval2 && max_n2 > 0;
+      if (mfma) {
+        // distances on the matrix cores (no validity masks on this path):
+        // list2 gathered straight into +-1 bytes
         v4i_* gx2 = reinterpret_cast<v4i_*>(d_gx2);
         if (six_words) {
           hipLaunchKernelGGL(k_match_expand2<6>, dim3((max_n2 * 6 + 255) / 256, nnp), dim3(256), 0, s,
-                             d_nps, d_gdesc2, gx2);
+                             d_probs, d_nps, gx2);
           hipLaunchKernelGGL((k_match_cand_mfma<6, MC_RT>), dim3((max_n1 + 128 * MC_RT - 1) / (128 * MC_RT), nnp), dim3(256), 0, s,
                              d_probs, d_nps, gx2, d_cand, d_rowinfo, d_ev);
         } else {
           hipLaunchKernelGGL(k_match_expand2<8>, dim3((max_n2 * 8 + 255) / 256, nnp), dim3(256), 0, s,
-                             d_nps, d_gdesc2, gx2);
+                             d_probs, d_nps, gx2);
           hipLaunchKernelGGL((k_match_cand_mfma<8, MC_RT>), dim3((max_n1 + 128 * MC_RT - 1) / (128 * MC_RT), nnp), dim3(256), 0, s,
                              d_probs, d_nps, gx2, d_cand, d_rowinfo, d_ev);
         }
-      } else if (six_words)
-        hipLaunchKernelGGL(k_match_cand_rows<6>, dim3((max_n1 + 127) / 128, nnp), dim3(256), 0, s,
-                           d_probs, d_nps, d_gdesc2, d_gval2, d_cand, d_rowinfo, d_ev);
-      else
-        hipLaunchKernelGGL(k_match_cand_rows<8>, dim3((max_n1 + 127) / 128, nnp), dim3(256), 0, s,
-                           d_probs, d_nps, d_gdesc2, d_gval2, d_cand, d_rowinfo, d_ev);
+      } else {
+        // list2 descriptors gathered into node order, then two rows per lane,
+        // the 4 waves splitting the positions; descriptors stream through LDS
+        if (max_n2 > 0)
+          hipLaunchKernelGGL(k_match_gather2, dim3((max_n2 + 127) / 128, nnp), dim3(256), 0, s, d_probs,
+                             d_nps, d_gdesc2, d_gval2);
+        if (six_words)
+          hipLaunchKernelGGL(k_match_cand_rows<6>, dim3((max_n1 + 127) / 128, nnp), dim3(256), 0, s,
+                             d_probs, d_nps, d_gdesc2, d_gval2, d_cand, d_rowinfo, d_ev);
+        else
+          hipLaunchKernelGGL(k_match_cand_rows<8>, dim3((max_n1 + 127) / 128, nnp), dim3(256), 0, s,
+                             d_probs, d_nps, d_gdesc2, d_gval2, d_cand, d_rowinfo, d_ev);
+      }
     } else if (max_n2 <= 64 * 32 && nnp <= 65535) {
       // list2 staged in LDS, distances in registers (32 per lane)
       const size_t lds = (size_t)std::max(max_n2, 1) * 32;

@@ -438,55 +438,21 @@ __device__ __forceinline__ void wave_sync_lds() {
 #define FS_CCAP 1024 /* per-strip corner list (overflow falls back to a map scan) */
 
 
-__global__ __launch_bounds__(FS_NT) void k_fast_strips(
-    const uint8_t* __restrict__ frames, size_t fstride, size_t rstride,
-    const uint8_t* __restrict__ pyr, size_t pstride, const LevelArgs LA,
-    const CellInfo* __restrict__ cells, const StripInfo* __restrict__ strips,
-    uint32_t* __restrict__ slots, size_t slot_stride, uint32_t* __restrict__ ccount, int ncells,
-    int ini_th, int min_th, int tpitch, int tmax_h, int mcells, int dbg) {
-  // LDS (occupancy is LDS-bound and the kernel is latency-bound: +12 KB per
-  // workgroup measured +38 % time): tile | strength map of the band rows only
-  // | per-cell counts; the NMS row masks reuse the tile, which is dead after
-  // pass 1 (fs_lds in api_extract.hip mirrors this layout)
-  extern __shared__ __align__(16) uint32_t sm[];
-  uint8_t* tile = reinterpret_cast<uint8_t*>(sm);                    // tpitch * tmax_h
-  uint8_t* amap_mem = tile + tpitch * tmax_h;                         // tpitch * (tmax_h - 6)
-  uint8_t* amap = amap_mem - 3 * tpitch;                              // indexed by tile row 3 .. 3+bh
-  int* cnt = reinterpret_cast<int*>(amap_mem + tpitch * (tmax_h - 6));  // mcells
-  const bool masks_in_tile = 16 * mcells * (tmax_h - 6) <= tpitch * tmax_h;
-  unsigned long long* mask = masks_in_tile ? reinterpret_cast<unsigned long long*>(tile)
-                                           : reinterpret_cast<unsigned long long*>(cnt + ((mcells + 3) & ~3));
-  unsigned long long* mask2 = mask + mcells * (tmax_h - 6);
-  __shared__ uint16_t wlist1[FS_NW][FS_L1CAP];
-  __shared__ uint16_t wlist2[FS_NW][FS_L2CAP];
-  __shared__ uint16_t clist[FS_CCAP];  // corners at t_lo (A > t_lo), any order
-  __shared__ int cslot[ORBX_STRIP_MAXCELLS];
-  __shared__ int ncorner;
+// ---------------------------------------------------------------------------
+// Everything after a strip's tile is in LDS: per-cell counters, pass 1,
+// NMS, raster-order output.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void fs_strip_body(
+    uint8_t* __restrict__ tile, uint8_t* __restrict__ amap_mem, int* __restrict__ cnt,
+    unsigned long long* __restrict__ mask, unsigned long long* __restrict__ mask2,
+    uint16_t (*wlist1)[FS_L1CAP], uint16_t (*wlist2)[FS_L2CAP], uint16_t* __restrict__ clist,
+    int* __restrict__ cslot, int& ncorner, const StripInfo& st, int f, int lead, int xal,
+    int slot_pref, uint32_t* __restrict__ slots, size_t slot_stride,
+    uint32_t* __restrict__ ccount, int ncells, int ini_th, int min_th, int tpitch, int dbg) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // uniform: list bases in SGPRs
-  // plain grid: with 8 strip columns at 1080p level 0, XCD (f*S + s) % 8 is
-  // a strip column, whose ring rows then meet in one L2.  Frame-grouped
-  // (frame_unit) and 4..256-strip chunked mappings cut the traffic 1.66x ->
-  // 1.0x of the level bytes but measured 1.5-3 % slower (DESIGN §4).
-  const int sx = blockIdx.x, f = blockIdx.y;
-  const StripInfo st = strips[sx];
-  const int pitch = st.level == 0 ? (int)rstride : LA.pitch[st.level];
-  const uint8_t* base = st.level == 0 ? frames + (size_t)f * fstride
-                                      : pyr + (size_t)f * pstride + LA.pyr_off[st.level];
-  const int slot_pref = tid < st.ncells ? cells[st.cell_begin + tid].slot_off : 0;  // in flight
   const int bh = st.h - 6;
-  const uintptr_t alb = reinterpret_cast<uintptr_t>(base) | (uintptr_t)pitch;
-  const bool aligned = (alb & 3) == 0;
-  const bool aligned16 = (alb & 15) == 0;
-  const int xal = aligned16 ? (st.x & ~15) : aligned ? (st.x & ~3) : st.x;
-  const int lead = st.x - xal;          // tile col of global st.x
-  const int tw = lead + st.w;           // columns in use
-  {
-    const uint8_t* s0 = base + (size_t)st.y * pitch + xal;
-    if (aligned16) stage_region<v4u, 4, FS_NT>(tile, tpitch, s0, pitch, st.h, (tw + 15) >> 4, tid);
-    else if (aligned) stage_region<uint32_t, 12, FS_NT>(tile, tpitch, s0, pitch, st.h, (tw + 3) >> 2, tid);
-    else stage_rows_u32<12, FS_NT>(tile, tpitch, s0, pitch, st.h, tw, tid);
-  }
+  uint8_t* amap = amap_mem - 3 * tpitch;  // indexed by tile row 3 .. 3+bh
   if (tid < st.ncells) {
     cnt[tid] = 0;
     cslot[tid] = slot_pref;
@@ -728,6 +694,57 @@ __global__ __launch_bounds__(FS_NT) void k_fast_strips(
     }
     if (lane == 0) ccount[(size_t)f * ncells + st.cell_begin + k] = (uint32_t)carry;
   }
+}
+
+__global__ __launch_bounds__(FS_NT) void k_fast_strips(
+    const uint8_t* __restrict__ frames, size_t fstride, size_t rstride,
+    const uint8_t* __restrict__ pyr, size_t pstride, const LevelArgs LA,
+    const CellInfo* __restrict__ cells, const StripInfo* __restrict__ strips,
+    uint32_t* __restrict__ slots, size_t slot_stride, uint32_t* __restrict__ ccount, int ncells,
+    int ini_th, int min_th, int tpitch, int tmax_h, int mcells, int dbg) {
+  // LDS (occupancy is LDS-bound and the kernel is latency-bound: +12 KB per
+  // workgroup measured +38 % time): tile | strength map of the band rows only
+  // | per-cell counts; the NMS row masks reuse the tile, which is dead after
+  // pass 1 (fs_lds in api_extract.hip mirrors this layout)
+  extern __shared__ __align__(16) uint32_t sm[];
+  uint8_t* tile = reinterpret_cast<uint8_t*>(sm);                    // tpitch * tmax_h
+  uint8_t* amap_mem = tile + tpitch * tmax_h;                         // tpitch * (tmax_h - 6)
+  int* cnt = reinterpret_cast<int*>(amap_mem + tpitch * (tmax_h - 6));  // mcells
+  const bool masks_in_tile = 16 * mcells * (tmax_h - 6) <= tpitch * tmax_h;
+  unsigned long long* mask = masks_in_tile ? reinterpret_cast<unsigned long long*>(tile)
+                                           : reinterpret_cast<unsigned long long*>(cnt + ((mcells + 3) & ~3));
+  unsigned long long* mask2 = mask + mcells * (tmax_h - 6);
+  __shared__ uint16_t wlist1[FS_NW][FS_L1CAP];
+  __shared__ uint16_t wlist2[FS_NW][FS_L2CAP];
+  __shared__ uint16_t clist[FS_CCAP];  // corners at t_lo (A > t_lo), any order
+  __shared__ int cslot[ORBX_STRIP_MAXCELLS];
+  __shared__ int ncorner;
+  const int tid = threadIdx.x;
+  // plain grid: with 8 strip columns at 1080p level 0, XCD (f*S + s) % 8 is
+  // a strip column, whose ring rows then meet in one L2.  Frame-grouped
+  // (frame_unit) and 4..256-strip chunked mappings cut the traffic 1.66x ->
+  // 1.0x of the level bytes but measured 1.5-3 % slower (DESIGN §4).
+  const int sx = blockIdx.x, f = blockIdx.y;
+  const StripInfo st = strips[sx];
+  const int pitch = st.level == 0 ? (int)rstride : LA.pitch[st.level];
+  const uint8_t* base = st.level == 0 ? frames + (size_t)f * fstride
+                                      : pyr + (size_t)f * pstride + LA.pyr_off[st.level];
+  const int slot_pref = tid < st.ncells ? cells[st.cell_begin + tid].slot_off : 0;  // in flight
+  const uintptr_t alb = reinterpret_cast<uintptr_t>(base) | (uintptr_t)pitch;
+  const bool aligned = (alb & 3) == 0;
+  const bool aligned16 = (alb & 15) == 0;
+  const int xal = aligned16 ? (st.x & ~15) : aligned ? (st.x & ~3) : st.x;
+  const int lead = st.x - xal;          // tile col of global st.x
+  const int tw = lead + st.w;           // columns in use
+  {
+    const uint8_t* s0 = base + (size_t)st.y * pitch + xal;
+    if (aligned16) stage_region<v4u, 4, FS_NT>(tile, tpitch, s0, pitch, st.h, (tw + 15) >> 4, tid);
+    else if (aligned) stage_region<uint32_t, 12, FS_NT>(tile, tpitch, s0, pitch, st.h, (tw + 3) >> 2, tid);
+    else stage_rows_u32<12, FS_NT>(tile, tpitch, s0, pitch, st.h, tw, tid);
+  }
+  fs_strip_body(tile, amap_mem, cnt, mask, mask2, wlist1, wlist2, clist, cslot, ncorner, st, f,
+                       lead, xal, slot_pref, slots, slot_stride, ccount, ncells, ini_th, min_th, tpitch,
+                       dbg);
 }
 
 // ---------------------------------------------------------------------------

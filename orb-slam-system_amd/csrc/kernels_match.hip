@@ -550,22 +550,26 @@ __device__ __forceinline__ v4i_ pm1_bytes(uint32_t bits, bool pos) {
 }
 
 // gx2[(g2 + j) * 2 * NK + 2 * s + h] = bits 16h .. 16h+15 of dword s of
-// position j's gathered descriptor, as +-1 bytes (a' = 2a - 1)
+// the descriptor at list position j of the node pair (desc2[feat2[off2 +
+// j]]), as +-1 bytes (a' = 2a - 1): the list2 gather and the expansion in
+// one pass (the MFMA path needs no packed copy)
 template <int NK>
-__global__ __launch_bounds__(256) void k_match_expand2(const MNodePair* __restrict__ nps,
-                                                       const uint4* __restrict__ gdesc2,
+__global__ __launch_bounds__(256) void k_match_expand2(const MProblem* __restrict__ probs,
+                                                       const MNodePair* __restrict__ nps,
                                                        v4i_* __restrict__ gx2) {
   const MNodePair NP = nps[blockIdx.y];
   const int i = blockIdx.x * 256 + threadIdx.x;  // (position, dword)
   const int j = i / NK, s = i - j * NK;
   if (j >= NP.n2) return;
-  const uint32_t w = reinterpret_cast<const uint32_t*>(gdesc2 + (size_t)(NP.g2 + j) * 2)[s];
+  const MProblem& P = probs[NP.prob];
+  const uint32_t idx2 = P.feat2[NP.off2 + j];
+  const uint32_t w = reinterpret_cast<const uint32_t*>(P.desc2 + (size_t)idx2 * 32)[s];
   v4i_* o = gx2 + ((size_t)(NP.g2 + j) * NK + s) * 2;
   o[0] = pm1_bytes(w & 0xFFFFu, true);
   o[1] = pm1_bytes(w >> 16, true);
 }
-template __global__ void k_match_expand2<6>(const MNodePair*, const uint4*, v4i_*);
-template __global__ void k_match_expand2<8>(const MNodePair*, const uint4*, v4i_*);
+template __global__ void k_match_expand2<6>(const MProblem*, const MNodePair*, v4i_*);
+template __global__ void k_match_expand2<8>(const MProblem*, const MNodePair*, v4i_*);
 
 // one 32-position x 32-row tile: distances on the MFMA, keys and top-T
 // insertions of the lane's 16 (row, position) values on the VALU
