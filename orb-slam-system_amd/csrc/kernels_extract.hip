@@ -400,6 +400,43 @@ __device__ __forceinline__ bool nms_keep_tile(const uint8_t* amap, int tpitch, i
 // 4 cyclically consecutive points of {0,2,..,14} all brighter (darker) than
 // v +- t: necessary for a 9-arc (any 9 contiguous circle points contain 4
 // consecutive even ones), i.e. for A > t.
+// Packed form: E_i = circle point 2i; P_i = (E_i, E_{i+4}) as 16-bit lanes,
+// so one packed min over four P's covers the windows starting at s and s+4:
+// s = 0/4: P0..P3; 1/5: P1,P2,P3,rot(P0); 2/6: P2,P3,rot(P0),rot(P1);
+// 3/7: P3,rot(P0),rot(P1),rot(P2) (rot swaps the halves).  Bright: some
+// window's min > v + t; dark: some window's max < v - t.
+__device__ __forceinline__ us2 rot16(us2 x) { return x.yx; }
+__device__ __forceinline__ bool fast_even_test_pk(const uint8_t* t, int tw, int th) {
+  us2 P0, P1, P2, P3;
+  P0.x = t[3 * tw];           // point 0  (0, 3)
+  P0.y = t[-3 * tw];          // point 8  (0, -3)
+  P1.x = t[2 * tw + 2];       // point 2  (2, 2)
+  P1.y = t[-2 * tw - 2];      // point 10 (-2, -2)
+  P2.x = t[3];                // point 4  (3, 0)
+  P2.y = t[-3];               // point 12 (-3, 0)
+  P3.x = t[-2 * tw + 2];      // point 6  (2, -2)
+  P3.y = t[2 * tw - 2];       // point 14 (-2, 2)
+  const unsigned short v = t[0];
+  const us2 s0 = rot16(P0), s1 = rot16(P1), s2 = rot16(P2);
+  const us2 m23 = __builtin_elementwise_min(P2, P3), m123 = __builtin_elementwise_min(P1, m23);
+  const us2 n01 = __builtin_elementwise_min(s0, s1);
+  const us2 B = __builtin_elementwise_max(
+      __builtin_elementwise_max(__builtin_elementwise_min(P0, m123), __builtin_elementwise_min(m123, s0)),
+      __builtin_elementwise_max(__builtin_elementwise_min(m23, n01),
+                                __builtin_elementwise_min(P3, __builtin_elementwise_min(n01, s2))));
+  const us2 x23 = __builtin_elementwise_max(P2, P3), x123 = __builtin_elementwise_max(P1, x23);
+  const us2 y01 = __builtin_elementwise_max(s0, s1);
+  const us2 D = __builtin_elementwise_min(
+      __builtin_elementwise_min(__builtin_elementwise_max(P0, x123), __builtin_elementwise_max(x123, s0)),
+      __builtin_elementwise_min(__builtin_elementwise_max(x23, y01),
+                                __builtin_elementwise_max(P3, __builtin_elementwise_max(y01, s2))));
+  const us2 hh = (us2)(unsigned short)(v + th);
+  const us2 vv = (us2)v, tt = (us2)(unsigned short)th;
+  const us2 db = __builtin_elementwise_sub_sat(B, hh);
+  const us2 dd = __builtin_elementwise_sub_sat(__builtin_elementwise_sub_sat(vv, D), tt);
+  return (as_u32(db) | as_u32(dd)) != 0u;
+}
+
 __device__ __forceinline__ bool fast_even_test(const uint8_t* t, int tw, int th) {
   const int v = t[0];
   const int hi = v + th, lo = v - th;
@@ -475,27 +512,30 @@ __device__ __forceinline__ void fs_strip_body(
   uint16_t* L1 = wlist1[wave];
   uint16_t* L2 = wlist2[wave];
   int n1 = 0, n2 = 0;  // wave-uniform list lengths
-  const unsigned long long lt = (1ull << lane) - 1ull;
   auto strength_batch = [&](int e, bool act) {
     bool corner = false;
     if (act) {
       const int rr = e >> 9, cc = e & 511;
-      const int a = fast_strength(tile + rr * tpitch + cc, tpitch);
+      const int a = fast_strength(tile + __mul24(rr, tpitch) + cc, tpitch);
       corner = a > t_lo;
-      amap[rr * tpitch + cc] = (uint8_t)(corner ? a : 0);
+      amap[__mul24(rr, tpitch) + cc] = (uint8_t)(corner ? a : 0);
     }
     const unsigned long long bal = __ballot(corner);
     int b = 0;
     if (lane == 0 && bal) b = atomicAdd(&ncorner, __popcll(bal));
     b = __builtin_amdgcn_readfirstlane(b);
-    const int q = b + __popcll(bal & lt);
+    const int q = b + lanes_below(bal);
     if (corner && q < FS_CCAP) clist[q] = (uint16_t)e;
   };
   auto even_batch = [&](int e, bool act) {
     const int ec = e & 511;
-    const bool keep = act && ec >= c0 && ec < c1 && fast_even_test(tile + (e >> 9) * tpitch + ec, tpitch, t_lo);
+#ifdef FS_EVEN_SCALAR  // profiling only: the scalar bit-mask form
+    const bool keep = act && ec >= c0 && ec < c1 && fast_even_test(tile + __mul24(e >> 9, tpitch) + ec, tpitch, t_lo);
+#else
+    const bool keep = act && ec >= c0 && ec < c1 && fast_even_test_pk(tile + __mul24(e >> 9, tpitch) + ec, tpitch, t_lo);
+#endif
     const unsigned long long bal = __ballot(keep);
-    if (keep) L2[n2 + __popcll(bal & lt)] = (uint16_t)e;
+    if (keep) L2[n2 + lanes_below(bal)] = (uint16_t)e;
     n2 += __popcll(bal);
     if (n2 >= 64) {
       wave_sync_lds();
@@ -520,8 +560,6 @@ __device__ __forceinline__ void fs_strip_body(
       const uint32_t w0 = row0[-1], w1 = row0[0], w2 = row0[1];
       const uint32_t up = *reinterpret_cast<const uint32_t*>(tile + off - 3 * tpitch);
       const uint32_t dn = *reinterpret_cast<const uint32_t*>(tile + off + 3 * tpitch);
-      const uint32_t I4 = __builtin_amdgcn_alignbyte(w2, w1, 3);   // (x+3, y)
-      const uint32_t I12 = __builtin_amdgcn_alignbyte(w1, w0, 1);  // (x-3, y)
       uint32_t clo = 0, chi = 0;  // candidate words: pixels 0,2 / 1,3 (16-bit lanes)
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
@@ -529,8 +567,11 @@ __device__ __forceinline__ void fs_strip_body(
         const us2 v = as_us2(__builtin_amdgcn_perm(0u, w1, sel));
         const us2 a0 = as_us2(__builtin_amdgcn_perm(0u, dn, sel));
         const us2 a8 = as_us2(__builtin_amdgcn_perm(0u, up, sel));
-        const us2 a4 = as_us2(__builtin_amdgcn_perm(0u, I4, sel));
-        const us2 a12 = as_us2(__builtin_amdgcn_perm(0u, I12, sel));
+        // (x+3, y) and (x-3, y) straight from the byte pairs {w2:w1} / {w1:w0}
+        // (one v_perm each, no v_alignbyte): pixel i's point 4 is byte i+3 of
+        // {w2:w1}, its point 12 byte i+1 of {w1:w0}
+        const us2 a4 = as_us2(__builtin_amdgcn_perm(w2, w1, h ? 0x0c060c04u : 0x0c050c03u));
+        const us2 a12 = as_us2(__builtin_amdgcn_perm(w1, w0, h ? 0x0c040c02u : 0x0c030c01u));
         const us2 t2 = as_us2(ttl);
         const us2 mb = __builtin_elementwise_min(__builtin_elementwise_max(a0, a8),
                                                  __builtin_elementwise_max(a4, a12));

@@ -33,6 +33,10 @@ __device__ __forceinline__ int wave_sum(int x) {
 }
 
 // value of lane l (l wave-uniform)
+// set bits of a wave-wide mask below this lane (v_mbcnt_lo/hi, no and/bcnt)
+__device__ __forceinline__ int lanes_below(unsigned long long m) {
+  return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
 __device__ __forceinline__ int lane_value(int x, int l) { return __builtin_amdgcn_readlane(x, l); }
 __device__ __forceinline__ uint32_t lane_value(uint32_t x, int l) {
   return (uint32_t)__builtin_amdgcn_readlane((int)x, l);
