@@ -20,6 +20,9 @@ __global__ void k_pyramid(const uint8_t*, size_t, size_t, uint8_t*, size_t, cons
 __global__ void k_fast_strips(const uint8_t*, size_t, size_t, const uint8_t*, size_t,
                               const LevelArgs, const CellInfo*, const StripInfo*, uint32_t*,
                               size_t, uint32_t*, int, int, int, int, int, int, int);
+__global__ void k_fast_strips_p288(const uint8_t*, size_t, size_t, const uint8_t*, size_t,
+                              const LevelArgs, const CellInfo*, const StripInfo*, uint32_t*,
+                              size_t, uint32_t*, int, int, int, int, int, int, int);
 __global__ void k_quadtree(const LevelInfo*, const CellInfo*, const uint32_t*, size_t,
                            const uint32_t*, int, uint32_t*, int32_t*, size_t, uint32_t*, size_t,
                            int*, int, int, int, int*);
@@ -168,6 +171,7 @@ extern "C" int orbx_plan_create(const orbx_params* prm, int width, int height, i
   if (p->qt_lds > 150 * 1024) { plan_free(p); return ORBX_ERR_UNSUPPORTED; }
   if (set_max_dynamic_lds((const void*)k_quadtree, device) ||
       set_max_dynamic_lds((const void*)k_fast_strips, device) ||
+      set_max_dynamic_lds((const void*)k_fast_strips_p288, device) ||
       set_max_dynamic_lds((const void*)k_pyramid, device)) { plan_free(p); return ORBX_ERR_HIP; }
   if (hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking) != hipSuccess ||
       hipHostMalloc((void**)&p->h_err, 64, hipHostMallocDefault) != hipSuccess) { plan_free(p); return ORBX_ERR_HIP; }
@@ -300,7 +304,7 @@ extern "C" int orbx_plan_extract(orbx_plan* p, const uint8_t* frames, int nframe
   // K2 FAST cells
   p->timer.begin(ORBX_STAGE_FAST, s);
   if (!P.strips.empty()) {
-    hipLaunchKernelGGL(k_fast_strips, dim3((unsigned)P.strips.size(), n), dim3(FS_NT), p->fs_lds, s,
+    hipLaunchKernelGGL(p->fs_tpitch == 288 ? k_fast_strips_p288 : k_fast_strips, dim3((unsigned)P.strips.size(), n), dim3(FS_NT), p->fs_lds, s,
                        frames, fstride, rstride, p->d_pyr, p->pyr_stride, p->largs, p->d_cells,
                        p->d_strips, p->d_slots, p->slot_stride, p->d_ccount, P.ncells, P.ini_th,
                        P.min_th, p->fs_tpitch, p->fs_tmaxh, p->fs_mcells, p->dbg);

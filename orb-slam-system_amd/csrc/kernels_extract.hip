@@ -479,13 +479,17 @@ __device__ __forceinline__ void wave_sync_lds() {
 // Everything after a strip's tile is in LDS: per-cell counters, pass 1,
 // NMS, raster-order output.
 // ---------------------------------------------------------------------------
+// TP: the tile pitch as a compile-time constant (every LDS offset of stage A
+// an immediate of one address register), 0 = runtime pitch
+template <int TP>
 __device__ __forceinline__ void fs_strip_body(
     uint8_t* __restrict__ tile, uint8_t* __restrict__ amap_mem, int* __restrict__ cnt,
     unsigned long long* __restrict__ mask, unsigned long long* __restrict__ mask2,
     uint16_t (*wlist1)[FS_L1CAP], uint16_t (*wlist2)[FS_L2CAP], uint16_t* __restrict__ clist,
     int* __restrict__ cslot, int& ncorner, const StripInfo& st, int f, int lead, int xal,
     int slot_pref, uint32_t* __restrict__ slots, size_t slot_stride,
-    uint32_t* __restrict__ ccount, int ncells, int ini_th, int min_th, int tpitch, int dbg) {
+    uint32_t* __restrict__ ccount, int ncells, int ini_th, int min_th, int tpitch_rt, int dbg) {
+  const int tpitch = TP ? TP : tpitch_rt;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // uniform: list bases in SGPRs
   const int bh = st.h - 6;
@@ -553,13 +557,16 @@ __device__ __forceinline__ void fs_strip_body(
     // (padding) finds no survivors; zf: zero the group's strength-map dword
     // (a padding lane may only repeat a group some lane of the same call
     // zeroes: a later zero would erase strengths already written)
-    auto group = [&](uint32_t off, uint32_t ebase, uint32_t ttl, bool zf) {
+    // gb = tile + off - 3 tpitch - 4 (every read of the group at a
+    // non-negative constant offset from it: one address register when the
+    // pitch is a compile-time constant), zp = amap + off
+    auto group = [&](const uint8_t* gb, uint8_t* zp, uint32_t ebase, uint32_t ttl, bool zf) {
       // (g = 0: w0 is the previous row's last dword -- only pixels left of
       // the band, rejected in stage B, read it; r >= 3 keeps it in the tile)
-      const uint32_t* row0 = reinterpret_cast<const uint32_t*>(tile + off);
-      const uint32_t w0 = row0[-1], w1 = row0[0], w2 = row0[1];
-      const uint32_t up = *reinterpret_cast<const uint32_t*>(tile + off - 3 * tpitch);
-      const uint32_t dn = *reinterpret_cast<const uint32_t*>(tile + off + 3 * tpitch);
+      const uint32_t* row0 = reinterpret_cast<const uint32_t*>(gb + 3 * tpitch);
+      const uint32_t w0 = row0[0], w1 = row0[1], w2 = row0[2];
+      const uint32_t up = *reinterpret_cast<const uint32_t*>(gb + 4);
+      const uint32_t dn = *reinterpret_cast<const uint32_t*>(gb + 6 * tpitch + 4);
       uint32_t clo = 0, chi = 0;  // candidate words: pixels 0,2 / 1,3 (16-bit lanes)
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
@@ -582,7 +589,7 @@ __device__ __forceinline__ void fs_strip_body(
         const uint32_t x = as_u32(db) | as_u32(dd);
         if (h) chi = x; else clo = x;
       }
-      if (zf) *reinterpret_cast<uint32_t*>(amap + off) = 0u;
+      if (zf) *reinterpret_cast<uint32_t*>(zp) = 0u;
       // append: the ballot is the compare's SGPR result, the lane's slot is
       // mbcnt of it from 0 at the uniform L1 + n1, only survivors store
       // (stores of every lane to a dummy slot measured 13 % slower).
@@ -616,14 +623,19 @@ __device__ __forceinline__ void fs_strip_body(
       const bool lact = lg < ng;
       const int g = g0 + min(lg, ng - 1);  // padding lanes repeat the last group
       const uint32_t tl = lact ? tt : 0xFF00FF00u;
-      const uint32_t offl = (uint32_t)(__mul24(3 + lr, tpitch) + 4 * g);
+      const int offl = __mul24(3 + lr, tpitch) + 4 * g;
       const uint32_t el = ((uint32_t)(3 + lr) << 9) | (uint32_t)(4 * g);
-      for (int rb = wave * rpw; rb < bh; rb += FS_NW * rpw) {  // wave-uniform
+      // per-lane pointers advanced by a uniform step (one VALU add each)
+      const int step = FS_NW * rpw * tpitch;
+      const uint8_t* gbl = tile + (offl - 3 * tpitch - 4 + __mul24(wave * rpw, tpitch));
+      uint8_t* zpl = amap + (offl + __mul24(wave * rpw, tpitch));
+      for (int rb = wave * rpw; rb < bh; rb += FS_NW * rpw, gbl += step, zpl += step) {  // wave-uniform
         if (rb + rpw <= bh) {
-          group(offl + (uint32_t)(rb * tpitch), el + ((uint32_t)rb << 9), tl, true);
+          group(gbl, zpl, el + ((uint32_t)rb << 9), tl, true);
         } else {  // last rows: lanes past the band repeat its last row, no survivors
           const int r = min(rb + lr, bh - 1);
-          group((uint32_t)(__mul24(3 + r, tpitch) + 4 * g), ((uint32_t)(3 + r) << 9) | (uint32_t)(4 * g),
+          const int off = __mul24(3 + r, tpitch) + 4 * g;
+          group(tile + (off - 3 * tpitch - 4), amap + off, ((uint32_t)(3 + r) << 9) | (uint32_t)(4 * g),
                 rb + lr < bh ? tl : 0xFF00FF00u, true);
         }
       }
@@ -635,7 +647,8 @@ __device__ __forceinline__ void fs_strip_body(
       for (int it0 = wave * 64; it0 < ntask; it0 += FS_NT) {  // wave-uniform trip count
         const bool act = it0 + lane < ntask;
         const int rc = act ? r : 3, gc = act ? g : g0;
-        group((uint32_t)(__mul24(rc, tpitch) + 4 * gc), ((uint32_t)rc << 9) | (uint32_t)(4 * gc),
+        const int off = __mul24(rc, tpitch) + 4 * gc;
+        group(tile + (off - 3 * tpitch - 4), amap + off, ((uint32_t)rc << 9) | (uint32_t)(4 * gc),
               act ? tt : 0xFF00FF00u, act);
         r += dr;
         g += dg;
@@ -737,12 +750,14 @@ __device__ __forceinline__ void fs_strip_body(
   }
 }
 
-__global__ __launch_bounds__(FS_NT) void k_fast_strips(
+template <int TP>
+__device__ __forceinline__ void fs_kernel(
     const uint8_t* __restrict__ frames, size_t fstride, size_t rstride,
-    const uint8_t* __restrict__ pyr, size_t pstride, const LevelArgs LA,
+    const uint8_t* __restrict__ pyr, size_t pstride, const LevelArgs& LA,
     const CellInfo* __restrict__ cells, const StripInfo* __restrict__ strips,
     uint32_t* __restrict__ slots, size_t slot_stride, uint32_t* __restrict__ ccount, int ncells,
-    int ini_th, int min_th, int tpitch, int tmax_h, int mcells, int dbg) {
+    int ini_th, int min_th, int tpitch_rt, int tmax_h, int mcells, int dbg) {
+  const int tpitch = TP ? TP : tpitch_rt;
   // LDS (occupancy is LDS-bound and the kernel is latency-bound: +12 KB per
   // workgroup measured +38 % time): tile | strength map of the band rows only
   // | per-cell counts; the NMS row masks reuse the tile, which is dead after
@@ -783,10 +798,24 @@ __global__ __launch_bounds__(FS_NT) void k_fast_strips(
     else if (aligned) stage_region<uint32_t, 12, FS_NT>(tile, tpitch, s0, pitch, st.h, (tw + 3) >> 2, tid);
     else stage_rows_u32<12, FS_NT>(tile, tpitch, s0, pitch, st.h, tw, tid);
   }
-  fs_strip_body(tile, amap_mem, cnt, mask, mask2, wlist1, wlist2, clist, cslot, ncorner, st, f,
-                       lead, xal, slot_pref, slots, slot_stride, ccount, ncells, ini_th, min_th, tpitch,
-                       dbg);
+  fs_strip_body<TP>(tile, amap_mem, cnt, mask, mask2, wlist1, wlist2, clist, cslot, ncorner, st, f,
+                    lead, xal, slot_pref, slots, slot_stride, ccount, ncells, ini_th, min_th, tpitch,
+                    dbg);
 }
+
+#define FS_KERNEL_ARGS                                                                              \
+  const uint8_t *__restrict__ frames, size_t fstride, size_t rstride, const uint8_t *__restrict__ pyr, \
+      size_t pstride, const LevelArgs LA, const CellInfo *__restrict__ cells,                       \
+      const StripInfo *__restrict__ strips, uint32_t *__restrict__ slots, size_t slot_stride,      \
+      uint32_t *__restrict__ ccount, int ncells, int ini_th, int min_th, int tpitch, int tmax_h,   \
+      int mcells, int dbg
+#define FS_KERNEL_PASS \
+  frames, fstride, rstride, pyr, pstride, LA, cells, strips, slots, slot_stride, ccount, ncells, ini_th, min_th, tpitch, tmax_h, mcells, dbg
+
+__global__ __launch_bounds__(FS_NT) void k_fast_strips(FS_KERNEL_ARGS) { fs_kernel<0>(FS_KERNEL_PASS); }
+// the plan's tile pitch is 288 for every strip width in 224..264 (all the
+// bench workloads): immediates instead of per-iteration address adds
+__global__ __launch_bounds__(FS_NT) void k_fast_strips_p288(FS_KERNEL_ARGS) { fs_kernel<288>(FS_KERNEL_PASS); }
 
 // ---------------------------------------------------------------------------
 // Block-wide exclusive scan of an LDS int array (256 threads), returns total.
