@@ -160,6 +160,7 @@ extern "C" int orbx_plan_create(const orbx_params* prm, int width, int height, i
   orbx_plan* p = new orbx_plan();
   if (const char* e = getenv("ORBX_DEBUG_STOP")) p->dbg = atoi(e);
   if (const char* e = getenv("ORBX_DEBUG_OBDIV")) p->ob_div = atoi(e);
+  if (const char* e = getenv("ORBX_CHUNK")) p->chunk = atoi(e);
   int rc = plan_geometry(*prm, width, height, p->P);
   if (rc) { delete p; return rc; }
   const Plan& P = p->P;
@@ -279,24 +280,24 @@ extern "C" int orbx_plan_stage_times(orbx_plan* p, double* ms, int* launches, in
   return p->timer.collect(ms, launches, n);
 }
 
-extern "C" int orbx_plan_extract(orbx_plan* p, const uint8_t* frames, int nframes,
-                                 size_t fstride, size_t rstride, orbx_keypoint* kps,
-                                 uint8_t* desc, int* counts, void* stream) {
-  if (!p || !frames || !kps || !desc || !counts || nframes < 1 || nframes > p->max_batch)
-    return ORBX_ERR_ARG;
+// one extraction pass over frames [0, n) of the given (already offset) buffers
+static int extract_pass(orbx_plan* p, const uint8_t* frames, int n, size_t fstride, size_t rstride,
+                        orbx_keypoint* kps, uint8_t* desc, int* counts, hipStream_t s, size_t f0) {
   const Plan& P = p->P;
-  if (rstride < (size_t)P.W || fstride < rstride * (size_t)P.H) return ORBX_ERR_ARG;
-  /* the kernels form row offsets with 24-bit multiplies (__umul24) */
-  if (rstride >= ((size_t)1 << 24)) return ORBX_ERR_UNSUPPORTED;
-  ORBX_TRY(hipSetDevice(p->device));
-  hipStream_t s = (hipStream_t)stream; /* NULL = the default stream */
-  const int L = P.params.nlevels, n = nframes;
+  const int L = P.params.nlevels;
+  uint8_t* const d_pyr = p->d_pyr + f0 * p->pyr_stride;
+  uint32_t* const d_slots = p->d_slots + f0 * p->slot_stride;
+  uint32_t* const d_ccount = p->d_ccount + f0 * (size_t)P.ncells;
+  uint32_t* const d_qkeys = p->d_qkeys + f0 * p->qk_stride;
+  int32_t* const d_qnode = p->d_qnode + f0 * p->qk_stride;
+  uint32_t* const d_qout = p->d_qout + f0 * p->qout_stride;
+  int* const d_lcount = p->d_lcount + f0 * (size_t)L;
   // K1 pyramid
   p->timer.begin(ORBX_STAGE_RESIZE, s);
   for (const PyrSeg& g : P.segs) {
     hipLaunchKernelGGL(k_pyramid, dim3(g.ntx * g.nty, n), dim3(256),
                        g.lds_a + g.lds_b + g.lds_yl, s, frames, fstride, rstride,
-                       p->d_pyr, p->pyr_stride, g, reinterpret_cast<const int4*>(p->d_pyr_xs),
+                       d_pyr, p->pyr_stride, g, reinterpret_cast<const int4*>(p->d_pyr_xs),
                        reinterpret_cast<const int4*>(p->d_pyr_ys),
                        reinterpret_cast<const uint4*>(p->d_pyr_blob), p->d_pyr_bo, p->dbg);
   }
@@ -305,8 +306,8 @@ extern "C" int orbx_plan_extract(orbx_plan* p, const uint8_t* frames, int nframe
   p->timer.begin(ORBX_STAGE_FAST, s);
   if (!P.strips.empty()) {
     hipLaunchKernelGGL(p->fs_tpitch == 288 ? k_fast_strips_p288 : k_fast_strips, dim3((unsigned)P.strips.size(), n), dim3(FS_NT), p->fs_lds, s,
-                       frames, fstride, rstride, p->d_pyr, p->pyr_stride, p->largs, p->d_cells,
-                       p->d_strips, p->d_slots, p->slot_stride, p->d_ccount, P.ncells, P.ini_th,
+                       frames, fstride, rstride, d_pyr, p->pyr_stride, p->largs, p->d_cells,
+                       p->d_strips, d_slots, p->slot_stride, d_ccount, P.ncells, P.ini_th,
                        P.min_th, p->fs_tpitch, p->fs_tmaxh, p->fs_mcells, p->dbg);
   }
   p->timer.end(ORBX_STAGE_FAST, s);
@@ -314,8 +315,8 @@ extern "C" int orbx_plan_extract(orbx_plan* p, const uint8_t* frames, int nframe
   // K3 DistributeOctTree
   p->timer.begin(ORBX_STAGE_QUADTREE, s);
   hipLaunchKernelGGL(k_quadtree, dim3(L, n), dim3(256), p->qt_lds, s, p->d_lv, p->d_cells,
-                     p->d_slots, p->slot_stride, p->d_ccount, P.ncells, p->d_qkeys, p->d_qnode,
-                     p->qk_stride, p->d_qout, p->qout_stride, p->d_lcount, L, P.qt_smax,
+                     d_slots, p->slot_stride, d_ccount, P.ncells, d_qkeys, d_qnode,
+                     p->qk_stride, d_qout, p->qout_stride, d_lcount, L, P.qt_smax,
                      P.qt_max_cells, p->d_err);
   p->timer.end(ORBX_STAGE_QUADTREE, s);
   // K4+K5+K6+K7 orientation, blur-at-sample descriptors, assembly
@@ -327,11 +328,34 @@ extern "C" int orbx_plan_extract(orbx_plan* p, const uint8_t* frames, int nframe
   int ob_waves = std::min(ob_full, std::max((ob_full + 3) / 4, (16384 + n - 1) / n));
   if (p->ob_div > 0) ob_waves = std::max(4, ob_full / p->ob_div); /* profiling only */
   hipLaunchKernelGGL(k_orient_brief, dim3((ob_waves + 3) / 4, n),
-                     dim3(256), 0, s, frames, fstride, rstride, p->d_pyr, p->pyr_stride, p->bargs,
-                     p->d_qout, p->qout_stride, p->d_lcount, kps, desc,
+                     dim3(256), 0, s, frames, fstride, rstride, d_pyr, p->pyr_stride, p->bargs,
+                     d_qout, p->qout_stride, d_lcount, kps, desc,
                      counts, p->dbg);
   p->timer.end(ORBX_STAGE_BRIEF, s);
   if (hipGetLastError() != hipSuccess) return ORBX_ERR_HIP;
+  return ORBX_OK;
+}
+
+extern "C" int orbx_plan_extract(orbx_plan* p, const uint8_t* frames, int nframes,
+                                 size_t fstride, size_t rstride, orbx_keypoint* kps,
+                                 uint8_t* desc, int* counts, void* stream) {
+  if (!p || !frames || !kps || !desc || !counts || nframes < 1 || nframes > p->max_batch)
+    return ORBX_ERR_ARG;
+  const Plan& P = p->P;
+  if (rstride < (size_t)P.W || fstride < rstride * (size_t)P.H) return ORBX_ERR_ARG;
+  /* the kernels form row offsets with 24-bit multiplies (__umul24) */
+  if (rstride >= ((size_t)1 << 24)) return ORBX_ERR_UNSUPPORTED;
+  ORBX_TRY(hipSetDevice(p->device));
+  hipStream_t s = (hipStream_t)stream; /* NULL = the default stream */
+  // frames in passes of p->chunk: one pass's pyramid levels stay in the
+  // Infinity Cache for its FAST and BRIEF reads
+  const int ck = p->chunk > 0 ? p->chunk : nframes;
+  const size_t kc = (size_t)P.kcap;
+  for (int c = 0; c < nframes; c += ck) {
+    const int rc = extract_pass(p, frames + (size_t)c * fstride, std::min(ck, nframes - c), fstride, rstride,
+                                kps + (size_t)c * kc, desc + (size_t)c * kc * 32, counts + c, s, (size_t)c);
+    if (rc) return rc;
+  }
   return ORBX_OK;
 }
 

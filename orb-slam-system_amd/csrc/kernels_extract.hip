@@ -467,6 +467,9 @@ __device__ __forceinline__ void wave_sync_lds() {
 }
 
 #define FS_NW (FS_NT / 64)
+struct GroupWords {
+  uint32_t w0, w1, w2, up, dn;
+};
 #ifndef FS_L1FLUSH
 #define FS_L1FLUSH 64 /* stage B runs once a wave's L1 holds this many entries */
 #endif
@@ -560,13 +563,20 @@ __device__ __forceinline__ void fs_strip_body(
     // gb = tile + off - 3 tpitch - 4 (every read of the group at a
     // non-negative constant offset from it: one address register when the
     // pitch is a compile-time constant), zp = amap + off
-    auto group = [&](const uint8_t* gb, uint8_t* zp, uint32_t ebase, uint32_t ttl, bool zf) {
-      // (g = 0: w0 is the previous row's last dword -- only pixels left of
-      // the band, rejected in stage B, read it; r >= 3 keeps it in the tile)
+    // (g = 0: w0 is the previous row's last dword -- only pixels left of
+    // the band, rejected in stage B, read it; r >= 3 keeps it in the tile)
+    auto gload = [&](const uint8_t* gb) {
       const uint32_t* row0 = reinterpret_cast<const uint32_t*>(gb + 3 * tpitch);
-      const uint32_t w0 = row0[0], w1 = row0[1], w2 = row0[2];
-      const uint32_t up = *reinterpret_cast<const uint32_t*>(gb + 4);
-      const uint32_t dn = *reinterpret_cast<const uint32_t*>(gb + 6 * tpitch + 4);
+      GroupWords q;
+      q.w0 = row0[0];
+      q.w1 = row0[1];
+      q.w2 = row0[2];
+      q.up = *reinterpret_cast<const uint32_t*>(gb + 4);
+      q.dn = *reinterpret_cast<const uint32_t*>(gb + 6 * tpitch + 4);
+      return q;
+    };
+    auto gtest = [&](const GroupWords& q, uint8_t* zp, uint32_t ebase, uint32_t ttl, bool zf) {
+      const uint32_t w0 = q.w0, w1 = q.w1, w2 = q.w2, up = q.up, dn = q.dn;
       uint32_t clo = 0, chi = 0;  // candidate words: pixels 0,2 / 1,3 (16-bit lanes)
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
@@ -613,6 +623,9 @@ __device__ __forceinline__ void fs_strip_body(
         }
         wave_sync_lds();
       }
+    };
+    auto group = [&](const uint8_t* gb, uint8_t* zp, uint32_t ebase, uint32_t ttl, bool zf) {
+      gtest(gload(gb), zp, ebase, ttl, zf);
     };
     if (ng <= 64) {
       // row-mapped: lane = (row lr of the step, group lg); a step covers

@@ -35,6 +35,7 @@ struct orbx_plan {
   orbx::StageTimer timer;
   int dbg = 0; /* ORBX_DEBUG_STOP: kernel phase early-exit for profiling only */
   int ob_div = 0; /* ORBX_DEBUG_OBDIV: k_orient_brief grid divisor, profiling only */
+  int chunk = 0;  /* frames per extraction pass (0 = the whole batch in one pass) */
 };
 
 struct orbx_extractor {
