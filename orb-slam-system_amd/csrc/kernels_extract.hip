@@ -1199,7 +1199,7 @@ __device__ __forceinline__ void brief_issue(const BriefKp& k, BriefRegs& R, int 
 #pragma unroll
     for (int u = 0; u < 9; ++u) {
       const uint32_t row = min(r0 + 5u * u, (uint32_t)(KP_ROWS - 1));
-      R.r[u] = ld32u(b + (row * (uint32_t)k.pitch + c4));
+      R.r[u] = ld32u(b + (__umul24(row, (uint32_t)k.pitch) + c4));  // pitch < 2^24 (API check)
     }
   } else {
     // patch crosses the level border: reflect-101 rows, dword loads where the
@@ -1212,7 +1212,7 @@ __device__ __forceinline__ void brief_issue(const BriefKp& k, BriefRegs& R, int 
     for (int u = 0; u < 9; ++u) {
       const int r = min((int)r0 + 5 * u, KP_ROWS - 1);
       const int gy = reflect101(min(max(k.py0 + r, -3), k.UH + 2), k.UH);
-      const uint32_t ro = (uint32_t)(gy * k.pitch);
+      const uint32_t ro = __umul24((uint32_t)gy, (uint32_t)k.pitch);
       if (cin) {
         R.r[u] = ld32u(k.img + (ro + (uint32_t)cx));
       } else {
@@ -1342,9 +1342,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OB_WPE))) v
     const int cc = me.x - me.px0;
     const int qlo = (cc - 18) >> 2;
     const uint16_t* ht = htask[cc - 21];
+    // the three rounds' task entries read up front (one LDS wait, not one
+    // per round behind the previous round's hblur stores)
+    uint32_t te[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) te[k] = ht[lane + 64 * k];
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
-      const uint32_t e = ht[lane + 64 * k];
+      const uint32_t e = te[k];
       if (e == 0xFFFFu) continue;
       const int rp = (int)(e >> 8), q = qlo + (int)(e & 0xFFu);
       const int r0 = 2 * rp, r1 = min(2 * rp + 1, KP_ROWS - 1);
@@ -1357,7 +1362,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OB_WPE))) v
         const uint32_t W0 = kb_w(m, 0), W1 = kb_w(m, 1), W2 = kb_w(m, 2);
         const uint32_t h0 = __builtin_amdgcn_udot4(a2, W2, __builtin_amdgcn_udot4(a1, W1, __builtin_amdgcn_udot4(a0, W0, 0u, false), false), false);
         const uint32_t h1 = __builtin_amdgcn_udot4(b2, W2, __builtin_amdgcn_udot4(b1, W1, __builtin_amdgcn_udot4(b0, W0, 0u, false), false), false);
-        hblur[wave][4 * q + m][rp] = h0 | (h1 << 16);
+        (&hblur[wave][0][0])[__mul24(4 * q + m, KP_HPAIRS) + rp] = h0 | (h1 << 16);
       }
     }
   }
@@ -1384,9 +1389,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OB_WPE))) v
 #pragma unroll
     for (int k = 0; k < 5; ++k) {
       const uint32_t ones = (__umul24((bits >> (4 * k)) & 0xFu, 0x00204081u)) & 0x01010101u;
+      // 0x00 / 0xFF bytes: v_perm selector 0x0C gives 0x00, 0x0D gives 0xFF
+      // (ones * 255 would be a quarter-rate v_mul_lo_u32)
+      const uint32_t bmask = __builtin_amdgcn_perm(0u, 0u, 0x0C0C0C0Cu + ones);
       const uint32_t I = rowp[k];
       s = __builtin_amdgcn_udot4(I, ones, s, false);
-      m = __builtin_amdgcn_udot4(I, (W + 0x04040404u * k) & ((ones << 8) - ones), m, false);
+      m = __builtin_amdgcn_udot4(I, (W + 0x04040404u * k) & bmask, m, false);
     }
     m10 = (int)m - 19 * (int)s;
     m01 = __mul24(v, (int)s);
