@@ -739,6 +739,37 @@ __device__ __forceinline__ void fs_strip_body(
   // pass 4: raster-order output per cell: one wave per cell, lane = band row,
   // row offsets by a wave prefix sum of the row popcounts
   uint32_t* fslots = slots + (size_t)f * slot_stride;
+#ifndef FS_OUT_ONE_CELL
+  if (bh <= 32) {
+    // two cells per wave (lane halves), so a wave walks its cells' corners
+    // once instead of once per cell
+    for (int kk = 2 * wave; kk < st.ncells; kk += 2 * FS_NW) {  // wave-uniform
+      const int k = kk + (lane >> 5), br = lane & 31;
+      const bool act = k < st.ncells && br < bh;
+      const int kc = act ? k : kk;
+      const unsigned long long* mk = (cnt[kc] != 0 ? mask : mask2) + __mul24(kc, bh);
+      unsigned long long m = act ? mk[br] : 0ull;
+      const int n = __popcll(m);
+      const int incl = wave_incl_scan(n);
+      const int tlo = lane_value(incl, 31), tall = lane_value(incl, 63);
+      int off = incl - n - (lane >= 32 ? tlo : 0);
+      const int cb0 = c0 + k * wcell, so = cslot[kc];
+      const int gy = st.y + 3 + br - ORBX_MINB;
+      const uint8_t* arow = amap + __mul24(3 + br, tpitch);
+      while (m) {
+        const int b = __ffsll(m) - 1;
+        m &= m - 1;
+        const int c = cb0 + b;
+        const int gx = xal + c - ORBX_MINB;
+        fslots[so + off++] = orbx_pack_key((uint32_t)gx, (uint32_t)gy, (uint32_t)arow[c] - 1u);
+      }
+      if (lane == 0) ccount[(size_t)f * ncells + st.cell_begin + kk] = (uint32_t)tlo;
+      if (lane == 32 && kk + 1 < st.ncells)
+        ccount[(size_t)f * ncells + st.cell_begin + kk + 1] = (uint32_t)(tall - tlo);
+    }
+    return;
+  }
+#endif
   for (int k = wave; k < st.ncells; k += FS_NW) {
     const unsigned long long* mk = (cnt[k] != 0 ? mask : mask2) + k * bh;
     const int cb0 = c0 + k * wcell, so = cslot[k];
@@ -793,7 +824,12 @@ __device__ __forceinline__ void fs_kernel(
   // a strip column, whose ring rows then meet in one L2.  Frame-grouped
   // (frame_unit) and 4..256-strip chunked mappings cut the traffic 1.66x ->
   // 1.0x of the level bytes but measured 1.5-3 % slower.
+#ifdef FS_FRAME_UNIT  // profiling variant: every strip of frame f on XCD f % 8
+  int sx, f;
+  frame_unit(sx, f);
+#else
   const int sx = blockIdx.x, f = blockIdx.y;
+#endif
   const StripInfo st = strips[sx];
   const int pitch = st.level == 0 ? (int)rstride : LA.pitch[st.level];
   const uint8_t* base = st.level == 0 ? frames + (size_t)f * fstride

@@ -17,6 +17,7 @@ STAGE_OF = {
     "k_resize": "resize",
     "k_pyramid": "resize",
     "k_fast_strips": "fast_cells",
+    "k_fast_strips_p288": "fast_cells",
     "k_quadtree": "quadtree",
     "k_orient_brief": "orient_brief",
     "k_match_select": "match_select",
