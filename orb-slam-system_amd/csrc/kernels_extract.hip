@@ -1304,14 +1304,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OB_WPE))) v
   const int excl = incl - lcv;
   const uint32_t* Q = qout + (size_t)f * qout_stride;
   uint32_t(*P)[KP_PSTRIDE] = patch[wave];
-  // the 256 test pairs {x0, y0, x1, y1} in LDS (ds_read, not a vector load
-  // that would wait behind the patch prefetch)
   // sincos exception keys, entries lane and lane + 64 (brief_sincos)
   const uint32_t exk0 = ORBX_SINCOS_EXC[lane < ORBX_SINCOS_NEXC ? lane : 0][0];
   const uint32_t exk1 = lane + 64 < ORBX_SINCOS_NEXC ? ORBX_SINCOS_EXC[lane + 64][0] : 0xFFFFFFFFu;
-  __shared__ uint32_t spat[256];
-  spat[threadIdx.x] = *reinterpret_cast<const uint32_t*>(ORBX_BRIEF_PATTERN[threadIdx.x]);
   for (int i = threadIdx.x; i < 4 * 192; i += 256) (&htask[0][0])[i] = (&ORBX_HTASK[0][0])[i];
+  // this lane's pattern points (pairs lane + 64 rr) as floats, held for the
+  // whole kernel (no per-keypoint byte extraction / conversion)
+  float pfx[3][2], pfy[3][2];
+#pragma unroll
+  for (int rr = 0; rr < 3; ++rr) {
+    const uint32_t pw = *reinterpret_cast<const uint32_t*>(ORBX_BRIEF_PATTERN[lane + 64 * rr]);
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      pfx[rr][e] = (float)(int)(int8_t)(pw >> (16 * e));
+      pfy[rr][e] = (float)(int)(int8_t)(pw >> (16 * e + 8));
+    }
+  }
   __syncthreads();
   // output position o -> keypoint.  Everything is wave-uniform and forced
   // scalar (readfirstlane): the key and the level tables are s_loads, so the
@@ -1448,12 +1456,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OB_WPE))) v
   uint64_t words[4] = {0, 0, 0, 0};
 #pragma unroll
   for (int rr = 0; rr < 3; ++rr) {
-    const uint32_t pw = spat[lane + 64 * rr];
     int t[2];
 #pragma unroll
     for (int e = 0; e < 2; ++e) {
-      const float fx = (float)(int)(int8_t)(pw >> (16 * e));
-      const float fy = (float)(int)(int8_t)(pw >> (16 * e + 8));
+      const float fx = pfx[rr][e], fy = pfy[rr][e];
       const float ya = fy * cs, yb = fy * sn;
       const int row = (int)__builtin_rintf(__builtin_fmaf(fx, sn, ya));
       const int col = (int)__builtin_rintf(__builtin_fmaf(fx, cs, -yb));
@@ -1467,7 +1473,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OB_WPE))) v
       acc = __builtin_amdgcn_udot2(as_us2(v1), as_us2(odd ? KV_O1 : KV_E1), acc, false);
       acc = __builtin_amdgcn_udot2(as_us2(v2), as_us2(odd ? KV_O2 : KV_E2), acc, false);
       acc = __builtin_amdgcn_udot2(as_us2(v3), as_us2(odd ? KV_O3 : KV_E3), acc, false);
-      t[e] = (int)min((acc + 32768u) >> 16, 255u);
+      t[e] = (int)((acc + 32768u) >> 16);  // <= 255: the taps sum to 65536
     }
     words[rr] = __ballot(t[0] < t[1]);
   }
