@@ -29,3 +29,24 @@ def test_bench_byte_models():
     P = [w * h for w, h in zip(geo.level("width"), geo.level("height"))]
     assert by["fast_cells"] == sum(P) - P[1]
     assert bench.min_pyr_fast_bytes(geo, 1) == sum(P) - P[1]
+
+
+import json  # noqa: E402
+
+import pytest  # noqa: E402
+
+
+@pytest.mark.gpu
+def test_bench_pipelined_step_runs_and_matches_serial():
+    # the default bench line times the pipelined step (extraction of step
+    # k+1 overlapping the matching of step k); bench.py itself aborts if its
+    # matches differ from the serial loop's, and reports the serial numbers
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--workload", "c1", "--batch", "8",
+                        "--steps", "3", "--warmup", "1", "--no-cpu-baseline", "--no-latency"],
+                       env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    assert d["n_gpus"] == 1 and d["value"] > 0
+    assert d["serial"]["value"] > 0 and "pipelined" in d["step_mode"]
+    assert d["config"]["matches_last_batch"] > 0
