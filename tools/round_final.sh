@@ -13,8 +13,10 @@ for wl in ${WLS:-c4 c1 c2 c5}; do
   cp gpurun_out/prof_${R}_$wl/trace/run_kernel_stats.csv $OUT/kernel_stats_$wl.csv
   echo "profiled $wl"
 done
-WL=c4 bash tools/pmc_sq.sh ${R}_c4 || exit $?
-python3 tools/sq_summary.py gpurun_out/pmc_${R}_c4 > $OUT/sq_summary_c4.txt || exit $?
+if [ "${SQ:-1}" = 1 ]; then
+  WL=c4 bash tools/pmc_sq.sh ${R}_c4 || exit $?
+  python3 tools/sq_summary.py gpurun_out/pmc_${R}_c4 > $OUT/sq_summary_c4.txt || exit $?
+fi
 for wl in ${WLS:-c4 c1 c2 c5}; do
   timeout -k 10 600 python bench.py --workload $wl --traffic $OUT/traffic_$wl.json > $OUT/bench_$wl.json 2> $OUT/bench_$wl.err || exit $?
   echo "bench $wl: $(head -c 200 $OUT/bench_$wl.json)"
