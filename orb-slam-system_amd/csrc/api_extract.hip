@@ -167,8 +167,8 @@ extern "C" int orbx_plan_create(const orbx_params* prm, int width, int height, i
   p->device = device;
   p->max_batch = max_batch;
   ORBX_TRY(hipSetDevice(device));
-  // quadtree LDS: cell offsets + 12 int arrays of qt_smax (see k_quadtree)
-  p->qt_lds = sizeof(int) * ((size_t)P.qt_max_cells + 1 + 12 * (size_t)P.qt_smax);
+  // quadtree LDS: cell offsets + 11 int arrays of qt_smax (see k_quadtree)
+  p->qt_lds = sizeof(int) * ((size_t)P.qt_max_cells + 1 + 11 * (size_t)P.qt_smax);
   if (p->qt_lds > 150 * 1024) { plan_free(p); return ORBX_ERR_UNSUPPORTED; }
   if (set_max_dynamic_lds((const void*)k_quadtree, device) ||
       set_max_dynamic_lds((const void*)k_fast_strips, device) ||

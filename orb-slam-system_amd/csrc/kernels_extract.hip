@@ -954,7 +954,6 @@ __global__ __launch_bounds__(256) void k_quadtree(
   int* nry = nrx + smax;                      // smax
   int* ncnt = nry + smax;                     // smax
   int* tmp1 = ncnt + smax;                    // smax
-  int* tmp2 = tmp1 + smax;                    // smax
   __shared__ int wtmp[4];
   __shared__ int s_flag;
 
@@ -1041,17 +1040,20 @@ __global__ __launch_bounds__(256) void k_quadtree(
       const int cn = cnt[i];
       int nch = 0;
       if (cn >= 2) nch = (child[4 * i] > 0) + (child[4 * i + 1] > 0) + (child[4 * i + 2] > 0) + (child[4 * i + 3] > 0);
-      tmp1[S - 1 - i] = nch;
-      tmp2[i] = cn == 1;
+      // one scan for both counts (S < 2^16): children per parent in the high
+      // half (reverse parent order), kept single-key nodes in the low half;
+      // the forward exclusive count of the latter is totK - (reverse
+      // exclusive + own)
+      tmp1[S - 1 - i] = (nch << 16) | (cn == 1);
     }
     __syncthreads();
-    const int totC = block_scan_excl(tmp1, S, wtmp);
-    const int totK = block_scan_excl(tmp2, S, wtmp);
+    const int tot = block_scan_excl(tmp1, S, wtmp);
+    const int totC = tot >> 16, totK = tot & 0xFFFF;
     newS = totC + totK;
     for (int i = tid; i < S; i += 256) {
       const int cn = cnt[i];
       if (cn >= 2) {
-        int pos = tmp1[S - 1 - i];
+        int pos = tmp1[S - 1 - i] >> 16;
         for (int q = 3; q >= 0; --q) {
           const int cc = child[4 * i + q];
           if (cc > 0) {
@@ -1069,7 +1071,7 @@ __global__ __launch_bounds__(256) void k_quadtree(
           }
         }
       } else if (cn == 1) {
-        const int pos = totC + tmp2[i];
+        const int pos = totC + totK - (tmp1[S - 1 - i] & 0xFFFF) - 1;
         if (pos < smax) {
           nrx[pos] = rx[i];
           nry[pos] = ry[i];
