@@ -102,12 +102,21 @@ def _free_port():
     return p
 
 
+def _share_gpu():
+    """Test-only rehearsal of the N-rank path on one GPU: ORBX_BENCH_SHARE_GPU=1
+    puts every rank on device 0 and exchanges over gloo (host-staged); the
+    real multi-GPU run uses one GPU per rank and RCCL."""
+    return os.environ.get("ORBX_BENCH_SHARE_GPU") == "1"
+
+
 def launch_ranks(n):
     """Start n rank processes of this script (RANK/LOCAL_RANK/WORLD_SIZE set),
     wait for all, return the worst exit code.  This process never initialises
     the GPU (torch.cuda.device_count() does not, on this image)."""
     import torch
     ndev = torch.cuda.device_count()
+    if _share_gpu():
+        ndev = n  # test rehearsal: every rank on device 0 (gloo exchange)
     if n > ndev:
         print("bench.py: --gpus %d but only %d GPU(s) visible" % (n, ndev), file=sys.stderr)
         return 2
@@ -380,16 +389,26 @@ def dist_setup(args):
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus and not (world == 1 and args.gpus == 1):
         raise SystemExit("bench.py: WORLD_SIZE=%d but --gpus %d" % (world, args.gpus))
+    if _share_gpu():
+        local = 0
     torch.cuda.set_device(local)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if _share_gpu():
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     return torch, dist, world, rank, local
+
+
+def xch_device(torch, dev):
+    """Where the boundary exchange buffers live: HBM for RCCL, host for gloo."""
+    return torch.device("cpu") if _share_gpu() else dev
 
 
 def finish_time(torch, dist, world, dev, el):
     if world > 1:
-        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        t = torch.tensor([el], dtype=torch.float64, device=xch_device(torch, dev))
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
     return el
@@ -414,7 +433,7 @@ def main_mono(args, wl):
     kps = torch.zeros((B + 1, kcap, 28), dtype=torch.uint8, device=dev)
     desc = torch.zeros((B + 1, kcap, 32), dtype=torch.uint8, device=dev)
     counts = torch.zeros(B + 1, dtype=torch.int32, device=dev)
-    xch = BoundaryExchange(kcap, world, dev) if match else None
+    xch = BoundaryExchange(kcap, world, xch_device(torch, dev)) if match else None
 
     def step():
         # slot 0 <- the predecessor of this step's first frame: on 1 GPU the
@@ -595,7 +614,7 @@ def main_c5(args, wl):
     kps = torch.zeros((B + 1, kcap, 28), dtype=torch.uint8, device=dev)
     desc = torch.zeros((B + 1, kcap, 32), dtype=torch.uint8, device=dev)
     counts = torch.zeros(B + 1, dtype=torch.int32, device=dev)
-    xch = BoundaryExchange(kcap, world, dev)
+    xch = BoundaryExchange(kcap, world, xch_device(torch, dev))
     mb, mbf = KITTI_BF / KITTI_FX, KITTI_BF
 
     def step():

@@ -50,3 +50,20 @@ def test_bench_pipelined_step_runs_and_matches_serial():
     assert d["n_gpus"] == 1 and d["value"] > 0
     assert d["serial"]["value"] > 0 and "pipelined" in d["step_mode"]
     assert d["config"]["matches_last_batch"] > 0
+
+
+@pytest.mark.gpu
+def test_bench_two_ranks_pipelined_on_one_gpu():
+    # rehearsal of the N-GPU bench path on one GPU (both ranks on cuda:0,
+    # boundary exchange over gloo): the serial loop runs the ring exchange,
+    # the pipelined loop runs it on the extraction stream, and bench.py
+    # aborts unless both give the same matches on every rank
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["ORBX_BENCH_SHARE_GPU"] = "1"
+    for wl in ("c1", "c5"):
+        r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--workload", wl,
+                            "--batch", "8", "--steps", "3", "--warmup", "1", "--no-cpu-baseline", "--no-latency"],
+                           env=env, capture_output=True, text=True, timeout=600)
+        assert r.returncode == 0, r.stderr[-3000:]
+        d = json.loads(r.stdout.strip().splitlines()[-1])
+        assert d["n_gpus"] == 2 and d["value"] > 0 and d["serial"]["value"] > 0
