@@ -514,6 +514,10 @@ __device__ __forceinline__ void fs_strip_body(
   // even-point test, 64 L1 entries at a time, appends to L2.  Stage C: the
   // full 16-point strength, 64 L2 entries at a time.  Lists are per wave, so
   // only wave-level LDS ordering is needed.
+  // nothing of the staging is in flight any more: an explicit vmcnt(0) here
+  // lets the waitcnt pass drop the (run-time no-op) vmcnt waits it otherwise
+  // re-inserts every stage-A iteration for registers the staging loads used
+  __builtin_amdgcn_s_waitcnt(0x0F70);
   const int g0 = c0 >> 2, g1 = (c1 + 3) >> 2, ng = g1 - g0;
   const int ntask = ng * bh;
   uint16_t* L1 = wlist1[wave];
@@ -615,6 +619,22 @@ __device__ __forceinline__ void fs_strip_body(
         if (k) L1n[pos] = (uint16_t)(ebase + (uint32_t)j);
         n1 += __popcll(bal);
       }
+#ifdef FS_PROBE_SALU  // profiling only: FS_PROBE_SALU extra scalar instructions per group
+      {
+        int sv = __builtin_amdgcn_readfirstlane(n1);
+#pragma unroll
+        for (int q = 0; q < FS_PROBE_SALU; ++q) asm volatile("s_add_u32 %0, %0, 1" : "+s"(sv));
+        n1 += (sv == -12345);
+      }
+#endif
+#ifdef FS_PROBE_VALU  // profiling only: FS_PROBE_VALU extra independent VALU per group
+      {
+        uint32_t vv = ebase;
+#pragma unroll
+        for (int q = 0; q < FS_PROBE_VALU; ++q) asm volatile("v_xor_b32 %0, 1, %0" : "+v"(vv));
+        n1 += __builtin_amdgcn_readfirstlane((int)(vv == 0xFFFFFFFEu));
+      }
+#endif
       if (n1 >= FS_L1FLUSH) {  // wave-uniform
         wave_sync_lds();
         while (n1 >= 64) {
@@ -642,15 +662,17 @@ __device__ __forceinline__ void fs_strip_body(
       const int step = FS_NW * rpw * tpitch;
       const uint8_t* gbl = tile + (offl - 3 * tpitch - 4 + __mul24(wave * rpw, tpitch));
       uint8_t* zpl = amap + (offl + __mul24(wave * rpw, tpitch));
-      for (int rb = wave * rpw; rb < bh; rb += FS_NW * rpw, gbl += step, zpl += step) {  // wave-uniform
-        if (rb + rpw <= bh) {
-          group(gbl, zpl, el + ((uint32_t)rb << 9), tl, true);
-        } else {  // last rows: lanes past the band repeat its last row, no survivors
-          const int r = min(rb + lr, bh - 1);
-          const int off = __mul24(3 + r, tpitch) + 4 * g;
-          group(tile + (off - 3 * tpitch - 4), amap + off, ((uint32_t)(3 + r) << 9) | (uint32_t)(4 * g),
-                rb + lr < bh ? tl : 0xFF00FF00u, true);
-        }
+      // full row blocks first (no per-iteration bounds test), then the
+      // wave's partial last block if it has one
+      int rb = wave * rpw;
+      uint32_t eb = el + ((uint32_t)rb << 9);
+      for (; rb + rpw <= bh; rb += FS_NW * rpw, gbl += step, zpl += step, eb += (uint32_t)(FS_NW * rpw) << 9)
+        group(gbl, zpl, eb, tl, true);  // wave-uniform trip count
+      if (rb < bh) {  // last rows: lanes past the band repeat its last row, no survivors
+        const int r = min(rb + lr, bh - 1);
+        const int off = __mul24(3 + r, tpitch) + 4 * g;
+        group(tile + (off - 3 * tpitch - 4), amap + off, ((uint32_t)(3 + r) << 9) | (uint32_t)(4 * g),
+              rb + lr < bh ? tl : 0xFF00FF00u, true);
       }
     } else {
       // flattened (row, group) tasks for bands wider than 64 groups
