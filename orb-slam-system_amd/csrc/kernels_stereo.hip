@@ -51,6 +51,16 @@ __device__ int stereo_block_scan(int* a, int n, int* wsum) {
   return total;
 }
 
+typedef unsigned short us2 __attribute__((ext_vector_type(2)));
+typedef short s2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ us2 st_as_us2(uint32_t x) { return __builtin_bit_cast(us2, x); }
+// dword load at any byte address (gfx950 global memory takes unaligned dwords)
+__device__ __forceinline__ uint32_t st_ld32u(const uint8_t* p) {
+  uint32_t v;
+  __builtin_memcpy(&v, p, 4);
+  return v;
+}
+
 __device__ __forceinline__ bool stereo_rows_of(const orbx_keypoint& k, const StereoArgs& A,
                                                int* minr, int* maxr) {
   if (k.octave < 0 || k.octave >= A.nlevels) return false;
@@ -176,9 +186,7 @@ __global__ __launch_bounds__(256) void k_stereo_match(
             if (dist < 100) best = min(best, ((uint32_t)dist << 16) | (uint32_t)iR);
           }
         }
-#pragma unroll
-        for (int d = 32; d >= 1; d >>= 1) best = min(best, (uint32_t)__shfl_xor((int)best, d, 64));
-        best = __builtin_amdgcn_readfirstlane(best);
+        best = wave_min_u32(best);  // DPP, no LDS round trips
         const int bestDist = best == 0xFFFFFFFFu ? 100 : (int)(best >> 16);
         if (bestDist < thOrbDist) {  // :532
           const int bestIdxR = (int)(best & 0xFFFFu);
@@ -205,7 +213,11 @@ __global__ __launch_bounds__(256) void k_stereo_match(
               const uint8_t* IL = Lb + (size_t)y0 * lp + xl0;
               const uint8_t* IRb = Rb + (size_t)y0 * rp + xr0;
               const int cL = IL[w * lp + w];
-              // 121 (incR, row) partial sums, two per lane
+              // 121 (incR, row) partial sums, two per lane: the row's 11
+              // left / right bytes as three dword loads each (the last one
+              // ending at byte 10: nothing past the window is read), then
+              // |(l + cR) - (r + cL)| on byte pairs in packed 16-bit lanes
+              const us2 cLL = (us2)(unsigned short)cL;
 #pragma unroll
               for (int h2 = 0; h2 < 2; ++h2) {
                 const int p = lane + 64 * h2;
@@ -213,51 +225,54 @@ __global__ __launch_bounds__(256) void k_stereo_match(
                   const int k = p / 11, yy = p - 11 * (p / 11);  // k = incR + L
                   const uint8_t* lr = IL + yy * lp;
                   const uint8_t* rr = IRb + yy * rp + k;
-                  const int cR = IRb[w * rp + k + w];
-                  int s = 0;
+                  const us2 cRR = (us2)(unsigned short)IRb[w * rp + k + w];
+                  const uint32_t lw[3] = {st_ld32u(lr), st_ld32u(lr + 4), st_ld32u(lr + 7) >> 8};
+                  const uint32_t rw[3] = {st_ld32u(rr), st_ld32u(rr + 4), st_ld32u(rr + 7) >> 8};
+                  us2 acc = (us2)(unsigned short)0;
 #pragma unroll
-                  for (int xx = 0; xx < 11; ++xx) {
-                    const int d = ((int)lr[xx] - cL) - ((int)rr[xx] - cR);
-                    s += d < 0 ? -d : d;
+                  for (int q = 0; q < 3; ++q) {
+#pragma unroll
+                    for (int hh = 0; hh < 2; ++hh) {
+                      const uint32_t sel = hh ? 0x0c030c01u : 0x0c020c00u;
+                      const us2 A = st_as_us2(__builtin_amdgcn_perm(0u, lw[q], sel)) + cRR;
+                      const us2 B = st_as_us2(__builtin_amdgcn_perm(0u, rw[q], sel)) + cLL;
+                      const s2v D = __builtin_bit_cast(s2v, A) - __builtin_bit_cast(s2v, B);
+                      us2 ad = __builtin_bit_cast(us2, __builtin_elementwise_abs(D));
+                      if (q == 2 && hh == 1) ad.y = 0;  // byte 11 is not in the window
+                      acc += ad;
+                    }
                   }
-                  part[wave][p] = s;
+                  part[wave][p] = (int)acc.x + (int)acc.y;
                 }
               }
               __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
               __builtin_amdgcn_wave_barrier();
               __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-              if (lane == 0) {
-                float vDists[11];
-                int bestSad = 0x7FFFFFFF, bestincR = 0;  // :552-553
+              // lane k < 11: vDists[k] (sum of its 11 rows); the first
+              // minimum in k order is the least (SAD << 4 | k)
+              int dk = 0;
+              if (lane < 11) {
 #pragma unroll
-                for (int k = 0; k < 11; ++k) {
-                  int s = 0;
-#pragma unroll
-                  for (int yy = 0; yy < 11; ++yy) s += part[wave][k * 11 + yy];
-                  const float dist = (float)s;  // cv::norm(IL, IR, NORM_L1): exact
-                  if (dist < (float)bestSad) {
-                    bestSad = (int)dist;
-                    bestincR = k - L;
-                  }
-                  vDists[k] = dist;
-                }
-                if (bestincR != -L && bestincR != L) {  // :580-581
-                  const float dist1 = vDists[L + bestincR - 1];
-                  const float dist2 = vDists[L + bestincR];
-                  const float dist3 = vDists[L + bestincR + 1];
-                  const float deltaR = (dist1 - dist3) / (2.0f * (dist1 + dist3 - 2.0f * dist2));
-                  if (!(deltaR < -1 || deltaR > 1)) {  // :590
-                    float bestuR = A.scale[levelL] * ((float)scaleduR0 + (float)bestincR + deltaR);
-                    float disparity = (uL - bestuR);
-                    if (disparity >= minD && disparity < maxD) {  // :598
-                      if (disparity <= 0) {
-                        disparity = 0.01f;
-                        bestuR = (float)((double)uL - 0.01);  // uL-0.01 in double (:603)
-                      }
-                      dp = A.mbf / disparity;
-                      ur = bestuR;
-                      sv = bestSad;
+                for (int yy = 0; yy < 11; ++yy) dk += part[wave][lane * 11 + yy];
+              }
+              const uint32_t bk = wave_min_u32(lane < 11 ? ((uint32_t)dk << 4) | (uint32_t)lane : 0xFFFFFFFFu);
+              const int bestSad = (int)(bk >> 4), bestincR = (int)(bk & 15u) - L;  // :552-578
+              if (bestincR != -L && bestincR != L) {  // :580-581
+                const float dist1 = (float)lane_value(dk, L + bestincR - 1);
+                const float dist2 = (float)lane_value(dk, L + bestincR);
+                const float dist3 = (float)lane_value(dk, L + bestincR + 1);
+                const float deltaR = (dist1 - dist3) / (2.0f * (dist1 + dist3 - 2.0f * dist2));
+                if (!(deltaR < -1 || deltaR > 1)) {  // :590
+                  float bestuR = A.scale[levelL] * ((float)scaleduR0 + (float)bestincR + deltaR);
+                  float disparity = (uL - bestuR);
+                  if (disparity >= minD && disparity < maxD) {  // :598
+                    if (disparity <= 0) {
+                      disparity = 0.01f;
+                      bestuR = (float)((double)uL - 0.01);  // uL-0.01 in double (:603)
                     }
+                    dp = A.mbf / disparity;
+                    ur = bestuR;
+                    sv = bestSad;
                   }
                 }
               }

@@ -32,11 +32,21 @@ __device__ __forceinline__ int wave_sum(int x) {
          __builtin_amdgcn_readlane(x, 47) + __builtin_amdgcn_readlane(x, 63);
 }
 
-// value of lane l (l wave-uniform)
+// minimum over the 64 lanes (unsigned), wave-uniform
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t x) {
+  x = min(x, (uint32_t)__builtin_amdgcn_update_dpp((int)0xFFFFFFFF, (int)x, 0x111, 0xf, 0xf, false));
+  x = min(x, (uint32_t)__builtin_amdgcn_update_dpp((int)0xFFFFFFFF, (int)x, 0x112, 0xf, 0xf, false));
+  x = min(x, (uint32_t)__builtin_amdgcn_update_dpp((int)0xFFFFFFFF, (int)x, 0x114, 0xf, 0xf, false));
+  x = min(x, (uint32_t)__builtin_amdgcn_update_dpp((int)0xFFFFFFFF, (int)x, 0x118, 0xf, 0xf, false));
+  return min(min((uint32_t)__builtin_amdgcn_readlane((int)x, 15), (uint32_t)__builtin_amdgcn_readlane((int)x, 31)),
+             min((uint32_t)__builtin_amdgcn_readlane((int)x, 47), (uint32_t)__builtin_amdgcn_readlane((int)x, 63)));
+}
+
 // set bits of a wave-wide mask below this lane (v_mbcnt_lo/hi, no and/bcnt)
 __device__ __forceinline__ int lanes_below(unsigned long long m) {
   return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
+// value of lane l (l wave-uniform)
 __device__ __forceinline__ int lane_value(int x, int l) { return __builtin_amdgcn_readlane(x, l); }
 __device__ __forceinline__ uint32_t lane_value(uint32_t x, int l) {
   return (uint32_t)__builtin_amdgcn_readlane((int)x, l);
