@@ -167,8 +167,8 @@ extern "C" int orbx_plan_create(const orbx_params* prm, int width, int height, i
   p->device = device;
   p->max_batch = max_batch;
   ORBX_TRY(hipSetDevice(device));
-  // quadtree LDS: cell offsets + 11 int arrays of qt_smax (see k_quadtree)
-  p->qt_lds = sizeof(int) * ((size_t)P.qt_max_cells + 1 + 11 * (size_t)P.qt_smax);
+  // quadtree LDS: cell offsets, then (reusing them) 11 int arrays of qt_smax
+  p->qt_lds = sizeof(int) * std::max((size_t)P.qt_max_cells + 1, 11 * (size_t)P.qt_smax);
   if (p->qt_lds > 150 * 1024) { plan_free(p); return ORBX_ERR_UNSUPPORTED; }
   if (set_max_dynamic_lds((const void*)k_quadtree, device) ||
       set_max_dynamic_lds((const void*)k_fast_strips, device) ||
@@ -314,7 +314,7 @@ static int extract_pass(orbx_plan* p, const uint8_t* frames, int n, size_t fstri
   if (p->dbg && p->dbg < 20) return ORBX_OK; /* phase probe: later stages would read partial results */
   // K3 DistributeOctTree
   p->timer.begin(ORBX_STAGE_QUADTREE, s);
-  hipLaunchKernelGGL(k_quadtree, dim3(L, n), dim3(256), p->qt_lds, s, p->d_lv, p->d_cells,
+  hipLaunchKernelGGL(k_quadtree, dim3(n, L), dim3(256), p->qt_lds, s, p->d_lv, p->d_cells,
                      d_slots, p->slot_stride, d_ccount, P.ncells, d_qkeys, d_qnode,
                      p->qk_stride, d_qout, p->qout_stride, d_lcount, L, P.qt_smax,
                      P.qt_max_cells, p->d_err);
