@@ -1017,6 +1017,10 @@ __global__ __launch_bounds__(256) void k_quadtree(
     keys[k] = fslots[cells[U.cell_begin + c].slot_off + (k - cell_off[c])];
   }
   __syncthreads();  // cell_off is dead: its LDS becomes the node arrays
+#if defined(QT_PROBE_STOP) && QT_PROBE_STOP == 1  // profiling only: the gather alone
+  if (tid == 0) lcount[(size_t)f * nlevels + l] = 0;
+  return;
+#endif
   auto for_keys = [&](auto&& body) {  // body(k, key, node&)
 #pragma unroll
     for (int j = 0; j < QT_J; ++j) {
@@ -1122,6 +1126,10 @@ __global__ __launch_bounds__(256) void k_quadtree(
     S = newS;
     __syncthreads();
   }
+#if defined(QT_PROBE_STOP) && QT_PROBE_STOP == 2  // profiling only: gather + passes
+  if (tid == 0) lcount[(size_t)f * nlevels + l] = 0;
+  return;
+#endif
   // per final node: first key with maximal response (:277-284)
   uint32_t* best = (uint32_t*)child;  // 4*smax >= newS
   if (newS > L.kcap) {
