@@ -26,6 +26,9 @@ __global__ void k_fast_strips_p288(const uint8_t*, size_t, size_t, const uint8_t
 __global__ void k_quadtree(const LevelInfo*, const CellInfo*, const uint32_t*, size_t,
                            const uint32_t*, int, uint32_t*, int32_t*, size_t, uint32_t*, size_t,
                            int*, int, int, int, int*);
+__global__ void k_quadtree_j6(const LevelInfo*, const CellInfo*, const uint32_t*, size_t,
+                              const uint32_t*, int, uint32_t*, int32_t*, size_t, uint32_t*, size_t,
+                              int*, int, int, int, int*);
 __global__ void k_orient_brief(const uint8_t*, size_t, size_t, const uint8_t*, size_t,
                                const BriefArgs, const uint32_t*, size_t, const int*,
                                orbx_keypoint*, uint8_t*, int*, int);
@@ -171,6 +174,7 @@ extern "C" int orbx_plan_create(const orbx_params* prm, int width, int height, i
   p->qt_lds = sizeof(int) * std::max((size_t)P.qt_max_cells + 1, 11 * (size_t)P.qt_smax);
   if (p->qt_lds > 150 * 1024) { plan_free(p); return ORBX_ERR_UNSUPPORTED; }
   if (set_max_dynamic_lds((const void*)k_quadtree, device) ||
+      set_max_dynamic_lds((const void*)k_quadtree_j6, device) ||
       set_max_dynamic_lds((const void*)k_fast_strips, device) ||
       set_max_dynamic_lds((const void*)k_fast_strips_p288, device) ||
       set_max_dynamic_lds((const void*)k_pyramid, device)) { plan_free(p); return ORBX_ERR_HIP; }
@@ -314,7 +318,9 @@ static int extract_pass(orbx_plan* p, const uint8_t* frames, int n, size_t fstri
   if (p->dbg && p->dbg < 20) return ORBX_OK; /* phase probe: later stages would read partial results */
   // K3 DistributeOctTree
   p->timer.begin(ORBX_STAGE_QUADTREE, s);
-  hipLaunchKernelGGL(k_quadtree, dim3(n, L), dim3(256), p->qt_lds, s, p->d_lv, p->d_cells,
+  // keys per thread in registers: 8 for 1080p-class level 0, else 6 (qt_body)
+  hipLaunchKernelGGL(P.levels[0].w * P.levels[0].h >= (1 << 20) ? k_quadtree : k_quadtree_j6, dim3(n, L),
+                     dim3(256), p->qt_lds, s, p->d_lv, p->d_cells,
                      d_slots, p->slot_stride, d_ccount, P.ncells, d_qkeys, d_qnode,
                      p->qk_stride, d_qout, p->qout_stride, d_lcount, L, P.qt_smax,
                      P.qt_max_cells, p->d_err);

@@ -939,10 +939,6 @@ __device__ __forceinline__ void child_rect(int rx, int ry, int q, int* crx, int*
   *cry = ny0 | (ny1 << 16);
 }
 
-#ifndef QT_J
-#define QT_J 12 /* keys per thread held in registers by k_quadtree (3072 per level; 16: 0.0745 ms, 12: 0.0732, 8: 0.0809) */
-#endif
-
 __device__ __forceinline__ int upper_bound_i(const int* a, int n, int v) {
   int lo = 0, hi = n;
   while (lo < hi) {
@@ -952,12 +948,25 @@ __device__ __forceinline__ int upper_bound_i(const int* a, int n, int v) {
   return lo;
 }
 
-__global__ __launch_bounds__(256) void k_quadtree(
-    const LevelInfo* __restrict__ lv, const CellInfo* __restrict__ cells,
-    const uint32_t* __restrict__ slots, size_t slot_stride, const uint32_t* __restrict__ ccount,
-    int ncells_total, uint32_t* __restrict__ qkeys, int32_t* __restrict__ qnode, size_t qk_stride,
-    uint32_t* __restrict__ qout, size_t qout_stride, int* __restrict__ lcount, int nlevels,
-    int smax, int maxcells, int* __restrict__ err) {
+#define QT_KERNEL_ARGS                                                                      \
+  const LevelInfo *__restrict__ lv, const CellInfo *__restrict__ cells,                    \
+      const uint32_t *__restrict__ slots, size_t slot_stride,                              \
+      const uint32_t *__restrict__ ccount, int ncells_total, uint32_t *__restrict__ qkeys, \
+      int32_t *__restrict__ qnode, size_t qk_stride, uint32_t *__restrict__ qout,          \
+      size_t qout_stride, int *__restrict__ lcount, int nlevels, int smax, int maxcells,   \
+      int *__restrict__ err
+#define QT_KERNEL_PASS \
+  lv, cells, slots, slot_stride, ccount, ncells_total, qkeys, qnode, qk_stride, qout, qout_stride, lcount, nlevels, smax, maxcells, err
+
+// QJ: keys per thread held in registers (256 QJ per level; more spill to the
+// global keys/node arrays).  Both instantiations are built for 8 waves per
+// SIMD (<= 64 VGPRs, 8 workgroups per CU): the kernel is latency-bound, so
+// occupancy beats a larger register file of keys.  Measured (same-run A/B,
+// ms per step): 12 keys at 95 VGPRs (5 waves) 0.089 / 0.173 / 0.117 (c4 /
+// c1 / c5); 8 keys at 8 waves 0.089 / 0.123 / 0.078; 6 keys at 8 waves
+// 0.092 / 0.115 / 0.075 -- 8 for 1080p-class levels, 6 below.
+template <int QJ>
+__device__ __forceinline__ void qt_body(QT_KERNEL_ARGS) {
   extern __shared__ __align__(16) int smem[];
   // grid (frames, levels): dispatch is round-robin over the 8 XCDs in
   // linear-id order, so consecutive frames of a level land on different XCDs,
@@ -994,15 +1003,15 @@ __global__ __launch_bounds__(256) void k_quadtree(
   if (tid == 0) cell_off[nc] = C;
   __syncthreads();
   const uint32_t* fslots = slots + (size_t)f * slot_stride;
-  // keys k = tid + 256 j (j < QT_J) and their node ids live in registers for
+  // keys k = tid + 256 j (j < QJ) and their node ids live in registers for
   // the whole distribution (every pass walks all keys twice: from global
   // memory that was a load-latency chain per pass); more keys than that
   // spill to the global scratch.  keys[] in global memory also serves the
   // final gather of the winners.
-  uint32_t kr[QT_J];
-  int nr[QT_J];
+  uint32_t kr[QJ];
+  int nr[QJ];
 #pragma unroll
-  for (int j = 0; j < QT_J; ++j) {
+  for (int j = 0; j < QJ; ++j) {
     const int k = tid + 256 * j;
     kr[j] = 0u;
     nr[j] = -1;
@@ -1012,7 +1021,7 @@ __global__ __launch_bounds__(256) void k_quadtree(
       keys[k] = kr[j];
     }
   }
-  for (int k = tid + 256 * QT_J; k < C; k += 256) {
+  for (int k = tid + 256 * QJ; k < C; k += 256) {
     const int c = upper_bound_i(cell_off, nc, k) - 1;
     keys[k] = fslots[cells[U.cell_begin + c].slot_off + (k - cell_off[c])];
   }
@@ -1023,11 +1032,11 @@ __global__ __launch_bounds__(256) void k_quadtree(
 #endif
   auto for_keys = [&](auto&& body) {  // body(k, key, node&)
 #pragma unroll
-    for (int j = 0; j < QT_J; ++j) {
+    for (int j = 0; j < QJ; ++j) {
       const int k = tid + 256 * j;
       if (k < C) body(k, kr[j], nr[j]);
     }
-    for (int k = tid + 256 * QT_J; k < C; k += 256) {
+    for (int k = tid + 256 * QJ; k < C; k += 256) {
       int n = node[k];
       body(k, keys[k], n);
       node[k] = n;
@@ -1150,6 +1159,13 @@ __global__ __launch_bounds__(256) void k_quadtree(
   if (tid == 0) lcount[(size_t)f * nlevels + l] = newS;
 }
 
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k_quadtree(QT_KERNEL_ARGS) {
+  qt_body<8>(QT_KERNEL_PASS);
+}
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k_quadtree_j6(QT_KERNEL_ARGS) {
+  qt_body<6>(QT_KERNEL_PASS);
+}
+
 // ---------------------------------------------------------------------------
 // cv::GaussianBlur(7x7, sigma 2, BORDER_REFLECT_101) on 8U (ORBextractor.cc:479)
 // uses OpenCV's bit-exact fixed-point kernel [18,34,48,56,48,34,18]/256:
@@ -1244,6 +1260,9 @@ __device__ constexpr uint32_t kb_w(int m, int d) {
 #define KP_COLS 48
 #define KP_HCOLS 44  /* hblur columns: patch columns 0..43 (samples use cc-18..cc+18 <= 42) */
 #define KP_HPAIRS 22 /* hblur row pairs: rows 0..43 (row 43 never weighted) */
+#ifndef KP_HSTRIDE
+#define KP_HSTRIDE 22 /* hblur column stride, dwords */
+#endif
 #define KP_PSTRIDE (KP_COLS / 4) /* patch row, dwords (+1 padding: no change measured) */
 
 // One keypoint of the frame's level-major output list: where its level
@@ -1325,7 +1344,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OB_WPE))) v
   __shared__ uint32_t patch[4][KP_ROWS][KP_PSTRIDE];
   // horizontally blurred patch, column-major: hblur[w][patch col][row pair]
   // = (H(row 2k), H(row 2k+1)) as u16 pair, H = sum_i k_i p (7 taps)
-  __shared__ uint32_t hblur[4][KP_HCOLS][KP_HPAIRS];
+  __shared__ uint32_t hblur[4][KP_HCOLS][KP_HSTRIDE];
   // horizontal-pass tasks per keypoint column cc = 21..24 (brief_htasks.inc)
   __shared__ uint16_t htask[4][192];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
@@ -1443,7 +1462,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OB_WPE))) v
         const uint32_t W0 = kb_w(m, 0), W1 = kb_w(m, 1), W2 = kb_w(m, 2);
         const uint32_t h0 = __builtin_amdgcn_udot4(a2, W2, __builtin_amdgcn_udot4(a1, W1, __builtin_amdgcn_udot4(a0, W0, 0u, false), false), false);
         const uint32_t h1 = __builtin_amdgcn_udot4(b2, W2, __builtin_amdgcn_udot4(b1, W1, __builtin_amdgcn_udot4(b0, W0, 0u, false), false), false);
-        (&hblur[wave][0][0])[__mul24(4 * q + m, KP_HPAIRS) + rp] = h0 | (h1 << 16);
+        (&hblur[wave][0][0])[__mul24(4 * q + m, KP_HSTRIDE) + rp] = h0 | (h1 << 16);
       }
     }
   }
