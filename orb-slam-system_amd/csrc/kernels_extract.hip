@@ -21,8 +21,32 @@
 #include "brief_pattern.inc"
 #define ORBX_SINCOS_STORAGE static __constant__ const
 #include "sincos_exceptions.inc"
-#define ORBX_HTASK_STORAGE static __constant__ const
+// the horizontal-blur task table, packed per lane for k_orient_brief: entry
+// (cc - 21, lane) holds the lane's three rounds as bytes 10 rp + q (0xFF =
+// none), one dword load per keypoint instead of an LDS copy of the table
+namespace orbx_htask_src {
+#define ORBX_HTASK_STORAGE constexpr
 #include "brief_htasks.inc"
+#undef ORBX_HTASK_STORAGE
+}
+struct BriefHtaskPacked {
+  uint32_t v[4][64];
+};
+constexpr BriefHtaskPacked brief_htask_pack() {
+  BriefHtaskPacked t{};
+  for (int c = 0; c < 4; ++c)
+    for (int l = 0; l < 64; ++l) {
+      uint32_t w = 0;
+      for (int k = 0; k < 3; ++k) {
+        const uint32_t e = orbx_htask_src::ORBX_HTASK[c][l + 64 * k];
+        const uint32_t b = e == 0xFFFFu ? 0xFFu : (e >> 8) * 10u + (e & 0xFFu);
+        w |= b << (8 * k);
+      }
+      t.v[c][l] = w;
+    }
+  return t;
+}
+static __constant__ const BriefHtaskPacked c_htask = brief_htask_pack();
 
 namespace orbx {
 
@@ -1258,7 +1282,7 @@ __device__ constexpr uint32_t kb_w(int m, int d) {
 #define KP_R 21
 #define KP_ROWS 43
 #define KP_COLS 48
-#define KP_HCOLS 44  /* hblur columns: patch columns 0..43 (samples use cc-18..cc+18 <= 42) */
+#define KP_HCOLS 40  /* hblur columns: patch columns 4 qlo .. 4 qlo + 39 (samples use cc-18..cc+18) */
 #define KP_HPAIRS 22 /* hblur row pairs: rows 0..43 (row 43 never weighted) */
 #ifndef KP_HSTRIDE
 #define KP_HSTRIDE 22 /* hblur column stride, dwords */
@@ -1281,11 +1305,13 @@ struct BriefKp {
 // registers (scalars in a struct: never spilled to scratch).
 struct BriefRegs {
   uint32_t r[9];
+  uint32_t ht;  // the keypoint's packed horizontal-pass tasks (c_htask)
 };
 
 __device__ __forceinline__ void brief_issue(const BriefKp& k, BriefRegs& R, int lane) {
   const int ln = min(lane, 59);
   const uint32_t c4 = (uint32_t)(ln % 12) * 4u, r0 = (uint32_t)(ln / 12);
+  R.ht = c_htask.v[k.x - k.px0 - 21][lane];  // cc = 21..24
   if (k.inside) {
     const uint8_t* b = k.img + (size_t)k.py0 * k.pitch + k.px0;  // wave-uniform
 #pragma unroll
@@ -1333,7 +1359,7 @@ __device__ __forceinline__ void brief_commit(const BriefRegs& R, uint32_t* P, in
 }
 
 #ifndef OB_WPE
-#define OB_WPE 6
+#define OB_WPE 7
 #endif
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OB_WPE))) void k_orient_brief(
     const uint8_t* __restrict__ frames, size_t fstride, size_t rstride,
@@ -1345,8 +1371,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OB_WPE))) v
   // horizontally blurred patch, column-major: hblur[w][patch col][row pair]
   // = (H(row 2k), H(row 2k+1)) as u16 pair, H = sum_i k_i p (7 taps)
   __shared__ uint32_t hblur[4][KP_HCOLS][KP_HSTRIDE];
-  // horizontal-pass tasks per keypoint column cc = 21..24 (brief_htasks.inc)
-  __shared__ uint16_t htask[4][192];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   int bx, f;
   frame_unit(bx, f);
@@ -1363,7 +1387,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OB_WPE))) v
   // sincos exception keys, entries lane and lane + 64 (brief_sincos)
   const uint32_t exk0 = ORBX_SINCOS_EXC[lane < ORBX_SINCOS_NEXC ? lane : 0][0];
   const uint32_t exk1 = lane + 64 < ORBX_SINCOS_NEXC ? ORBX_SINCOS_EXC[lane + 64][0] : 0xFFFFFFFFu;
-  for (int i = threadIdx.x; i < 4 * 192; i += 256) (&htask[0][0])[i] = (&ORBX_HTASK[0][0])[i];
   // this lane's pattern points (pairs lane + 64 rr) as floats, held for the
   // whole kernel (no per-keypoint byte extraction / conversion)
   float pfx[3][2], pfy[3][2];
@@ -1415,6 +1438,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OB_WPE))) v
   for (; o < total; o += stride) {  // wave-uniform
   // ---- stage this keypoint's patch (unblurred level), reflect-101 outside ----
   brief_commit(R, &P[0][0], lane);
+  const uint32_t hte = R.ht;  // before the next keypoint's issue overwrites R
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   const BriefKp me = cur;
@@ -1441,17 +1465,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OB_WPE))) v
     // (tools/gen_brief_htasks.py), 189-190 tasks, 3 rounds of 64 lanes
     const int cc = me.x - me.px0;
     const int qlo = (cc - 18) >> 2;
-    const uint16_t* ht = htask[cc - 21];
-    // the three rounds' task entries read up front (one LDS wait, not one
-    // per round behind the previous round's hblur stores)
-    uint32_t te[3];
-#pragma unroll
-    for (int k = 0; k < 3; ++k) te[k] = ht[lane + 64 * k];
+    // this lane's task of round k: byte k of hte (loaded with the patch;
+    // LDS holds patch + 40-column hblur only: 22.3 KB, 7 workgroups per CU)
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
-      const uint32_t e = te[k];
-      if (e == 0xFFFFu) continue;
-      const int rp = (int)(e >> 8), q = qlo + (int)(e & 0xFFu);
+      const uint32_t e = (hte >> (8 * k)) & 0xFFu;
+      if (e == 0xFFu) continue;
+      const int rp = (int)((e * 205u) >> 11), qi = (int)e - 10 * rp;  // e / 10 (exact for e < 256)
+      const int q = qlo + qi;
       const int r0 = 2 * rp, r1 = min(2 * rp + 1, KP_ROWS - 1);
       const int d0 = max(q - 1, 0);  // q == 0: the weights of dword q-1 are 0 for the columns used
       const uint32_t a0 = P[r0][d0], a1 = P[r0][q], a2 = P[r0][q + 1];
@@ -1462,7 +1483,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OB_WPE))) v
         const uint32_t W0 = kb_w(m, 0), W1 = kb_w(m, 1), W2 = kb_w(m, 2);
         const uint32_t h0 = __builtin_amdgcn_udot4(a2, W2, __builtin_amdgcn_udot4(a1, W1, __builtin_amdgcn_udot4(a0, W0, 0u, false), false), false);
         const uint32_t h1 = __builtin_amdgcn_udot4(b2, W2, __builtin_amdgcn_udot4(b1, W1, __builtin_amdgcn_udot4(b0, W0, 0u, false), false), false);
-        (&hblur[wave][0][0])[__mul24(4 * q + m, KP_HSTRIDE) + rp] = h0 | (h1 << 16);
+        (&hblur[wave][0][0])[__mul24(4 * qi + m, KP_HSTRIDE) + rp] = h0 | (h1 << 16);  // column 4 q + m - 4 qlo
       }
     }
   }
@@ -1474,6 +1495,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OB_WPE))) v
   // sum (u + 19) I are two v_dot4_u32_u8 per dword (weights u + 19 keep every
   // byte of a touched dword in 1..37: no borrow between bytes).
   const int cc = x - px0, cr = KP_R;
+  const int hcc = cc - 4 * ((cc - 18) >> 2);  // hblur column of the keypoint (column 4 qlo is 0)
   int m10 = 0, m01 = 0;
   if (lane < 62) {
     const int v = (lane >> 1) - 15, av = v < 0 ? -v : v;
@@ -1520,7 +1542,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OB_WPE))) v
       const int row = (int)__builtin_rintf(__builtin_fmaf(fx, sn, ya));
       const int col = (int)__builtin_rintf(__builtin_fmaf(fx, cs, -yb));
       const int rt = cr + row - 3;  // first vertical tap (patch row)
-      const uint32_t* hc = &hblur[wave][cc + col][rt >> 1];
+      const uint32_t* hc = &hblur[wave][hcc + col][rt >> 1];
       const uint32_t v0 = hc[0], v1 = hc[1], v2 = hc[2], v3 = hc[3];
       // row pairs (2k, 2k+1): taps rt..rt+6 start at the pair's low half
       // (rt even) or high half (rt odd)
