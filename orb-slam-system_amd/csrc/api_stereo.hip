@@ -27,6 +27,7 @@ using namespace orbx;
 
 struct orbs_plan {
   int device = 0, max_batch = 0, waves = 4;
+  int sm_div = 0; /* ORBX_DEBUG_SMDIV: k_stereo_match keypoints per wave, profiling only */
   orbx_params params;
   int W = 0, H = 0;
   StereoArgs args;
@@ -88,6 +89,7 @@ static int splan_create(const orbx_plan* g, int max_batch, orbs_plan** out) {
   const int span = (int)std::ceil(4.0 * smax) + 3;
   A.rcap = P.kcap * span;
   sp->waves = std::max(4, std::min(P.kcap, P.params.nfeatures + 256));
+  if (const char* e = getenv("ORBX_DEBUG_SMDIV")) sp->sm_div = atoi(e); /* profiling only */
   hipSetDevice(sp->device);
   const size_t B = (size_t)max_batch;
   const size_t K = (size_t)std::max(P.kcap, 1);
@@ -149,7 +151,12 @@ static int splan_launch(orbs_plan* sp, int n, const uint8_t* fl, const uint8_t* 
                      sp->d_rowoff, sp->d_rows, sp->d_err);
   sp->timer.end(ORBX_STAGE_SROWS, s);
   sp->timer.begin(ORBX_STAGE_SMATCH, s);
-  hipLaunchKernelGGL(k_stereo_match, dim3((sp->waves + 3) / 4, n), dim3(256), 0, s, kl, dl, cl,
+  // waves stride over the left keypoints: about 4 per wave once the batch
+  // fills the chip (1 / 2 / 4 / 8 / 12 per wave: 0.399 / 0.391 / 0.386 /
+  // 0.392 / 0.403 ms at c5), one per wave for small batches
+  int sw = std::min(sp->waves, std::max((sp->waves + 3) / 4, (16384 + n - 1) / n));
+  if (sp->sm_div > 0) sw = std::max(4, sp->waves / sp->sm_div);
+  hipLaunchKernelGGL(k_stereo_match, dim3((sw + 3) / 4, n), dim3(256), 0, s, kl, dl, cl,
                      kr, dr, fl, fr, fstride, rstride, pyr_l, pyr_r, pstride, A, sp->d_rowoff,
                      sp->d_rows, ur, dep, sp->d_sad, sp->d_err);
   sp->timer.end(ORBX_STAGE_SMATCH, s);
