@@ -907,10 +907,15 @@ __device__ __forceinline__ void fs_kernel(
 #define FS_KERNEL_PASS \
   frames, fstride, rstride, pyr, pstride, LA, cells, strips, slots, slot_stride, ccount, ncells, ini_th, min_th, tpitch, tmax_h, mcells, dbg
 
-__global__ __launch_bounds__(FS_NT) void k_fast_strips(FS_KERNEL_ARGS) { fs_kernel<0>(FS_KERNEL_PASS); }
+#ifdef FS_WPE  // profiling variant: occupancy target
+#define FS_ATTR __attribute__((amdgpu_waves_per_eu(FS_WPE)))
+#else
+#define FS_ATTR
+#endif
+__global__ __launch_bounds__(FS_NT) FS_ATTR void k_fast_strips(FS_KERNEL_ARGS) { fs_kernel<0>(FS_KERNEL_PASS); }
 // the plan's tile pitch is 288 for every strip width in 224..264 (all the
 // bench workloads): immediates instead of per-iteration address adds
-__global__ __launch_bounds__(FS_NT) void k_fast_strips_p288(FS_KERNEL_ARGS) { fs_kernel<288>(FS_KERNEL_PASS); }
+__global__ __launch_bounds__(FS_NT) FS_ATTR void k_fast_strips_p288(FS_KERNEL_ARGS) { fs_kernel<288>(FS_KERNEL_PASS); }
 
 // ---------------------------------------------------------------------------
 // Block-wide exclusive scan of an LDS int array (256 threads), returns total.
