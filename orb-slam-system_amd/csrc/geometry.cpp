@@ -321,10 +321,12 @@ static int plan_pyramid(Plan& P) {
                                  {16, 16}, {16, 8}, {8, 8}};
   int k0 = 0; /* ORBX_DEBUG_PYR_TILE=k: start the tile search at tiles[k] (profiling only) */
   if (const char* e = getenv("ORBX_DEBUG_PYR_TILE")) k0 = std::min(std::max(atoi(e), 0), 8);
+  size_t maxseg = 1 << 20; /* ORBX_DEBUG_PYR_MAXSEG=n: at most n levels per segment, source included (profiling only) */
+  if (const char* e = getenv("ORBX_DEBUG_PYR_MAXSEG")) maxseg = (size_t)std::max(atoi(e), 2);
   size_t i = 1;
   while (i < uniq.size()) {
     bool done = false;
-    for (size_t j = uniq.size(); j > i && !done; --j) {
+    for (size_t j = std::min(uniq.size(), i - 1 + maxseg); j > i && !done; --j) {
       std::vector<int> lev(uniq.begin() + (i - 1), uniq.begin() + j);
       const int ntile = (j == i + 1) ? 9 : 6;
       for (int k = std::min(k0, ntile - 1); k < ntile && !done; ++k) {
