@@ -426,7 +426,7 @@ def main_mono(args, wl):
     plan = orbx.Plan(prm, W, H, B, device=local)
     kcap = plan.kcap
     match = wl["match"]
-    mp = orbx.MatchPlan(B, kcap, wl["topn"], device=local) if match else None
+    mp = orbx.MatchPlan(B, kcap, wl["topn"], device=local, zero_tail=True) if match else None
     frames = torch.empty((B, H, W), dtype=torch.uint8, device=dev)
     orbx.synth_frames(frames, shard_first_frame(rank, B), args.kind)
     # frame slots: 0 = the frame preceding this batch, 1..B = this batch
@@ -603,7 +603,7 @@ def main_c5(args, wl):
     pr = orbx.Plan(prm, W, H, B, device=local)
     sp = orbx.StereoPlan(pl, device=local)
     kcap = pl.kcap
-    mp = orbx.MatchPlan(B, kcap, wl["topn"], device=local)
+    mp = orbx.MatchPlan(B, kcap, wl["topn"], device=local, zero_tail=True)
     # 16 distinct synthetic pairs (numpy spec), tiled over the batch
     npairs = min(16, B)
     first = rank * B

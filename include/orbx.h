@@ -186,7 +186,10 @@ typedef struct {
 
 /* ORBmatcher::SearchByBoW(KeyFrame*, KeyFrame*, vector<MapPoint*>&)
  * (src/ORBmatcher.cc:278-366).  Host inputs; match12[n1] = matched index in
- * kf2 (vpMatches12[i] = vpMapPoints2[match12[i]]) or -1.  Synchronous. */
+ * kf2 (vpMatches12[i] = vpMapPoints2[match12[i]]), -1 where the reference
+ * never writes vpMatches12[i] (it only resize()s the caller's vector, :289),
+ * or -2 where it matched and the rotation check reset it to nullptr (:359).
+ * Synchronous. */
 int orbm_search_by_bow(const orbx_bow_frame* kf1, const orbx_bow_frame* kf2, float nnratio,
                        int check_ori, int device, int32_t* match12, int* nmatches);
 
@@ -204,10 +207,8 @@ int orbm_descriptor_distance_batch(const uint8_t* a, int na, const uint8_t* b, i
  * keypoint index in frame B or -1.  Frame p of side A is d_kps_a + p*kcap,
  * d_desc_a + p*kcap*32, d_count_a[p] (side B likewise), i.e. the layout of
  * orbx_plan_extract outputs; d_match12 is [npairs][kcap], d_nmatches
- * [npairs].  Asynchronous on `stream`.  The descriptors must be
- * orbx_plan_extract outputs: their bytes 24..31 are zero (the reference's
- * 728-entry BRIEF pattern), which the candidate kernel relies on to skip
- * those two dwords; orbm_search_by_bow takes arbitrary descriptors. */
+ * [npairs].  Asynchronous on `stream`.  Descriptors are arbitrary 32-byte
+ * rows unless the caller opts in to ORBM_PLAN_ZERO_TAIL. */
 typedef struct orbm_plan orbm_plan;
 int orbm_plan_create(int max_pairs, int kcap, int topn, int device, orbm_plan** out);
 int orbm_plan_destroy(orbm_plan* mp);
@@ -218,6 +219,16 @@ int orbm_plan_match_frames(orbm_plan* mp, int npairs, const orbx_keypoint* d_kps
                            int32_t* d_match12, int* d_nmatches, void* stream);
 int orbm_plan_set_timing(orbm_plan* mp, int enable);
 int orbm_plan_stage_times(orbm_plan* mp, double* ms, int* launches, int nstages);
+/* Options of orbm_plan_match_frames (default 0):
+ * ORBM_PLAN_ZERO_TAIL  the caller guarantees bytes 24..31 of every descriptor
+ *                      are zero -- true of orbx_plan_extract outputs (the
+ *                      reference's 728-entry BRIEF pattern leaves them 0) --
+ *                      so the distance kernels skip those two dwords;
+ * ORBM_PLAN_VALU       distances by xor/popcount on the VALU instead of the
+ *                      i8 MFMA formulation (same results; for testing). */
+#define ORBM_PLAN_ZERO_TAIL 1
+#define ORBM_PLAN_VALU 2
+int orbm_plan_set_options(orbm_plan* mp, int flags);
 
 /* ---------------------------------------------------------------------------
  * Stereo matcher: Frame::ComputeStereoMatches (src/Frame.cc:446-620), the

@@ -920,7 +920,7 @@ int oo_search_by_bow(int n1, const uint8_t* desc1, const float* angle1, const ui
       if (bin == ind1 || bin == ind2 || bin == ind3) continue;
       for (int i = 0; i < nhist; ++i)
         if (histbin[i] == bin) {
-          match12[hist[i]] = -1;
+          match12[hist[i]] = -2; /* vpMatches12[idx1] = nullptr (:359); -2 tells it from untouched */
           nmatches--;
         }
     }

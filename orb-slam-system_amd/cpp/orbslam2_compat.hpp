@@ -314,9 +314,13 @@ class ORBmatcher {
     orbx_throw(orbm_search_by_bow(&f1.f, &f2.f, mfNNratio, mbCheckOrientation ? 1 : 0, 0,
                                   m12.data(), &n),
                "SearchByBoW");
-    vpMatches12 = std::vector<MP*>(vpMapPoints1.size(), static_cast<MP*>(nullptr));
-    for (size_t i = 0; i < m12.size(); ++i)
+    // as the reference (:289, :330, :359): the caller's entries survive the
+    // resize; matched ones are overwritten, rotation-rejected ones reset
+    vpMatches12.resize(vpMapPoints1.size(), static_cast<MP*>(nullptr));
+    for (size_t i = 0; i < m12.size(); ++i) {
       if (m12[i] >= 0) vpMatches12[i] = vpMapPoints2[m12[i]];
+      else if (m12[i] == -2) vpMatches12[i] = static_cast<MP*>(nullptr);
+    }
     return n;
   }
 
@@ -324,7 +328,7 @@ class ORBmatcher {
   // in the reference: F.N null matches, returns 0.  Kept as is.
   template <class KF, class FR, class MP>
   int SearchByBoW(KF* /*pKF*/, FR& F, std::vector<MP*>& vpMapPointMatches) {
-    vpMapPointMatches = std::vector<MP*>(F.N, static_cast<MP*>(nullptr));
+    vpMapPointMatches.resize(F.N, static_cast<MP*>(nullptr));  // :90
     return 0;
   }
 

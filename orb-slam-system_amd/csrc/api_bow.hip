@@ -247,11 +247,14 @@ extern "C" int orbv_transform_batch(orbv_vocab* v, int nframes, const uint8_t* d
   hipStream_t s = (hipStream_t)stream;
   const size_t need = (size_t)nframes * kcap;
   if (need > v->res_cap) {
+    /* geometric growth: the retired buffers (which launches on other
+     * streams may still read) stay below twice the current one */
+    const size_t cap = std::max(need, v->res_cap + v->res_cap / 2);
     if (v->d_res) v->retired.push_back(v->d_res);
     v->d_res = nullptr;
     v->res_cap = 0;
-    ORBX_TRY(hipMalloc((void**)&v->d_res, need * sizeof(BowRes)));
-    v->res_cap = need;
+    ORBX_TRY(hipMalloc((void**)&v->d_res, cap * sizeof(BowRes)));
+    v->res_cap = cap;
   }
   if (v->nwords == 0) { /* if(empty()) return;  (:1133): empty vectors */
     ORBX_TRY(hipMemsetAsync(d_nbow, 0, nframes * sizeof(int), s));

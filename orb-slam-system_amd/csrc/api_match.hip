@@ -387,9 +387,13 @@ __global__ void k_match_setup(MProblem* probs, MNodePair* nps, int npairs,
 
 struct orbm_plan {
   int device = 0, max_pairs = 0, kcap = 0, topn = 0;
-  /* frames come from orbx_plan_extract, whose descriptors have bytes 24..31
-   * zero (static_assert on the pattern in kernels_extract.hip) */
-  bool six_words = true;
+  /* ORBM_PLAN_ZERO_TAIL (opt-in, orbm_plan_set_options): the caller
+   * guarantees bytes 24..31 of every descriptor are zero, as they are for
+   * orbx_plan_extract outputs (static_assert on the pattern in
+   * kernels_extract.hip), and the candidate kernels skip dwords 6-7.  Off by
+   * default: any other descriptor source gets all 8 dwords. */
+  bool six_words = false;
+  bool force_valu = false; /* ORBM_PLAN_VALU: popcount kernel instead of the MFMA path */
   MProblem* d_probs = nullptr;
   MNodePair* d_nps = nullptr;
   uint32_t* d_sel = nullptr;
@@ -449,6 +453,13 @@ extern "C" int orbm_plan_destroy(orbm_plan* m) {
   return ORBX_OK;
 }
 
+extern "C" int orbm_plan_set_options(orbm_plan* m, int flags) {
+  if (!m || (flags & ~(ORBM_PLAN_ZERO_TAIL | ORBM_PLAN_VALU))) return ORBX_ERR_ARG;
+  m->six_words = (flags & ORBM_PLAN_ZERO_TAIL) != 0;
+  m->force_valu = (flags & ORBM_PLAN_VALU) != 0;
+  return ORBX_OK;
+}
+
 extern "C" int orbm_plan_set_timing(orbm_plan* m, int enable) {
   if (!m) return ORBX_ERR_ARG;
   hipSetDevice(m->device);
@@ -480,7 +491,7 @@ extern "C" int orbm_plan_match_frames(orbm_plan* m, int npairs, const orbx_keypo
                      kps_a, count_a, kps_b, count_b, m->kcap, m->topn, m->d_sel);
   m->timer.end(ORBX_STAGE_MSELECT, s);
   launch_match(m->d_probs, npairs, m->d_nps, npairs, npairs * m->topn, 0, m->topn, m->topn,
-               m->kcap, m->d_gdesc2, nullptr, m->d_gx2, m->d_cand, m->d_rowinfo, m->d_ev, m->d_last,
+               m->kcap, m->d_gdesc2, nullptr, m->force_valu ? nullptr : m->d_gx2, m->d_cand, m->d_rowinfo, m->d_ev, m->d_last,
                m->d_last_off, s, &m->timer, m->six_words);
   return hipGetLastError() == hipSuccess ? ORBX_OK : ORBX_ERR_HIP;
 }

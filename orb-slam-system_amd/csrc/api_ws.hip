@@ -65,6 +65,19 @@ CallWs* ws_acquire(int device) {
 }
 
 void ws_release(CallWs* w) {
+  // an early error return may leave copies into / out of the pinned staging
+  // buffer or kernels queued on the workspace's stream: the next user must
+  // not see them, so a busy stream is drained first, and a workspace whose
+  // stream cannot be drained is destroyed instead of pooled
+  if (hipStreamQuery(w->stream) != hipSuccess && hipStreamSynchronize(w->stream) != hipSuccess) {
+    (void)hipGetLastError();
+    hipSetDevice(w->device);
+    if (w->d) hipFree(w->d);
+    if (w->h) hipHostFree(w->h);
+    hipStreamDestroy(w->stream);
+    delete w;
+    return;
+  }
   std::lock_guard<std::mutex> g(g_pool_mu);
   (*g_pool)[w->device].push_back(w);
 }

@@ -202,11 +202,16 @@ __global__ __launch_bounds__(256) void k_pyramid(const uint8_t* __restrict__ fra
   {
     const uint8_t* src;
     size_t sp;
+#ifdef PYR_PROBE_SAMESRC  // profiling only: every frame stages frame 0's source region
+    const int fsrc = 0;
+#else
+    const int fsrc = f;
+#endif
     if (S.off[0] < 0) {
-      src = frames + (size_t)f * fstride;
+      src = frames + (size_t)fsrc * fstride;
       sp = rstride;
     } else {
-      src = pyr + (size_t)f * pstride + S.off[0];
+      src = pyr + (size_t)fsrc * pstride + S.off[0];
       sp = (size_t)S.pitch[0];
     }
     const int nr = Y.y - Y.x;
@@ -878,8 +883,13 @@ __device__ __forceinline__ void fs_kernel(
 #endif
   const StripInfo st = strips[sx];
   const int pitch = st.level == 0 ? (int)rstride : LA.pitch[st.level];
-  const uint8_t* base = st.level == 0 ? frames + (size_t)f * fstride
-                                      : pyr + (size_t)f * pstride + LA.pyr_off[st.level];
+#ifdef FS_PROBE_SAMESRC  // profiling only: every frame's strips read frame 0 (cache-resident source)
+  const int fsrc = 0;
+#else
+  const int fsrc = f;
+#endif
+  const uint8_t* base = st.level == 0 ? frames + (size_t)fsrc * fstride
+                                      : pyr + (size_t)fsrc * pstride + LA.pyr_off[st.level];
   const int slot_pref = tid < st.ncells ? cells[st.cell_begin + tid].slot_off : 0;  // in flight
   const uintptr_t alb = reinterpret_cast<uintptr_t>(base) | (uintptr_t)pitch;
   const bool aligned = (alb & 3) == 0;

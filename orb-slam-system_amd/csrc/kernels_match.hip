@@ -1073,7 +1073,7 @@ __global__ __launch_bounds__(256) void k_match_finalize(const MProblem* __restri
         const int2 e = ev[r];
         if (e.x < 0) continue;
         if (e.y == ind[0] || e.y == ind[1] || e.y == ind[2]) continue;
-        P.match12[rowinfo[r].w] = -1;
+        P.match12[rowinfo[r].w] = -2;  // set to nullptr by the rotation check (:359)
         ++nf;
       }
     }

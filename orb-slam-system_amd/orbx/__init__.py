@@ -41,6 +41,7 @@ assert KEYPOINT_DTYPE.itemsize == 28
 
 OK, ERR_ARG, ERR_CELL_ROI, ERR_LEVEL_SIZE, ERR_QUADTREE, ERR_CAPACITY, ERR_UNSUPPORTED, \
     ERR_HIP, ERR_NO_DEVICE = 0, -1, -2, -3, -4, -5, -6, -7, -8
+ORBM_PLAN_ZERO_TAIL, ORBM_PLAN_VALU = 1, 2  # orbm_plan_set_options flags (include/orbx.h)
 
 EXPORTED = [
     "orbx_abi_version", "orbx_status_string", "orbx_device_count", "orbx_tables",
@@ -50,7 +51,7 @@ EXPORTED = [
     "orbx_plan_check", "orbx_stage_count", "orbx_stage_name", "orbx_plan_set_timing",
     "orbx_plan_stage_times", "orbx_synth_frames", "orbm_search_by_bow",
     "orbm_descriptor_distance_batch", "orbm_plan_create", "orbm_plan_destroy",
-    "orbm_plan_match_frames", "orbm_plan_set_timing", "orbm_plan_stage_times",
+    "orbm_plan_match_frames", "orbm_plan_set_timing", "orbm_plan_stage_times", "orbm_plan_set_options",
     "orbx_stereo_match", "orbs_plan_create", "orbs_plan_destroy", "orbs_plan_match",
     "orbs_plan_check", "orbs_plan_set_timing", "orbs_plan_stage_times",
     "orbv_vocab_load_text", "orbv_vocab_create", "orbv_vocab_destroy", "orbv_vocab_info",
@@ -133,6 +134,7 @@ _sig = {
     "orbm_plan_destroy": (I, [P]),
     "orbm_plan_match_frames": (I, [P, I, P, P, P, P, P, P, F, I, P, P, P]),
     "orbm_plan_set_timing": (I, [P, I]),
+    "orbm_plan_set_options": (I, [P, I]),
     "orbm_plan_stage_times": (I, [P, P, P, I]),
     "orbx_stereo_match": (I, [P, P, P, P, I, P, P, I, F, F, P, P, P]),
     "orbs_plan_create": (I, [P, I, P]),
@@ -550,14 +552,20 @@ class Plan:
 
 
 class MatchPlan:
-    """Batched brute-force SearchByBoW between extractor frames (single node, top-N)."""
+    """Batched brute-force SearchByBoW between extractor frames (single node, top-N).
 
-    def __init__(self, max_pairs, kcap, topn=2000, device=0):
+    zero_tail=True asserts that bytes 24..31 of every descriptor are zero (true
+    of Plan.extract outputs) and lets the distance kernels skip them; valu=True
+    takes the xor/popcount distance kernel instead of the MFMA one."""
+
+    def __init__(self, max_pairs, kcap, topn=2000, device=0, zero_tail=False, valu=False):
         import torch
         h = ctypes.c_void_p()
         _check(_lib.orbm_plan_create(max_pairs, kcap, topn, device, ctypes.byref(h)),
                "orbm_plan_create")
         self._h, self.kcap, self.topn, self.max_pairs = h, kcap, topn, max_pairs
+        _check(_lib.orbm_plan_set_options(h, (ORBM_PLAN_ZERO_TAIL if zero_tail else 0)
+                                          | (ORBM_PLAN_VALU if valu else 0)), "orbm_plan_set_options")
         dev = torch.device("cuda", device)
         self.match12 = torch.empty((max_pairs, kcap), dtype=torch.int32, device=dev)
         self.nmatches = torch.zeros(max_pairs, dtype=torch.int32, device=dev)

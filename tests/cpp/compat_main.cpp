@@ -94,8 +94,9 @@ int main(int argc, char** argv) {
   std::vector<uint8_t> d0L, d0R;
   std::vector<int> m0;
   int nm0 = -1;
+  TMapPoint sentinel;  // a caller's stale entry: survives where the reference never writes
   for (int rep = 0; rep < reps; ++rep) {
-    std::vector<TMapPoint*> matches;
+    std::vector<TMapPoint*> matches(kf1.mvpMapPoints.size(), &sentinel);
     int nm = -1;
     // LoopClosing thread: SearchByBoW while the stereo frame is extracted
     std::thread loop([&] {
@@ -104,9 +105,11 @@ int main(int argc, char** argv) {
     });
     TFrame frame(L, R, left, right);
     loop.join();
+    // C-ABI encoding: index, -1 never written (:289 resize keeps the entry),
+    // -2 reset to nullptr by the rotation check (:359)
     std::vector<int> m(matches.size(), -1);
     for (size_t i = 0; i < matches.size(); ++i)
-      if (matches[i]) m[i] = (int)(matches[i] - mp2.data());
+      m[i] = matches[i] == &sentinel ? -1 : matches[i] ? (int)(matches[i] - mp2.data()) : -2;
     auto flat = [](const cv::Mat& d) {
       return d.empty() ? std::vector<uint8_t>() : std::vector<uint8_t>(d.data, d.data + (size_t)d.rows * 32);
     };

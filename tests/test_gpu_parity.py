@@ -193,14 +193,22 @@ def _topn_bow(k, d, topn):
                 node_id=np.array([0], np.uint32), off=np.array([0, len(sel)], np.uint32), feat=sel)
 
 
-@pytest.mark.parametrize("W,H,nf,kind,first", [(640, 480, 1000, "noise", 40),
-                                                (1920, 1080, 2000, "rects", 40),
-                                                (640, 480, 1000, "pan", 40),
-                                                (1920, 1080, 2000, "pan", 45)])
-def test_match_plan_matches_oracle(gpu, oracle, W, H, nf, kind, first):
+@pytest.mark.parametrize("W,H,nf,kind,first,opts", [(640, 480, 1000, "noise", 40, {}),
+                                                     (1920, 1080, 2000, "rects", 40, {}),
+                                                     (640, 480, 1000, "pan", 40, {}),
+                                                     (1920, 1080, 2000, "pan", 45, {}),
+                                                     (1920, 1080, 2000, "pan", 45, {"zero_tail": True}),
+                                                     (1920, 1080, 2000, "pan", 45, {"valu": True}),
+                                                     (640, 480, 1000, "pan", 40, {"zero_tail": True, "valu": True}),
+                                                     (640, 480, 1000, "pan", 40, {"tail": True}),
+                                                     (640, 480, 1000, "pan", 40, {"tail": True, "valu": True})])
+def test_match_plan_matches_oracle(gpu, oracle, W, H, nf, kind, first, opts):
     """Batched SearchByBoW of consecutive frames; 'pan' frames are temporally
     correlated, so hundreds of matches per pair go through the serial
-    vbMatched2 resolver (and frame 48 starts a new clip)."""
+    vbMatched2 resolver (and frame 48 starts a new clip).  opts: the plan's
+    distance path (zero_tail: 6-dword distances, valu: popcount kernel
+    instead of the MFMA one); tail: descriptor bytes 24..31 overwritten with
+    random bytes, which the default 8-dword path must take into account."""
     import torch
     B = 4
     guard = "empty" if W == 1920 else "strict"
@@ -208,7 +216,12 @@ def test_match_plan_matches_oracle(gpu, oracle, W, H, nf, kind, first):
     plan = gpu.Plan(prm, W, H, B)
     frames = torch.from_numpy(synth.frames(W, H, first, B, kind)).cuda()
     plan.extract(frames)
-    mp = gpu.MatchPlan(B - 1, plan.kcap, topn=nf)
+    if opts.get("tail"):
+        g = torch.Generator(device="cpu").manual_seed(W + first)
+        tail = torch.randint(0, 256, (B, plan.kcap, 8), dtype=torch.uint8, generator=g)
+        plan.desc[:B, :, 24:] = tail.cuda()
+    mp = gpu.MatchPlan(B - 1, plan.kcap, topn=nf, zero_tail=opts.get("zero_tail", False),
+                       valu=opts.get("valu", False))
     mp.match(B - 1, plan.kps[1:], plan.desc[1:], plan.counts[1:], plan.kps, plan.desc,
              plan.counts, 0.75, True)
     plan.check()
