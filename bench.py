@@ -328,9 +328,12 @@ def latency_leg(calls=200, warm=20):
     from orbx import synth
     L = orbx.lib()
     out = {}
-    for tag, (W, H, nf, guard) in (("extract_640x480", (640, 480, 1000, "strict")),
-                                   ("extract_1920x1080", (1920, 1080, 2000, "empty"))):
+    for tag, (W, H, nf, guard), opts in (
+            ("extract_640x480", (640, 480, 1000, "strict"), {}),
+            ("extract_1920x1080", (1920, 1080, 2000, "empty"), {}),
+            ("extract_1920x1080_pageable_h2d", (1920, 1080, 2000, "empty"), {"pageable_h2d": True})):
         ex = orbx.Extractor(nf, 1.2, 8, 20, 7, guard)
+        ex.set_options(**opts)
         imgs = [np.ascontiguousarray(synth.frame(W, H, i, "pan")) for i in range(8)]
         cap = ctypes.c_int(0)
         orbx._check(L.orbx_extractor_capacity(ex._h, W, H, ctypes.byref(cap)))
@@ -348,8 +351,10 @@ def latency_leg(calls=200, warm=20):
             if i >= warm:
                 ts.append((t1 - t0) * 1e6)
         out[tag] = {"p50_us": round(_pct(ts, 50), 1), "p99_us": round(_pct(ts, 99), 1),
-                    "calls": calls, "keypoints": n.value}
+                    "max_us": round(max(ts), 1), "calls": calls, "keypoints": n.value,
+                    "refetches": ex.stats()["refetches"]}
         del ex
+    out["compat_operator_1920x1080"] = compat_latency(calls, warm)
     # SearchByBoW(KF, KF): 2000 x 2000 in one vocabulary node
     ex = orbx.Extractor(2000, 1.2, 8, 20, 7, "empty")
     frames = []
@@ -374,10 +379,33 @@ def latency_leg(calls=200, warm=20):
     out["search_by_bow_2000x2000"] = {"p50_us": round(_pct(ts, 50), 1),
                                       "p99_us": round(_pct(ts, 99), 1), "calls": calls,
                                       "features": [int(b1.n), int(b2.n)], "matches": nm.value}
-    out["note"] = ("one synchronous C-ABI call at a time from the host (image H2D, kernels, "
-                   "results D2H), timed around the call; the throughput line above is the "
-                   "batched device-resident path")
+    out["note"] = ("one synchronous C-ABI call at a time from the host (image H2D through pinned "
+                   "staging unless *_pageable_h2d, kernels, results D2H), timed around the call; "
+                   "compat_operator_*: ORB_SLAM2::ORBextractor::operator() of cpp/orbslam2_compat.hpp "
+                   "(tools/compat_latency.cpp), with and without mvImagePyramid on the host; the "
+                   "throughput line above is the batched device-resident path")
     return out
+
+
+def compat_latency(calls, warm):
+    """ORB_SLAM2::ORBextractor::operator() (cpp/orbslam2_compat.hpp) at 1080p,
+    timed in C++ by tools/compat_latency.cpp (built in-tree next to liborbx.so)."""
+    import tempfile
+    from orbx import synth
+    exe = os.path.join(ROOT, "orb-slam-system_amd", "compat_latency")
+    if not os.path.exists(exe):
+        return {"error": "orb-slam-system_amd/compat_latency not built"}
+    W, H = 1920, 1080
+    with tempfile.NamedTemporaryFile(suffix=".raw") as f:
+        for i in range(8):
+            f.write(np.ascontiguousarray(synth.frame(W, H, i, "pan")).tobytes())
+        f.flush()
+        env = dict(os.environ, ORBX_CELL_GUARD="1")
+        r = subprocess.run([exe, str(W), str(H), "2000", str(warm), str(calls), f.name, "8"],
+                           capture_output=True, text=True, timeout=300, env=env)
+    if r.returncode != 0:
+        return {"error": "compat_latency exit %d: %s" % (r.returncode, r.stderr[-300:])}
+    return json.loads(r.stdout)
 
 
 # --------------------------------------------------------------------------- distributed

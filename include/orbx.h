@@ -119,6 +119,33 @@ int orbx_extract(orbx_extractor* e, const uint8_t* img, int width, int height, s
 int orbx_extractor_level(orbx_extractor* e, int level, uint8_t* dst, size_t dst_stride,
                          int* width, int* height);
 
+/* Options of an extractor (default 0; persistent across calls):
+ * ORBX_EXTRACTOR_PYRAMID_TO_HOST  every orbx_extract also brings the whole
+ *     pyramid back (the reference refills mvImagePyramid on each call,
+ *     src/ORBextractor.cc:497-515, read by Frame::ComputeStereoMatches): one
+ *     D2H of the level buffer on a second stream, overlapped with the rest
+ *     of the extraction; read it with orbx_extractor_level_host;
+ * ORBX_EXTRACTOR_PAGEABLE_H2D  upload the caller's image straight from its
+ *     (pageable) rows instead of through the extractor's pinned staging
+ *     (measurement aid; ignored with PYRAMID_TO_HOST, whose level 0 is the
+ *     staged copy). */
+#define ORBX_EXTRACTOR_PYRAMID_TO_HOST 1
+#define ORBX_EXTRACTOR_PAGEABLE_H2D 2
+int orbx_extractor_set_options(orbx_extractor* e, int flags);
+
+/* Host view of mvImagePyramid[level] after an orbx_extract with
+ * ORBX_EXTRACTOR_PYRAMID_TO_HOST: *data / *stride point into extractor-owned
+ * pinned memory, valid until the next orbx_extract or destroy of `e` (levels
+ * whose size equals the previous level's -- level 1 with the reference's
+ * scale table -- share its pixels, as cv::resize copies them). */
+int orbx_extractor_level_host(orbx_extractor* e, int level, const uint8_t** data, size_t* stride,
+                              int* width, int* height);
+
+/* Call statistics of an extractor since creation: calls of orbx_extract and
+ * the calls whose keypoint count exceeded the speculative result copy (a
+ * second D2H round trip). */
+int orbx_extractor_stats(orbx_extractor* e, long long* calls, long long* refetches);
+
 /* ---------------------------------------------------------------------------
  * Batched device-resident extraction (the throughput path; bench.py).
  * ------------------------------------------------------------------------- */
@@ -143,6 +170,11 @@ int orbx_plan_extract(orbx_plan* plan, const uint8_t* d_frames, int nframes, siz
                       void* stream);
 /* synchronises `stream`, returns and clears the latched device error */
 int orbx_plan_check(orbx_plan* plan, void* stream);
+/* Debug counters since the last call (then reset; synchronises the plan's
+ * stream): FAST strips whose corner list overflowed into the strength-map
+ * scan.  Testing aid: ORBX_DEBUG_CCAP=<n> at plan creation lowers the list
+ * capacity so the scan runs on ordinary frames. */
+int orbx_plan_debug_counters(orbx_plan* plan, int* fast_overflow_strips);
 
 /* Per-stage device timing (HIP events around every launch of a stage). */
 int orbx_stage_count(void);

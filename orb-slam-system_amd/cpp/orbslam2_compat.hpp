@@ -200,6 +200,7 @@ class ORBextractor {
                            mvInvLevelSigma2.data(), mnFeaturesPerLevel.data(), umax.data()),
                "ORBextractor");
     orbx_throw(orbx_extractor_create(&p, 0, &h_), "ORBextractor");
+    orbx_throw(orbx_extractor_set_options(h_, ORBX_EXTRACTOR_PYRAMID_TO_HOST), "ORBextractor");
     mvImagePyramid.resize(nlevels);
   }
   ~ORBextractor() { orbx_extractor_destroy(h_); }
@@ -238,20 +239,27 @@ class ORBextractor {
   std::vector<float> inline GetInverseScaleSigmaSquares() { return mvInvLevelSigma2; }
 
   // the reference fills this on every call (read by Frame::ComputeStereoMatches,
-  // src/Frame.cc:453,543,555,560); monocular callers may turn the copy off
+  // src/Frame.cc:453,543,555,560).  The pyramid comes back with the call (one
+  // D2H of the level buffer overlapped with FAST .. BRIEF; level 0 is the
+  // staged copy of the image) and the headers point into the extractor's
+  // pinned buffers, which the next operator() call overwrites -- the
+  // reference's call sites read it before extracting again.  Monocular
+  // callers may turn it off.
   std::vector<cv::Mat> mvImagePyramid;
-  void SetPyramidToHost(bool on) { pyramid_to_host_ = on; }
+  void SetPyramidToHost(bool on) {
+    pyramid_to_host_ = on;
+    orbx_throw(orbx_extractor_set_options(h_, on ? ORBX_EXTRACTOR_PYRAMID_TO_HOST : 0), "ORBextractor");
+  }
   orbx_extractor* Orbx() const { return h_; }
 
  protected:
   void fill_pyramid() {
     for (int l = 0; l < nlevels; ++l) {
+      const uint8_t* d = nullptr;
+      size_t st = 0;
       int w = 0, h = 0;
-      orbx_throw(orbx_extractor_level(h_, l, nullptr, 0, &w, &h), "mvImagePyramid");
-      mvImagePyramid[l].create(h, w, CV_8U);
-      orbx_throw(orbx_extractor_level(h_, l, mvImagePyramid[l].data, mvImagePyramid[l].step, nullptr,
-                                      nullptr),
-                 "mvImagePyramid");
+      orbx_throw(orbx_extractor_level_host(h_, l, &d, &st, &w, &h), "mvImagePyramid");
+      mvImagePyramid[l] = cv::Mat(h, w, CV_8U, const_cast<uint8_t*>(d), st);
     }
   }
 

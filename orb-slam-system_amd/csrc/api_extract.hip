@@ -19,10 +19,10 @@ __global__ void k_pyramid(const uint8_t*, size_t, size_t, uint8_t*, size_t, cons
                           const int4*, const int4*, const uint4*, const int*, int);
 __global__ void k_fast_strips(const uint8_t*, size_t, size_t, const uint8_t*, size_t,
                               const LevelArgs, const CellInfo*, const StripInfo*, uint32_t*,
-                              size_t, uint32_t*, int, int, int, int, int, int, int);
+                              size_t, uint32_t*, int, int, int, int, int, int, int, int*, int);
 __global__ void k_fast_strips_p288(const uint8_t*, size_t, size_t, const uint8_t*, size_t,
                               const LevelArgs, const CellInfo*, const StripInfo*, uint32_t*,
-                              size_t, uint32_t*, int, int, int, int, int, int, int);
+                              size_t, uint32_t*, int, int, int, int, int, int, int, int*, int);
 __global__ void k_quadtree(const LevelInfo*, const CellInfo*, const uint32_t*, size_t,
                            const uint32_t*, int, uint32_t*, int32_t*, size_t, uint32_t*, size_t,
                            int*, int, int, int, int*);
@@ -164,6 +164,9 @@ extern "C" int orbx_plan_create(const orbx_params* prm, int width, int height, i
   if (const char* e = getenv("ORBX_DEBUG_STOP")) p->dbg = atoi(e);
   if (const char* e = getenv("ORBX_DEBUG_OBDIV")) p->ob_div = atoi(e);
   if (const char* e = getenv("ORBX_CHUNK")) p->chunk = atoi(e);
+  p->fs_ccap = FS_CCAP;
+  /* testing only: a smaller FAST corner list, so the overflow path runs */
+  if (const char* e = getenv("ORBX_DEBUG_CCAP")) p->fs_ccap = std::max(0, std::min(FS_CCAP, atoi(e)));
   int rc = plan_geometry(*prm, width, height, p->P);
   if (rc) { delete p; return rc; }
   const Plan& P = p->P;
@@ -306,13 +309,15 @@ static int extract_pass(orbx_plan* p, const uint8_t* frames, int n, size_t fstri
                        reinterpret_cast<const uint4*>(p->d_pyr_blob), p->d_pyr_bo, p->dbg);
   }
   p->timer.end(ORBX_STAGE_RESIZE, s);
+  if (p->ev_after_pyr && hipEventRecord(p->ev_after_pyr, s) != hipSuccess) return ORBX_ERR_HIP;
   // K2 FAST cells
   p->timer.begin(ORBX_STAGE_FAST, s);
   if (!P.strips.empty()) {
     hipLaunchKernelGGL(p->fs_tpitch == 288 ? k_fast_strips_p288 : k_fast_strips, dim3((unsigned)P.strips.size(), n), dim3(FS_NT), p->fs_lds, s,
                        frames, fstride, rstride, d_pyr, p->pyr_stride, p->largs, p->d_cells,
                        p->d_strips, d_slots, p->slot_stride, d_ccount, P.ncells, P.ini_th,
-                       P.min_th, p->fs_tpitch, p->fs_tmaxh, p->fs_mcells, p->dbg);
+                       P.min_th, p->fs_tpitch, p->fs_tmaxh, p->fs_mcells, p->fs_ccap,
+                       p->d_err + ORBX_ERRW_FAST_OVF, p->dbg);
   }
   p->timer.end(ORBX_STAGE_FAST, s);
   if (p->dbg && p->dbg < 20) return ORBX_OK; /* phase probe: later stages would read partial results */
@@ -384,6 +389,20 @@ extern "C" int orbx_plan_check(orbx_plan* p, void* stream) {
   return ORBX_OK;
 }
 
+extern "C" int orbx_plan_debug_counters(orbx_plan* p, int* fast_overflow_strips) {
+  if (!p || !fast_overflow_strips) return ORBX_ERR_ARG;
+  ORBX_TRY(hipSetDevice(p->device));
+  int v = 0;
+  ORBX_TRY(hipMemcpyAsync(&p->h_err[ORBX_ERRW_FAST_OVF], p->d_err + ORBX_ERRW_FAST_OVF, sizeof(int),
+                          hipMemcpyDeviceToHost, p->stream));
+  ORBX_TRY(hipStreamSynchronize(p->stream));
+  v = p->h_err[ORBX_ERRW_FAST_OVF];
+  ORBX_TRY(hipMemsetAsync(p->d_err + ORBX_ERRW_FAST_OVF, 0, sizeof(int), p->stream));
+  ORBX_TRY(hipStreamSynchronize(p->stream));
+  *fast_overflow_strips = v;
+  return ORBX_OK;
+}
+
 extern "C" int orbx_synth_frames(uint8_t* d_frames, int W, int H, size_t fstride, int nframes,
                                  int first_idx, int kind, void* stream) {
   if (!d_frames || W <= 0 || H <= 0 || nframes < 1 || kind < 0 || kind > 3 ||
@@ -435,8 +454,14 @@ static void extractor_release_plan(orbx_extractor* e) {
   if (e->d_desc) hipFree(e->d_desc);
   if (e->d_count) hipFree(e->d_count);
   if (e->h_res) hipHostFree(e->h_res);
+  if (e->h_img) hipHostFree(e->h_img);
+  if (e->h_pyr) hipHostFree(e->h_pyr);
+  if (e->ev_pyr) hipEventDestroy(e->ev_pyr);
+  if (e->s_copy) hipStreamDestroy(e->s_copy);
   e->plan = nullptr; e->d_img = nullptr; e->d_kps = nullptr; e->d_desc = nullptr;
   e->d_count = nullptr; e->h_res = nullptr; e->W = e->H = 0; e->have_frame = false;
+  e->h_img = nullptr; e->h_pyr = nullptr; e->ev_pyr = nullptr; e->s_copy = nullptr;
+  e->pyr_bytes = 0; e->host_pyr = false;
 }
 
 static int extractor_prepare(orbx_extractor* e, int W, int H) {
@@ -450,7 +475,16 @@ static int extractor_prepare(orbx_extractor* e, int W, int H) {
       dev_alloc((void**)&e->d_desc, 32 * kcap) ||
       dev_alloc((void**)&e->d_count, sizeof(int)) ||
       hipHostMalloc((void**)&e->h_res, 64 + (sizeof(orbx_keypoint) + 32) * kcap,
-                    hipHostMallocDefault) != hipSuccess) {
+                    hipHostMallocDefault) != hipSuccess ||
+      hipHostMalloc((void**)&e->h_img, (size_t)W * H, hipHostMallocDefault) != hipSuccess) {
+    extractor_release_plan(e);
+    return ORBX_ERR_HIP;
+  }
+  e->pyr_bytes = (size_t)e->plan->P.pyr_bytes;
+  if (e->pyr_bytes &&
+      (hipHostMalloc((void**)&e->h_pyr, e->pyr_bytes, hipHostMallocDefault) != hipSuccess ||
+       hipStreamCreateWithFlags(&e->s_copy, hipStreamNonBlocking) != hipSuccess ||
+       hipEventCreateWithFlags(&e->ev_pyr, hipEventDisableTiming) != hipSuccess)) {
     extractor_release_plan(e);
     return ORBX_ERR_HIP;
   }
@@ -501,11 +535,39 @@ extern "C" int orbx_extract(orbx_extractor* e, const uint8_t* img, int W, int H,
   ORBX_TRY(hipSetDevice(e->device));
   orbx_plan* p = e->plan;
   hipStream_t s = p->stream;
-  ORBX_TRY(hipMemcpy2DAsync(e->d_img, (size_t)W, img, stride, (size_t)W, (size_t)H,
-                            hipMemcpyHostToDevice, s));
+  e->host_pyr = false;
+  ++e->n_calls;
+  const bool to_host = (e->flags & ORBX_EXTRACTOR_PYRAMID_TO_HOST) != 0;
+  if ((e->flags & ORBX_EXTRACTOR_PAGEABLE_H2D) && !to_host) {
+    ORBX_TRY(hipMemcpy2DAsync(e->d_img, (size_t)W, img, stride, (size_t)W, (size_t)H,
+                              hipMemcpyHostToDevice, s));
+  } else {
+    // through the pinned staging buffer in row chunks of ~256 KB: the host
+    // copy of chunk c+1 runs while chunk c is DMA'd (a pageable source is
+    // staged by the runtime anyway, host-synchronously)
+    const int rows_per = std::max(1, (256 << 10) / W);
+    for (int r0 = 0; r0 < H; r0 += rows_per) {
+      const int nr = std::min(rows_per, H - r0);
+      uint8_t* h = e->h_img + (size_t)r0 * W;
+      if (stride == (size_t)W) {
+        memcpy(h, img + (size_t)r0 * W, (size_t)nr * W);
+      } else {
+        for (int r = 0; r < nr; ++r) memcpy(h + (size_t)r * W, img + (size_t)(r0 + r) * stride, (size_t)W);
+      }
+      ORBX_TRY(hipMemcpyAsync(e->d_img + (size_t)r0 * W, h, (size_t)nr * W, hipMemcpyHostToDevice, s));
+    }
+  }
+  p->ev_after_pyr = (to_host && e->pyr_bytes) ? e->ev_pyr : nullptr;
   rc = orbx_plan_extract(p, e->d_img, 1, (size_t)W * H, (size_t)W, e->d_kps, e->d_desc,
                          e->d_count, s);
+  p->ev_after_pyr = nullptr;
   if (rc) return rc;
+  if (to_host && e->pyr_bytes) {
+    // the level buffer (levels >= 2; 0 and 1 are the staged image) comes
+    // back on the copy stream while FAST, the quadtree and BRIEF run
+    ORBX_TRY(hipStreamWaitEvent(e->s_copy, e->ev_pyr, 0));
+    ORBX_TRY(hipMemcpyAsync(e->h_pyr, p->d_pyr, e->pyr_bytes, hipMemcpyDeviceToHost, e->s_copy));
+  }
   // one round trip in the common case: the error word, the count and a
   // speculative prefix of the rows (sized by the previous call) come back
   // together into pinned staging; only a larger frame needs a second copy
@@ -520,17 +582,20 @@ extern "C" int orbx_extract(orbx_extractor* e, const uint8_t* img, int W, int H,
                           hipMemcpyDeviceToHost, s));
   ORBX_TRY(hipMemcpyAsync(h_desc, e->d_desc, 32 * (size_t)guess, hipMemcpyDeviceToHost, s));
   ORBX_TRY(hipStreamSynchronize(s));
+  if (to_host && e->pyr_bytes) ORBX_TRY(hipStreamSynchronize(e->s_copy));
   if (*p->h_err) {
     rc = orbx_plan_check(p, s); /* resets the device error word */
     e->have_frame = false;
     return rc ? rc : ORBX_ERR_CAPACITY;
   }
   e->have_frame = true;
+  e->host_pyr = to_host;
   const int K = *h_cnt;
   *n = K;
   if (K == 0) return ORBX_OK; /* keypoints untouched, descriptors released (:460-463) */
   if (K > cap || !kps || !desc) return ORBX_ERR_CAPACITY;
   if (K > guess) {
+    ++e->n_refetch;
     ORBX_TRY(hipMemcpyAsync(h_kps + guess, e->d_kps + guess,
                             sizeof(orbx_keypoint) * (size_t)(K - guess), hipMemcpyDeviceToHost, s));
     ORBX_TRY(hipMemcpyAsync(h_desc + 32 * (size_t)guess, e->d_desc + 32 * (size_t)guess,
@@ -540,6 +605,36 @@ extern "C" int orbx_extract(orbx_extractor* e, const uint8_t* img, int W, int H,
   e->last_k = K;
   memcpy(kps, h_kps, sizeof(orbx_keypoint) * (size_t)K);
   memcpy(desc, h_desc, 32 * (size_t)K);
+  return ORBX_OK;
+}
+
+extern "C" int orbx_extractor_set_options(orbx_extractor* e, int flags) {
+  if (!e || (flags & ~(ORBX_EXTRACTOR_PYRAMID_TO_HOST | ORBX_EXTRACTOR_PAGEABLE_H2D))) return ORBX_ERR_ARG;
+  e->flags = flags;
+  return ORBX_OK;
+}
+
+extern "C" int orbx_extractor_stats(orbx_extractor* e, long long* calls, long long* refetches) {
+  if (!e) return ORBX_ERR_ARG;
+  if (calls) *calls = e->n_calls;
+  if (refetches) *refetches = e->n_refetch;
+  return ORBX_OK;
+}
+
+extern "C" int orbx_extractor_level_host(orbx_extractor* e, int level, const uint8_t** data,
+                                         size_t* stride, int* width, int* height) {
+  if (!e || !e->plan || !e->have_frame || !e->host_pyr || level < 0 || level >= e->params.nlevels)
+    return ORBX_ERR_ARG;
+  const LevelInfo& L = e->plan->P.levels[level];
+  if (width) *width = L.w;
+  if (height) *height = L.h;
+  if (L.unique == 0) {
+    if (data) *data = e->h_img;
+    if (stride) *stride = (size_t)e->W;
+  } else {
+    if (data) *data = e->h_pyr + e->plan->P.levels[L.unique].pyr_off;
+    if (stride) *stride = (size_t)L.pitch;
+  }
   return ORBX_OK;
 }
 

@@ -504,7 +504,6 @@ struct GroupWords {
 #endif
 #define FS_L1CAP (FS_L1FLUSH + 256) /* per-wave cardinal survivors: < FS_L1FLUSH carried + <= 256 new */
 #define FS_L2CAP 128 /* per-wave even-test survivors: < 64 carried + <= 64 new */
-#define FS_CCAP 1024 /* per-strip corner list (overflow falls back to a map scan) */
 
 
 // ---------------------------------------------------------------------------
@@ -520,7 +519,8 @@ __device__ __forceinline__ void fs_strip_body(
     uint16_t (*wlist1)[FS_L1CAP], uint16_t (*wlist2)[FS_L2CAP], uint16_t* __restrict__ clist,
     int* __restrict__ cslot, int& ncorner, const StripInfo& st, int f, int lead, int xal,
     int slot_pref, uint32_t* __restrict__ slots, size_t slot_stride,
-    uint32_t* __restrict__ ccount, int ncells, int ini_th, int min_th, int tpitch_rt, int dbg) {
+    uint32_t* __restrict__ ccount, int ncells, int ini_th, int min_th, int tpitch_rt, int ccap,
+    int* __restrict__ ovf, int dbg) {
   const int tpitch = TP ? TP : tpitch_rt;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // uniform: list bases in SGPRs
@@ -565,7 +565,7 @@ __device__ __forceinline__ void fs_strip_body(
     if (lane == 0 && bal) b = atomicAdd(&ncorner, __popcll(bal));
     b = __builtin_amdgcn_readfirstlane(b);
     const int q = b + lanes_below(bal);
-    if (corner && q < FS_CCAP) clist[q] = (uint16_t)e;
+    if (corner && q < ccap) clist[q] = (uint16_t)e;
   };
   auto even_batch = [&](int e, bool act) {
     const int ec = e & 511;
@@ -761,13 +761,14 @@ __device__ __forceinline__ void fs_strip_body(
     if (a > min_th && a - 1 > nbm) atomicOr(&mask2[k * bh + (r - 3)], bit);
   };
   const int nc = ncorner;
-  if (nc <= FS_CCAP) {
+  if (nc <= ccap) {
     for (int q = tid; q < nc; q += FS_NT) {
       const int e = clist[q];
       const int r = e >> 9, c = e & 511;
       nms_pixel(r, c, amap[r * tpitch + c]);
     }
   } else {  // list overflow: scan the strength map
+    if (tid == 0) atomicAdd(ovf, 1);  // strips that took this path (orbx_plan_debug_counters)
     const int dr = FS_NT / ng, dg = FS_NT - dr * ng;
     int r = 3 + tid / ng, g = g0 + tid % ng;
     for (; r < 3 + bh;) {
@@ -851,7 +852,8 @@ __device__ __forceinline__ void fs_kernel(
     const uint8_t* __restrict__ pyr, size_t pstride, const LevelArgs& LA,
     const CellInfo* __restrict__ cells, const StripInfo* __restrict__ strips,
     uint32_t* __restrict__ slots, size_t slot_stride, uint32_t* __restrict__ ccount, int ncells,
-    int ini_th, int min_th, int tpitch_rt, int tmax_h, int mcells, int dbg) {
+    int ini_th, int min_th, int tpitch_rt, int tmax_h, int mcells, int ccap, int* __restrict__ ovf,
+    int dbg) {
   const int tpitch = TP ? TP : tpitch_rt;
   // LDS (occupancy is LDS-bound and the kernel is latency-bound: +12 KB per
   // workgroup measured +38 % time): tile | strength map of the band rows only
@@ -905,7 +907,7 @@ __device__ __forceinline__ void fs_kernel(
   }
   fs_strip_body<TP>(tile, amap_mem, cnt, mask, mask2, wlist1, wlist2, clist, cslot, ncorner, st, f,
                     lead, xal, slot_pref, slots, slot_stride, ccount, ncells, ini_th, min_th, tpitch,
-                    dbg);
+                    ccap, ovf, dbg);
 }
 
 #define FS_KERNEL_ARGS                                                                              \
@@ -913,9 +915,9 @@ __device__ __forceinline__ void fs_kernel(
       size_t pstride, const LevelArgs LA, const CellInfo *__restrict__ cells,                       \
       const StripInfo *__restrict__ strips, uint32_t *__restrict__ slots, size_t slot_stride,      \
       uint32_t *__restrict__ ccount, int ncells, int ini_th, int min_th, int tpitch, int tmax_h,   \
-      int mcells, int dbg
+      int mcells, int ccap, int *__restrict__ ovf, int dbg
 #define FS_KERNEL_PASS \
-  frames, fstride, rstride, pyr, pstride, LA, cells, strips, slots, slot_stride, ccount, ncells, ini_th, min_th, tpitch, tmax_h, mcells, dbg
+  frames, fstride, rstride, pyr, pstride, LA, cells, strips, slots, slot_stride, ccount, ncells, ini_th, min_th, tpitch, tmax_h, mcells, ccap, ovf, dbg
 
 #ifdef FS_WPE  // profiling variant: occupancy target
 #define FS_ATTR __attribute__((amdgpu_waves_per_eu(FS_WPE)))

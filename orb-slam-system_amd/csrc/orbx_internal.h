@@ -96,6 +96,11 @@ struct StereoArgs {
 #ifndef FS_NT
 #define FS_NT 256 /* threads per k_fast_strips workgroup (one strip) */
 #endif
+#ifndef FS_CCAP
+#define FS_CCAP 1024 /* per-strip corner list (overflow falls back to a map scan) */
+#endif
+/* d_err[ORBX_ERRW_FAST_OVF]: strips whose corner list overflowed (debug counter) */
+#define ORBX_ERRW_FAST_OVF 1
 #define ORBX_DEVERR_STEREO 4 /* the reference would index out of range / throw */
 #define ORBX_STEREO_MAXROWS 8192
 

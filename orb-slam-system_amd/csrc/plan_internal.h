@@ -35,7 +35,9 @@ struct orbx_plan {
   orbx::StageTimer timer;
   int dbg = 0; /* ORBX_DEBUG_STOP: kernel phase early-exit for profiling only */
   int ob_div = 0; /* ORBX_DEBUG_OBDIV: k_orient_brief grid divisor, profiling only */
+  int fs_ccap = 0; /* FAST per-strip corner list entries used (FS_CCAP; ORBX_DEBUG_CCAP lowers it) */
   int chunk = 0;  /* frames per extraction pass (0 = the whole batch in one pass) */
+  hipEvent_t ev_after_pyr = nullptr; /* recorded after the pyramid launch when set (orbx_extract) */
 };
 
 struct orbx_extractor {
@@ -51,6 +53,14 @@ struct orbx_extractor {
   uint8_t* h_res = nullptr;
   int last_k = 0; /* keypoints of the previous call: sizes the speculative copy */
   bool have_frame = false;
+  int flags = 0;             /* ORBX_EXTRACTOR_* */
+  uint8_t* h_img = nullptr;  /* pinned staging of the caller's image (= host level 0) */
+  uint8_t* h_pyr = nullptr;  /* pinned host copy of the level buffer (PYRAMID_TO_HOST) */
+  size_t pyr_bytes = 0;
+  hipStream_t s_copy = nullptr; /* pyramid D2H, overlapped with FAST .. BRIEF */
+  hipEvent_t ev_pyr = nullptr;
+  bool host_pyr = false;     /* the last call filled h_img / h_pyr */
+  long long n_calls = 0, n_refetch = 0;
   void* stereo = nullptr; /* orbs_plan of orbx_stereo_match (api_stereo.hip) */
 };
 

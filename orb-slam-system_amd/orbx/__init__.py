@@ -47,8 +47,9 @@ EXPORTED = [
     "orbx_abi_version", "orbx_status_string", "orbx_device_count", "orbx_tables",
     "orbx_geometry_compute", "orbx_resize_tables", "orbx_extractor_create",
     "orbx_extractor_destroy", "orbx_extractor_capacity", "orbx_extract", "orbx_extractor_level",
+    "orbx_extractor_set_options", "orbx_extractor_level_host", "orbx_extractor_stats",
     "orbx_plan_create", "orbx_plan_destroy", "orbx_plan_geometry", "orbx_plan_extract",
-    "orbx_plan_check", "orbx_stage_count", "orbx_stage_name", "orbx_plan_set_timing",
+    "orbx_plan_check", "orbx_plan_debug_counters", "orbx_stage_count", "orbx_stage_name", "orbx_plan_set_timing",
     "orbx_plan_stage_times", "orbx_synth_frames", "orbm_search_by_bow",
     "orbm_descriptor_distance_batch", "orbm_plan_create", "orbm_plan_destroy",
     "orbm_plan_match_frames", "orbm_plan_set_timing", "orbm_plan_stage_times", "orbm_plan_set_options",
@@ -118,11 +119,15 @@ _sig = {
     "orbx_extractor_capacity": (I, [P, I, I, P]),
     "orbx_extract": (I, [P, P, I, I, SZ, P, I, P, P]),
     "orbx_extractor_level": (I, [P, I, P, SZ, P, P]),
+    "orbx_extractor_set_options": (I, [P, I]),
+    "orbx_extractor_level_host": (I, [P, I, P, P, P, P]),
+    "orbx_extractor_stats": (I, [P, P, P]),
     "orbx_plan_create": (I, [P, I, I, I, I, P]),
     "orbx_plan_destroy": (I, [P]),
     "orbx_plan_geometry": (I, [P, P]),
     "orbx_plan_extract": (I, [P, P, I, SZ, SZ, P, P, P, P]),
     "orbx_plan_check": (I, [P, P]),
+    "orbx_plan_debug_counters": (I, [P, P]),
     "orbx_stage_count": (I, []),
     "orbx_stage_name": (ctypes.c_char_p, [I]),
     "orbx_plan_set_timing": (I, [P, I]),
@@ -281,6 +286,27 @@ class Extractor:
         out = np.zeros((h.value, w.value), np.uint8)
         _check(_lib.orbx_extractor_level(self._h, l, _p(out), w.value, None, None))
         return out
+
+    def set_options(self, pyramid_to_host=False, pageable_h2d=False):
+        """ORBX_EXTRACTOR_* options (include/orbx.h)"""
+        _check(_lib.orbx_extractor_set_options(self._h, (1 if pyramid_to_host else 0)
+                                               | (2 if pageable_h2d else 0)), "orbx_extractor_set_options")
+
+    def level_host(self, l):
+        """copy of the host pyramid level the last extract() brought back
+        (pyramid_to_host option)"""
+        d, st = ctypes.c_void_p(), ctypes.c_size_t()
+        w, h = ctypes.c_int(), ctypes.c_int()
+        _check(_lib.orbx_extractor_level_host(self._h, l, ctypes.byref(d), ctypes.byref(st),
+                                              ctypes.byref(w), ctypes.byref(h)), "orbx_extractor_level_host")
+        buf = (ctypes.c_uint8 * (st.value * (h.value - 1) + w.value)).from_address(d.value)
+        a = np.frombuffer(buf, np.uint8)
+        return np.lib.stride_tricks.as_strided(a, (h.value, w.value), (st.value, 1)).copy()
+
+    def stats(self):
+        c, r = ctypes.c_longlong(), ctypes.c_longlong()
+        _check(_lib.orbx_extractor_stats(self._h, ctypes.byref(c), ctypes.byref(r)))
+        return {"calls": c.value, "refetches": r.value}
 
 
 # --------------------------------------------------------------------------- stereo
@@ -527,6 +553,12 @@ class Plan:
 
     def check(self, stream=None):
         _check(_lib.orbx_plan_check(self._h, _stream_handle(stream)), "orbx_plan_check")
+
+    def debug_counters(self):
+        """{'fast_overflow_strips': n} since the last call (synchronises the plan's stream)"""
+        v = ctypes.c_int(0)
+        _check(_lib.orbx_plan_debug_counters(self._h, ctypes.byref(v)), "orbx_plan_debug_counters")
+        return {"fast_overflow_strips": v.value}
 
     def set_timing(self, enable):
         _check(_lib.orbx_plan_set_timing(self._h, 1 if enable else 0))

@@ -47,6 +47,33 @@ def test_extract_matches_oracle(gpu, oracle, w, h, nf, L, guard, kind, idx):
         assert np.array_equal(ex.level(l), ref.level(l)), "pyramid level %d" % l
 
 
+@pytest.mark.parametrize("w,h,nf,guard", [(640, 480, 1000, "strict"), (1920, 1080, 2000, "empty"),
+                                           (642, 361, 1000, "strict")])
+def test_extractor_options_match_oracle(gpu, oracle, w, h, nf, guard):
+    """ORBX_EXTRACTOR_PYRAMID_TO_HOST (the compat operator()'s mvImagePyramid,
+    brought back with the call) and the pageable-H2D upload give the same
+    keypoints / descriptors; the host levels equal the oracle's pyramid and
+    follow the next call."""
+    ref = oracle.Extractor(nf, 1.2, 8, 20, 7, cell_guard=guard)
+    ex = gpu.Extractor(nf, 1.2, 8, 20, 7, cell_guard=guard)
+    for i, opts in enumerate(({"pyramid_to_host": True}, {"pyramid_to_host": True},
+                              {"pageable_h2d": True}, {})):
+        img = synth.frame(w, h, 90 + i, "pan" if i % 2 else "noise")
+        ex.set_options(**opts)
+        k, d = ex.extract(img)
+        rk, rd = ref.extract(img)
+        _cmp_kps(k, rk, "keypoints %r" % opts)
+        assert np.array_equal(d, rd), "descriptors differ %r" % opts
+        if opts.get("pyramid_to_host"):
+            for l in range(8):
+                assert np.array_equal(ex.level_host(l), ref.level(l)), "host level %d" % l
+        else:
+            with pytest.raises(gpu.OrbxError):
+                ex.level_host(0)
+    st = ex.stats()
+    assert st["calls"] == 4 and 0 <= st["refetches"] <= 4
+
+
 # other pyramid ratios: the pyramid's 8-byte source window (k_pyramid) and
 # the planner's tiling change with the scale factor
 SCALE_CASES = [
@@ -104,6 +131,35 @@ def test_batched_plan_matches_single(gpu, oracle):
         rk, rd = ref.extract(synth.frame(W, H, 20 + f))
         _cmp_kps(res[f][0], rk, "frame %d" % f)
         assert np.array_equal(res[f][1], rd)
+
+
+@pytest.mark.parametrize("W,H,nf,guard,ccap", [(640, 480, 1000, "strict", 0),
+                                                (640, 480, 1000, "strict", 24),
+                                                (1920, 1080, 2000, "empty", 48),
+                                                (1241, 376, 2000, "strict", 96)])
+def test_fast_corner_list_overflow_path(gpu, oracle, monkeypatch, W, H, nf, guard, ccap):
+    """k_fast_strips' per-strip corner list overflow: with the list capacity
+    lowered (ORBX_DEBUG_CCAP, read at plan creation) the NMS walks the
+    strength map instead of the list.  The debug counter proves the branch
+    ran; every keypoint field and descriptor byte must still equal the oracle."""
+    import torch
+    B = 3
+    monkeypatch.setenv("ORBX_DEBUG_CCAP", str(ccap))
+    plan = gpu.Plan(gpu.params(nf, 1.2, 8, 20, 7, guard), W, H, B)
+    monkeypatch.delenv("ORBX_DEBUG_CCAP")
+    kinds = ("noise", "rects", "pan")
+    frames = np.stack([synth.frame(W, H, 60 + f, kinds[f]) for f in range(B)])
+    plan.extract(torch.from_numpy(frames).cuda())
+    plan.check()
+    ovf = plan.debug_counters()["fast_overflow_strips"]
+    assert ovf > 0, "the overflow branch never ran"
+    res = plan.results(B)
+    for f in range(B):
+        rk, rd = oracle.Extractor(nf, 1.2, 8, 20, 7, cell_guard=guard).extract(frames[f])
+        _cmp_kps(res[f][0], rk, "frame %d (%d overflowing strips)" % (f, ovf))
+        assert np.array_equal(res[f][1], rd)
+    # the production capacity: this plan's counter starts at 0 again
+    assert plan.debug_counters()["fast_overflow_strips"] == 0
 
 
 def _random_bow(rng, n, nnodes, vocab, desc=None, dup=False):
