@@ -408,6 +408,96 @@ def compat_latency(calls, warm):
     return json.loads(r.stdout)
 
 
+# --------------------------------------------------------------------------- host-fed throughput
+def host_fed_leg(torch, orbx, plan, mp, wl, args, dev, ref_counts, steps=6, warm=2):
+    """The c4 step fed from the host, as a real Tracking front end sees it
+    (ORBextractor::operator() starts from a host cv::Mat, ORBextractor.cc:
+    442-448): each step's 256 frames come from pinned host memory (H2D on a
+    copy stream), are extracted and matched against their predecessors on a
+    compute stream, and the keypoints, descriptors and matches go back to
+    pinned host memory on a third stream (D2H of the first R rows per frame).
+    Steps k-1 (D2H), k (compute) and k+1 (H2D) overlap on double buffers."""
+    B, W, H, kcap = args.batch, wl["W"], wl["H"], plan.kcap
+    R = min(kcap, (wl["nfeatures"] * 5 // 4 + 63) // 64 * 64)  # rows returned per frame
+    host = torch.empty((2, B, H, W), dtype=torch.uint8).pin_memory()
+    tmp = torch.empty((B, H, W), dtype=torch.uint8, device=dev)
+    for j in range(2):
+        orbx.synth_frames(tmp, j * B, args.kind)
+        torch.cuda.synchronize()
+        host[j].copy_(tmp)
+    del tmp
+    dfr = [torch.empty((B, H, W), dtype=torch.uint8, device=dev) for _ in range(2)]
+    kps = [torch.zeros((B + 1, kcap, 28), dtype=torch.uint8, device=dev) for _ in range(2)]
+    desc = [torch.zeros((B + 1, kcap, 32), dtype=torch.uint8, device=dev) for _ in range(2)]
+    cnt = [torch.zeros(B + 1, dtype=torch.int32, device=dev) for _ in range(2)]
+    m12 = [torch.empty((B, R), dtype=torch.int32, device=dev) for _ in range(2)]
+    hk = torch.empty((2, B, R, 28), dtype=torch.uint8).pin_memory()
+    hd = torch.empty((2, B, R, 32), dtype=torch.uint8).pin_memory()
+    hc = torch.empty((2, B), dtype=torch.int32).pin_memory()
+    hm = torch.empty((2, B, R), dtype=torch.int32).pin_memory()
+    s_in, s_c, s_out = (torch.cuda.Stream(device=dev) for _ in range(3))
+    ev_in = [torch.cuda.Event() for _ in range(2)]
+    ev_c = [torch.cuda.Event() for _ in range(2)]
+    ev_out = [torch.cuda.Event() for _ in range(2)]
+    for s in (s_in, s_c, s_out):
+        s.wait_stream(torch.cuda.current_stream())
+    for i in range(2):
+        ev_c[i].record(s_c)
+        ev_out[i].record(s_out)
+
+    def step(k):
+        i = k & 1
+        with torch.cuda.stream(s_in):
+            s_in.wait_event(ev_c[i])  # the compute of step k-2 has read dfr[i]
+            dfr[i].copy_(host[k & 1], non_blocking=True)
+            ev_in[i].record(s_in)
+        with torch.cuda.stream(s_c):
+            s_c.wait_event(ev_in[i])
+            s_c.wait_event(ev_out[i])  # the D2H of step k-2 has read buffer i
+            kps[i][0].copy_(kps[1 - i][B])
+            desc[i][0].copy_(desc[1 - i][B])
+            cnt[i][0:1].copy_(cnt[1 - i][B:B + 1])
+            plan.extract(dfr[i], stream=s_c, out=(kps[i][1:], desc[i][1:], cnt[i][1:]))
+            mp.match(B, kps[i][1:], desc[i][1:], cnt[i][1:], kps[i], desc[i], cnt[i], args.nnratio,
+                     True, stream=s_c)
+            m12[i].copy_(mp.match12[:B, :R])
+            ev_c[i].record(s_c)
+        with torch.cuda.stream(s_out):
+            s_out.wait_event(ev_c[i])
+            hk[i].copy_(kps[i][1:, :R], non_blocking=True)
+            hd[i].copy_(desc[i][1:, :R], non_blocking=True)
+            hc[i].copy_(cnt[i][1:], non_blocking=True)
+            hm[i].copy_(m12[i], non_blocking=True)
+            ev_out[i].record(s_out)
+
+    for k in range(warm):
+        step(k)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(warm, warm + steps):
+        step(k)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    plan.check()
+    maxk = int(hc.max().item())
+    # host[0] holds the resident run's frames and buffer 0 (even steps) the
+    # results of host[0]: the keypoint counts must agree
+    same = bool(torch.equal(hc[0], ref_counts.cpu()))
+    h2d = B * W * H
+    d2h = B * (R * (28 + 32 + 4) + 4)
+    return {"value": round(B * steps / el, 2), "unit": "frames/s", "steps": steps,
+            "ms_per_step": round(el / steps * 1e3, 3),
+            "pcie_h2d_gbs": round(h2d * steps / el / 1e9, 2),
+            "pcie_d2h_gbs": round(d2h * steps / el / 1e9, 2),
+            "bytes_per_step": {"h2d": h2d, "d2h": d2h}, "rows_returned_per_frame": R,
+            "max_keypoints_per_frame": maxk, "rows_cover_all_keypoints": maxk <= R,
+            "counts_equal_resident_run": same,
+            "note": "frames from pinned host memory (H2D on a copy stream), extraction + SearchByBoW "
+                    "on a compute stream, keypoints/descriptors/matches back to pinned host memory "
+                    "on a third stream; steps overlap on double buffers (bound: the PCIe H2D of the "
+                    "frames)"}
+
+
 # --------------------------------------------------------------------------- distributed
 def dist_setup(args):
     import torch
@@ -421,11 +511,16 @@ def dist_setup(args):
         local = 0
     torch.cuda.set_device(local)
     if world > 1:
+        import datetime
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        # collective timeout: a rank that stops answering makes the
+        # others fail (non-zero exit; launch_ranks then stops the siblings)
+        # instead of hanging the job
+        tmo = datetime.timedelta(seconds=float(os.environ.get("ORBX_COLLECTIVE_TIMEOUT_S", "180")))
         if _share_gpu():
-            dist.init_process_group("gloo")
+            dist.init_process_group("gloo", timeout=tmo)
         else:
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local), timeout=tmo)
     return torch, dist, world, rank, local
 
 
@@ -609,6 +704,7 @@ def main_mono(args, wl):
                          "note": "stage times and roofline entries come from this serial timed loop "
                                  "(kernels alone on the GPU)"}
     if world == 1 and not args.no_latency and args.workload == "c4":
+        out["host_fed"] = host_fed_leg(torch, orbx, plan, mp, wl, args, dev, counts[1:])
         out["latency"] = latency_leg()
     if world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args, wl)

@@ -400,6 +400,17 @@ int orbm_compute_distinctive_descriptors(const uint8_t* desc, const int32_t* off
 int orbx_undistort_keypoints(const orbx_keypoint* kps, int n, const float* K, const float* dist,
                              int ndist, int device, orbx_keypoint* out);
 
+/* Multi-GPU boundary frame (bench/orbx.dist): one frame of
+ * orbx_plan_extract outputs (kcap keypoint rows, kcap descriptor rows, the
+ * count) as one contiguous record of orbx_boundary_record_bytes(kcap) bytes
+ * [kps | desc | count | pad], the unit of the RCCL all-gather.  Device
+ * pointers (kps/desc 4-B aligned), asynchronous on `stream`, one launch. */
+size_t orbx_boundary_record_bytes(int kcap);
+int orbx_boundary_pack(const orbx_keypoint* d_kps, const uint8_t* d_desc, const int* d_count,
+                       int kcap, uint8_t* d_record, void* stream);
+int orbx_boundary_unpack(const uint8_t* d_record, int kcap, orbx_keypoint* d_kps, uint8_t* d_desc,
+                         int* d_count, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -15,6 +15,8 @@ struct UndistortArgs {
 };
 __global__ void k_distinctive(const uint8_t*, const int32_t*, int, int32_t*);
 __global__ void k_undistort(const orbx_keypoint*, int, const UndistortArgs, orbx_keypoint*);
+__global__ void k_boundary_copy(const uint8_t*, size_t, const uint8_t*, size_t, const uint8_t*, size_t,
+                                uint8_t*, int, uint8_t*, uint8_t*, uint8_t*);
 }  // namespace orbx
 
 using namespace orbx;
@@ -98,4 +100,32 @@ extern "C" int orbx_undistort_keypoints(const orbx_keypoint* kps, int n, const f
   ORBX_TRY(hipStreamSynchronize(w->stream));
   memcpy(out, w->h + o_out, (size_t)n * sizeof(orbx_keypoint));
   return ORBX_OK;
+}
+
+extern "C" size_t orbx_boundary_record_bytes(int kcap) {
+  return kcap > 0 ? (size_t)kcap * (sizeof(orbx_keypoint) + 32) + 16 : 0;
+}
+
+static int boundary_copy(int kcap, const void* a, const void* b, const void* c, void* rec, int unpack,
+                         void* oa, void* ob, void* oc, void* stream) {
+  if (kcap < 1) return ORBX_ERR_ARG;
+  const size_t na = (size_t)kcap * sizeof(orbx_keypoint), nb = (size_t)kcap * 32, nc = 4;
+  const size_t n = na + nb + nc;
+  const unsigned blocks = (unsigned)std::min<size_t>((n + 4095) / 4096, 1024);
+  hipLaunchKernelGGL(k_boundary_copy, dim3(blocks), dim3(256), 0, (hipStream_t)stream,
+                     (const uint8_t*)a, na, (const uint8_t*)b, nb, (const uint8_t*)c, nc,
+                     (uint8_t*)rec, unpack, (uint8_t*)oa, (uint8_t*)ob, (uint8_t*)oc);
+  return hipGetLastError() == hipSuccess ? ORBX_OK : ORBX_ERR_HIP;
+}
+
+extern "C" int orbx_boundary_pack(const orbx_keypoint* d_kps, const uint8_t* d_desc,
+                                  const int* d_count, int kcap, uint8_t* d_record, void* stream) {
+  if (!d_kps || !d_desc || !d_count || !d_record) return ORBX_ERR_ARG;
+  return boundary_copy(kcap, d_kps, d_desc, d_count, d_record, 0, nullptr, nullptr, nullptr, stream);
+}
+
+extern "C" int orbx_boundary_unpack(const uint8_t* d_record, int kcap, orbx_keypoint* d_kps,
+                                    uint8_t* d_desc, int* d_count, void* stream) {
+  if (!d_kps || !d_desc || !d_count || !d_record) return ORBX_ERR_ARG;
+  return boundary_copy(kcap, d_record, nullptr, nullptr, nullptr, 1, d_kps, d_desc, d_count, stream);
 }

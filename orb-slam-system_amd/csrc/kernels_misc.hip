@@ -88,4 +88,38 @@ __global__ __launch_bounds__(256) void k_undistort(const orbx_keypoint* __restri
   out[i] = kp;
 }
 
+// ---------------------------------------------------------------------------
+// Multi-GPU boundary frame (orbx/dist.py): one frame's outputs
+// (kcap keypoint rows, kcap descriptor rows, count) packed into / unpacked
+// from one contiguous exchange record [kps | desc | count]: one launch each
+// instead of six tensor copies (dword copies, 16 B per thread and pass; the
+// region sizes 28 kcap, 32 kcap and 4 are dword multiples).  Rows beyond the
+// frame's count are copied too (the record has a fixed size for the
+// all-gather).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_boundary_copy(const uint8_t* __restrict__ a, size_t na,
+                                                       const uint8_t* __restrict__ b, size_t nb,
+                                                       const uint8_t* __restrict__ c, size_t nc,
+                                                       uint8_t* __restrict__ out, int unpack,
+                                                       uint8_t* __restrict__ oa,
+                                                       uint8_t* __restrict__ ob,
+                                                       uint8_t* __restrict__ oc) {
+  // pack: out = a | b | c; unpack: a (= the record) -> oa | ob | oc
+  const size_t n = na + nb + nc;
+  for (size_t i = ((size_t)blockIdx.x * 256 + threadIdx.x) * 16; i < n; i += (size_t)gridDim.x * 256 * 16) {
+    uint32_t w[4];
+    const int m = (int)min((size_t)16, n - i) >> 2;
+    for (int k = 0; k < m; ++k) {
+      const size_t j = i + 4 * k;
+      const uint8_t* src = unpack ? a + j : (j < na ? a + j : j < na + nb ? b + (j - na) : c + (j - na - nb));
+      w[k] = *reinterpret_cast<const uint32_t*>(src);
+    }
+    for (int k = 0; k < m; ++k) {
+      const size_t j = i + 4 * k;
+      uint8_t* dst = !unpack ? out + j : (j < na ? oa + j : j < na + nb ? ob + (j - na) : oc + (j - na - nb));
+      *reinterpret_cast<uint32_t*>(dst) = w[k];
+    }
+  }
+}
+
 }  // namespace orbx

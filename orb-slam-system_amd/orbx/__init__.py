@@ -48,6 +48,7 @@ EXPORTED = [
     "orbx_geometry_compute", "orbx_resize_tables", "orbx_extractor_create",
     "orbx_extractor_destroy", "orbx_extractor_capacity", "orbx_extract", "orbx_extractor_level",
     "orbx_extractor_set_options", "orbx_extractor_level_host", "orbx_extractor_stats",
+    "orbx_boundary_record_bytes", "orbx_boundary_pack", "orbx_boundary_unpack",
     "orbx_plan_create", "orbx_plan_destroy", "orbx_plan_geometry", "orbx_plan_extract",
     "orbx_plan_check", "orbx_plan_debug_counters", "orbx_stage_count", "orbx_stage_name", "orbx_plan_set_timing",
     "orbx_plan_stage_times", "orbx_synth_frames", "orbm_search_by_bow",
@@ -122,6 +123,9 @@ _sig = {
     "orbx_extractor_set_options": (I, [P, I]),
     "orbx_extractor_level_host": (I, [P, I, P, P, P, P]),
     "orbx_extractor_stats": (I, [P, P, P]),
+    "orbx_boundary_record_bytes": (SZ, [I]),
+    "orbx_boundary_pack": (I, [P, P, P, I, P, P]),
+    "orbx_boundary_unpack": (I, [P, I, P, P, P, P]),
     "orbx_plan_create": (I, [P, I, I, I, I, P]),
     "orbx_plan_destroy": (I, [P]),
     "orbx_plan_geometry": (I, [P, P]),

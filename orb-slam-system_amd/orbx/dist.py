@@ -9,6 +9,8 @@ takes rank W-1's entry of the previous step (the job's frame before its
 first one), kept from the previous exchange.  With the "nccl" backend this
 is an RCCL all-gather over xGMI; tests run it with gloo on CPU.
 """
+import ctypes
+
 import torch
 
 
@@ -22,12 +24,29 @@ class BoundaryExchange:
 
     def __init__(self, kcap, world, device):
         self.kcap, self.world = kcap, world
-        self.nbytes = kcap * 60 + 16
+        self.nbytes = kcap * 60 + 16  # = orbx_boundary_record_bytes(kcap)
         self.mine = torch.zeros(self.nbytes, dtype=torch.uint8, device=device)
-        self.gathered = torch.zeros((world, self.nbytes), dtype=torch.uint8, device=device)
+        # two all-gather targets used alternately: rank 0 reads the previous
+        # step's last record from the other one (no carry copy)
+        self._bufs = [torch.zeros((world, self.nbytes), dtype=torch.uint8, device=device)
+                      for _ in range(2)]
+        self._step = 0
+        self.gathered = self._bufs[0]
+
+    def _native(self, *ts):
+        # device-resident exchange (RCCL): one liborbx launch per pack /
+        # unpack (orbx_boundary_pack / _unpack) instead of three tensor copies
+        return self.mine.is_cuda and all(t.is_cuda and t.is_contiguous() for t in ts)
 
     def pack(self, kps, desc, count):
         k = self.kcap
+        if self._native(kps, desc, count):
+            import orbx
+            orbx._check(orbx.lib().orbx_boundary_pack(
+                ctypes.c_void_p(kps.data_ptr()), ctypes.c_void_p(desc.data_ptr()),
+                ctypes.c_void_p(count.data_ptr()), k, ctypes.c_void_p(self.mine.data_ptr()),
+                orbx._stream_handle(None)), "orbx_boundary_pack")
+            return
         self.mine[:k * 28].copy_(kps.reshape(-1))
         self.mine[k * 28:k * 60].copy_(desc.reshape(-1))
         self.mine[k * 60:k * 60 + 4].copy_(count.reshape(1).view(torch.uint8))
@@ -39,25 +58,30 @@ class BoundaryExchange:
         """After this step's extraction: last = (kps, desc, count) of this
         rank's last frame, slot0 = buffers receiving its first frame's
         predecessor (see module doc)."""
-        if not hasattr(self, "carry"):
-            self.carry = torch.zeros_like(self.mine)  # job-wide last frame of the previous step
+        prev = self.gathered  # previous step's records (zeros before the first step)
+        self.gathered = self._bufs[self._step & 1]
+        if self._step == 0:
+            prev = self._bufs[1]
+        self._step += 1
         self.pack(*last)
         self.exchange(dist, group)
         if rank > 0:
             self.unpack_into(rank - 1, *slot0)
-        else:
-            self._unpack(self.carry, *slot0)
-        self.carry.copy_(self.gathered[self.world - 1])
+        else:  # the job-wide last frame of the previous step
+            self._unpack(prev[self.world - 1], *slot0)
 
     def _unpack(self, src, kps, desc, count):
         k = self.kcap
+        if self._native(src, kps, desc, count):
+            import orbx
+            orbx._check(orbx.lib().orbx_boundary_unpack(
+                ctypes.c_void_p(src.data_ptr()), k, ctypes.c_void_p(kps.data_ptr()),
+                ctypes.c_void_p(desc.data_ptr()), ctypes.c_void_p(count.data_ptr()),
+                orbx._stream_handle(None)), "orbx_boundary_unpack")
+            return
         kps.copy_(src[:k * 28].view(k, 28))
         desc.copy_(src[k * 28:k * 60].view(k, 32))
         count.copy_(src[k * 60:k * 60 + 4].view(torch.int32).reshape(count.shape))
 
     def unpack_into(self, src_rank, kps, desc, count):
-        k = self.kcap
-        src = self.gathered[src_rank]
-        kps.copy_(src[:k * 28].view(k, 28))
-        desc.copy_(src[k * 28:k * 60].view(k, 32))
-        count.copy_(src[k * 60:k * 60 + 4].view(torch.int32).reshape(count.shape))
+        self._unpack(self.gathered[src_rank], kps, desc, count)

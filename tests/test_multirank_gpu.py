@@ -21,7 +21,7 @@ def _free_port():
     return p
 
 
-def _rank(rank, world, port, q):
+def _rank(rank, world, port, q, backend="gloo"):
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sys.path.insert(0, os.path.join(root, "orb-slam-system_amd"))
@@ -29,19 +29,25 @@ def _rank(rank, world, port, q):
     import torch.distributed as dist
     import orbx
     from orbx.dist import BoundaryExchange, shard_first_frame
+    import datetime
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    # gloo: both ranks on cuda:0, host-staged exchange; nccl: one GPU per
+    # rank, the records all-gathered by RCCL straight from HBM
+    dev = torch.device("cuda", rank if backend == "nccl" else 0)
+    torch.cuda.set_device(dev)
+    kw = {"device_id": dev} if backend == "nccl" else {}
+    dist.init_process_group(backend, rank=rank, world_size=world,
+                            timeout=datetime.timedelta(seconds=120), **kw)
     try:
-        dev = torch.device("cuda", 0)
         prm = orbx.params(NF, 1.2, 8, 20, 7)
-        plan = orbx.Plan(prm, W, H, B)
+        plan = orbx.Plan(prm, W, H, B, device=dev.index)
         kcap = plan.kcap
-        mp = orbx.MatchPlan(B, kcap, NF)
+        mp = orbx.MatchPlan(B, kcap, NF, device=dev.index)
         kps = torch.zeros((B + 1, kcap, 28), dtype=torch.uint8, device=dev)
         desc = torch.zeros((B + 1, kcap, 32), dtype=torch.uint8, device=dev)
         counts = torch.zeros(B + 1, dtype=torch.int32, device=dev)
-        xch = BoundaryExchange(kcap, world, torch.device("cpu"))  # gloo: host-staged
+        xch = BoundaryExchange(kcap, world, dev if backend == "nccl" else torch.device("cpu"))
         frames = torch.empty((B, H, W), dtype=torch.uint8, device=dev)
         res = []
         for step in range(STEPS):
@@ -59,15 +65,23 @@ def _rank(rank, world, port, q):
         dist.destroy_process_group()
 
 
+def _two_gpus():
+    import torch
+    return torch.cuda.device_count() >= 2  # does not initialise the GPU on this image
+
+
 @pytest.mark.gpu
-def test_two_ranks_match_single_process(gpu):
+@pytest.mark.parametrize("backend", ["gloo", "nccl"])
+def test_two_ranks_match_single_process(gpu, backend):
     import torch
     import torch.multiprocessing as mp
+    if backend == "nccl" and not _two_gpus():
+        pytest.skip("RCCL rehearsal needs 2 visible GPUs")
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_rank, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_rank, args=(r, world, port, q, backend)) for r in range(world)]
     for p in procs:
         p.start()
     got = dict(q.get(timeout=240) for _ in range(world))
@@ -106,3 +120,27 @@ def test_two_ranks_match_single_process(gpu):
                     boundary += 1
                     assert int(n[i]) > 0  # the exchanged predecessor really matched
     assert boundary == world * STEPS - 1
+
+
+@pytest.mark.gpu
+def test_boundary_record_pack_unpack(gpu):
+    """orbx_boundary_pack / _unpack (one launch each) build the same record as
+    the tensor copies of the host-staged path and restore the frame exactly."""
+    import torch
+    from orbx.dist import BoundaryExchange
+    kcap = 1337
+    g = torch.Generator(device="cpu").manual_seed(7)
+    kps = torch.randint(0, 256, (kcap, 28), dtype=torch.uint8, generator=g).cuda()
+    desc = torch.randint(0, 256, (kcap, 32), dtype=torch.uint8, generator=g).cuda()
+    cnt = torch.tensor([1234], dtype=torch.int32).cuda()
+    dev_x = BoundaryExchange(kcap, 1, torch.device("cuda"))
+    host_x = BoundaryExchange(kcap, 1, torch.device("cpu"))
+    dev_x.pack(kps, desc, cnt)
+    host_x.pack(kps.cpu(), desc.cpu(), cnt.cpu())
+    torch.cuda.synchronize()
+    assert dev_x.mine.numel() == gpu.lib().orbx_boundary_record_bytes(kcap)
+    assert torch.equal(dev_x.mine[:kcap * 60 + 4].cpu(), host_x.mine[:kcap * 60 + 4])
+    k2, d2, c2 = torch.zeros_like(kps), torch.zeros_like(desc), torch.zeros_like(cnt)
+    dev_x._unpack(dev_x.mine, k2, d2, c2)
+    torch.cuda.synchronize()
+    assert torch.equal(k2, kps) and torch.equal(d2, desc) and int(c2.item()) == 1234
