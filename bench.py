@@ -331,7 +331,7 @@ def latency_leg(calls=200, warm=20):
     for tag, (W, H, nf, guard), opts in (
             ("extract_640x480", (640, 480, 1000, "strict"), {}),
             ("extract_1920x1080", (1920, 1080, 2000, "empty"), {}),
-            ("extract_1920x1080_pageable_h2d", (1920, 1080, 2000, "empty"), {"pageable_h2d": True})):
+            ("extract_1920x1080_pinned_h2d", (1920, 1080, 2000, "empty"), {"pinned_h2d": True})):
         ex = orbx.Extractor(nf, 1.2, 8, 20, 7, guard)
         ex.set_options(**opts)
         imgs = [np.ascontiguousarray(synth.frame(W, H, i, "pan")) for i in range(8)]
@@ -379,8 +379,9 @@ def latency_leg(calls=200, warm=20):
     out["search_by_bow_2000x2000"] = {"p50_us": round(_pct(ts, 50), 1),
                                       "p99_us": round(_pct(ts, 99), 1), "calls": calls,
                                       "features": [int(b1.n), int(b2.n)], "matches": nm.value}
-    out["note"] = ("one synchronous C-ABI call at a time from the host (image H2D through pinned "
-                   "staging unless *_pageable_h2d, kernels, results D2H), timed around the call; "
+    out["note"] = ("one synchronous C-ABI call at a time from the host (image H2D from the caller's "
+                   "pageable rows, or through pinned staging for *_pinned_h2d; kernels; results D2H), "
+                   "timed around the call; "
                    "compat_operator_*: ORB_SLAM2::ORBextractor::operator() of cpp/orbslam2_compat.hpp "
                    "(tools/compat_latency.cpp), with and without mvImagePyramid on the host; the "
                    "throughput line above is the batched device-resident path")
@@ -418,7 +419,7 @@ def host_fed_leg(torch, orbx, plan, mp, wl, args, dev, ref_counts, steps=6, warm
     pinned host memory on a third stream (D2H of the first R rows per frame).
     Steps k-1 (D2H), k (compute) and k+1 (H2D) overlap on double buffers."""
     B, W, H, kcap = args.batch, wl["W"], wl["H"], plan.kcap
-    R = min(kcap, (wl["nfeatures"] * 5 // 4 + 63) // 64 * 64)  # rows returned per frame
+    R = min(kcap, (wl["nfeatures"] * 3 // 2 + 63) // 64 * 64)  # rows returned per frame
     host = torch.empty((2, B, H, W), dtype=torch.uint8).pin_memory()
     tmp = torch.empty((B, H, W), dtype=torch.uint8, device=dev)
     for j in range(2):

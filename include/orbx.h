@@ -125,12 +125,12 @@ int orbx_extractor_level(orbx_extractor* e, int level, uint8_t* dst, size_t dst_
  *     src/ORBextractor.cc:497-515, read by Frame::ComputeStereoMatches): one
  *     D2H of the level buffer on a second stream, overlapped with the rest
  *     of the extraction; read it with orbx_extractor_level_host;
- * ORBX_EXTRACTOR_PAGEABLE_H2D  upload the caller's image straight from its
- *     (pageable) rows instead of through the extractor's pinned staging
- *     (measurement aid; ignored with PYRAMID_TO_HOST, whose level 0 is the
- *     staged copy). */
+ * ORBX_EXTRACTOR_PINNED_H2D  upload the caller's image through the
+ *     extractor's pinned staging buffer (host copy in row chunks overlapped
+ *     with the DMA) instead of straight from its pageable rows (measurement
+ *     option: slower at 1080p). */
 #define ORBX_EXTRACTOR_PYRAMID_TO_HOST 1
-#define ORBX_EXTRACTOR_PAGEABLE_H2D 2
+#define ORBX_EXTRACTOR_PINNED_H2D 2
 int orbx_extractor_set_options(orbx_extractor* e, int flags);
 
 /* Host view of mvImagePyramid[level] after an orbx_extract with

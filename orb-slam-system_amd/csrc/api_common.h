@@ -141,6 +141,13 @@ struct WsLease {
   WsLease& operator=(const WsLease&) = delete;
 };
 
+// Completion wait of the synchronous drop-in calls: the caller (Tracking,
+// LoopClosing) blocks on the result anyway, so the stream is polled for up
+// to ORBX_SPIN_US microseconds before falling back to hipStreamSynchronize,
+// whose blocking wake-up showed up as 2-4x p50 outliers in the per-call
+// latency (bench latency leg).
+hipError_t stream_wait(hipStream_t s);
+
 // hipFuncAttributeMaxDynamicSharedMemorySize is process-wide per kernel:
 // set it once per (kernel, device) to the CU's whole LDS, never per call (a
 // concurrent call writing a smaller value could undercut a larger launch).

@@ -481,10 +481,9 @@ static int extractor_prepare(orbx_extractor* e, int W, int H) {
     return ORBX_ERR_HIP;
   }
   e->pyr_bytes = (size_t)e->plan->P.pyr_bytes;
-  if (e->pyr_bytes &&
-      (hipHostMalloc((void**)&e->h_pyr, e->pyr_bytes, hipHostMallocDefault) != hipSuccess ||
-       hipStreamCreateWithFlags(&e->s_copy, hipStreamNonBlocking) != hipSuccess ||
-       hipEventCreateWithFlags(&e->ev_pyr, hipEventDisableTiming) != hipSuccess)) {
+  if ((e->pyr_bytes && hipHostMalloc((void**)&e->h_pyr, e->pyr_bytes, hipHostMallocDefault) != hipSuccess) ||
+      hipStreamCreateWithFlags(&e->s_copy, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&e->ev_pyr, hipEventDisableTiming) != hipSuccess) {
     extractor_release_plan(e);
     return ORBX_ERR_HIP;
   }
@@ -517,6 +516,10 @@ extern "C" int orbx_extractor_destroy(orbx_extractor* e) {
 
 extern "C" int orbx_extractor_capacity(orbx_extractor* e, int W, int H, int* kcap) {
   if (!e || !kcap) return ORBX_ERR_ARG;
+  if (e->plan && e->W == W && e->H == H) {  // every call of the drop-in asks: no re-planning
+    *kcap = e->plan->P.kcap;
+    return ORBX_OK;
+  }
   Plan P;
   int rc = plan_geometry(e->params, W, H, P);
   if (rc) return rc;
@@ -538,13 +541,15 @@ extern "C" int orbx_extract(orbx_extractor* e, const uint8_t* img, int W, int H,
   e->host_pyr = false;
   ++e->n_calls;
   const bool to_host = (e->flags & ORBX_EXTRACTOR_PYRAMID_TO_HOST) != 0;
-  if ((e->flags & ORBX_EXTRACTOR_PAGEABLE_H2D) && !to_host) {
+  if (!(e->flags & ORBX_EXTRACTOR_PINNED_H2D)) {
+    // straight from the caller's (pageable) rows: the runtime's own staging
+    // measured faster than a host copy into pinned memory (176 vs 257 us per
+    // 1080p call, bench latency leg)
     ORBX_TRY(hipMemcpy2DAsync(e->d_img, (size_t)W, img, stride, (size_t)W, (size_t)H,
                               hipMemcpyHostToDevice, s));
   } else {
     // through the pinned staging buffer in row chunks of ~256 KB: the host
-    // copy of chunk c+1 runs while chunk c is DMA'd (a pageable source is
-    // staged by the runtime anyway, host-synchronously)
+    // copy of chunk c+1 runs while chunk c is DMA'd (measurement option)
     const int rows_per = std::max(1, (256 << 10) / W);
     for (int r0 = 0; r0 < H; r0 += rows_per) {
       const int nr = std::min(rows_per, H - r0);
@@ -557,16 +562,20 @@ extern "C" int orbx_extract(orbx_extractor* e, const uint8_t* img, int W, int H,
       ORBX_TRY(hipMemcpyAsync(e->d_img + (size_t)r0 * W, h, (size_t)nr * W, hipMemcpyHostToDevice, s));
     }
   }
-  p->ev_after_pyr = (to_host && e->pyr_bytes) ? e->ev_pyr : nullptr;
+  p->ev_after_pyr = to_host ? e->ev_pyr : nullptr;
   rc = orbx_plan_extract(p, e->d_img, 1, (size_t)W * H, (size_t)W, e->d_kps, e->d_desc,
                          e->d_count, s);
   p->ev_after_pyr = nullptr;
   if (rc) return rc;
-  if (to_host && e->pyr_bytes) {
-    // the level buffer (levels >= 2; 0 and 1 are the staged image) comes
-    // back on the copy stream while FAST, the quadtree and BRIEF run
+  if (to_host) {
+    // the levels come back on the copy stream while FAST, the quadtree and
+    // BRIEF run: level 0 (= level 1) from the uploaded image, the level
+    // buffer (levels >= 2) once the pyramid kernel is done
     ORBX_TRY(hipStreamWaitEvent(e->s_copy, e->ev_pyr, 0));
-    ORBX_TRY(hipMemcpyAsync(e->h_pyr, p->d_pyr, e->pyr_bytes, hipMemcpyDeviceToHost, e->s_copy));
+    if (!(e->flags & ORBX_EXTRACTOR_PINNED_H2D))
+      ORBX_TRY(hipMemcpyAsync(e->h_img, e->d_img, (size_t)W * H, hipMemcpyDeviceToHost, e->s_copy));
+    if (e->pyr_bytes)
+      ORBX_TRY(hipMemcpyAsync(e->h_pyr, p->d_pyr, e->pyr_bytes, hipMemcpyDeviceToHost, e->s_copy));
   }
   // one round trip in the common case: the error word, the count and a
   // speculative prefix of the rows (sized by the previous call) come back
@@ -581,8 +590,8 @@ extern "C" int orbx_extract(orbx_extractor* e, const uint8_t* img, int W, int H,
   ORBX_TRY(hipMemcpyAsync(h_kps, e->d_kps, sizeof(orbx_keypoint) * (size_t)guess,
                           hipMemcpyDeviceToHost, s));
   ORBX_TRY(hipMemcpyAsync(h_desc, e->d_desc, 32 * (size_t)guess, hipMemcpyDeviceToHost, s));
-  ORBX_TRY(hipStreamSynchronize(s));
-  if (to_host && e->pyr_bytes) ORBX_TRY(hipStreamSynchronize(e->s_copy));
+  ORBX_TRY(stream_wait(s));
+  if (to_host) ORBX_TRY(stream_wait(e->s_copy));
   if (*p->h_err) {
     rc = orbx_plan_check(p, s); /* resets the device error word */
     e->have_frame = false;
@@ -600,7 +609,7 @@ extern "C" int orbx_extract(orbx_extractor* e, const uint8_t* img, int W, int H,
                             sizeof(orbx_keypoint) * (size_t)(K - guess), hipMemcpyDeviceToHost, s));
     ORBX_TRY(hipMemcpyAsync(h_desc + 32 * (size_t)guess, e->d_desc + 32 * (size_t)guess,
                             32 * (size_t)(K - guess), hipMemcpyDeviceToHost, s));
-    ORBX_TRY(hipStreamSynchronize(s));
+    ORBX_TRY(stream_wait(s));
   }
   e->last_k = K;
   memcpy(kps, h_kps, sizeof(orbx_keypoint) * (size_t)K);
@@ -609,7 +618,7 @@ extern "C" int orbx_extract(orbx_extractor* e, const uint8_t* img, int W, int H,
 }
 
 extern "C" int orbx_extractor_set_options(orbx_extractor* e, int flags) {
-  if (!e || (flags & ~(ORBX_EXTRACTOR_PYRAMID_TO_HOST | ORBX_EXTRACTOR_PAGEABLE_H2D))) return ORBX_ERR_ARG;
+  if (!e || (flags & ~(ORBX_EXTRACTOR_PYRAMID_TO_HOST | ORBX_EXTRACTOR_PINNED_H2D))) return ORBX_ERR_ARG;
   e->flags = flags;
   return ORBX_OK;
 }

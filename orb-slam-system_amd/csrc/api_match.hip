@@ -292,7 +292,7 @@ extern "C" int orbm_search_by_bow(const orbx_bow_frame* kf1, const orbx_bow_fram
                upper_bytes_zero(kf1->desc, kf1->n) && upper_bytes_zero(kf2->desc, kf2->n));
   if (hipGetLastError() != hipSuccess) return ORBX_ERR_HIP;
   ORBX_TRY(hipMemcpyAsync(h + in_end, d + in_end, out_end - in_end, hipMemcpyDeviceToHost, s));
-  ORBX_TRY(hipStreamSynchronize(s));
+  ORBX_TRY(stream_wait(s));
   memcpy(match12, h + o_m12, n1 * 4);
   memcpy(nmatches, h + o_nm, sizeof(int));
   return ORBX_OK;
@@ -332,7 +332,7 @@ extern "C" int orbm_descriptor_distance_batch(const uint8_t* a, int na, const ui
                      reinterpret_cast<int32_t*>(d + o_d));
   if (hipGetLastError() != hipSuccess) return ORBX_ERR_HIP;
   ORBX_TRY(hipMemcpyAsync(h + o_d, d + o_d, (size_t)npairs * 4, hipMemcpyDeviceToHost, s));
-  ORBX_TRY(hipStreamSynchronize(s));
+  ORBX_TRY(stream_wait(s));
   memcpy(dist, h + o_d, (size_t)npairs * 4);
   return ORBX_OK;
 }

@@ -54,7 +54,7 @@ extern "C" int orbm_compute_distinctive_descriptors(const uint8_t* desc, const i
   if (hipGetLastError() != hipSuccess) return ORBX_ERR_HIP;
   ORBX_TRY(hipMemcpyAsync(w->h + o_best, w->d + o_best, (size_t)nmp * 4, hipMemcpyDeviceToHost,
                           w->stream));
-  ORBX_TRY(hipStreamSynchronize(w->stream));
+  ORBX_TRY(stream_wait(w->stream));
   memcpy(best, w->h + o_best, (size_t)nmp * 4);
   return ORBX_OK;
 }
@@ -97,7 +97,7 @@ extern "C" int orbx_undistort_keypoints(const orbx_keypoint* kps, int n, const f
   if (hipGetLastError() != hipSuccess) return ORBX_ERR_HIP;
   ORBX_TRY(hipMemcpyAsync(w->h + o_out, w->d + o_out, (size_t)n * sizeof(orbx_keypoint),
                           hipMemcpyDeviceToHost, w->stream));
-  ORBX_TRY(hipStreamSynchronize(w->stream));
+  ORBX_TRY(stream_wait(w->stream));
   memcpy(out, w->h + o_out, (size_t)n * sizeof(orbx_keypoint));
   return ORBX_OK;
 }

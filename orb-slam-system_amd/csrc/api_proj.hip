@@ -101,7 +101,7 @@ extern "C" int orbm_search_by_projection(int mode, const orbx_proj_frame* F,
                      d_nc, d_match, d_nm);
   if (hipGetLastError() != hipSuccess) return ORBX_ERR_HIP;
   ORBX_TRY(hipMemcpyAsync(h + in_end, d + in_end, out_end - in_end, hipMemcpyDeviceToHost, s));
-  ORBX_TRY(hipStreamSynchronize(s));
+  ORBX_TRY(stream_wait(s));
   memcpy(match, h + o_match, (size_t)n * 4);
   memcpy(nmatches, h + o_nm, sizeof(int));
   return ORBX_OK;

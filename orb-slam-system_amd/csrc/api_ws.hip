@@ -2,6 +2,7 @@
 // for the synchronous drop-in entry points (api_common.h).
 #include <hip/hip_runtime.h>
 
+#include <chrono>
 #include <map>
 #include <mutex>
 #include <utility>
@@ -80,6 +81,19 @@ void ws_release(CallWs* w) {
   }
   std::lock_guard<std::mutex> g(g_pool_mu);
   (*g_pool)[w->device].push_back(w);
+}
+
+#ifndef ORBX_SPIN_US
+#define ORBX_SPIN_US 20000
+#endif
+hipError_t stream_wait(hipStream_t s) {
+  const auto t_end = std::chrono::steady_clock::now() + std::chrono::microseconds(ORBX_SPIN_US);
+  for (;;) {
+    const hipError_t q = hipStreamQuery(s);
+    if (q != hipErrorNotReady) return q;
+    if (std::chrono::steady_clock::now() >= t_end) return hipStreamSynchronize(s);
+    __builtin_ia32_pause();
+  }
 }
 
 int set_max_dynamic_lds(const void* kernel, int device) {

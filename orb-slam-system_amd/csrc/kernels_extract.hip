@@ -608,9 +608,11 @@ __device__ __forceinline__ void fs_strip_body(
       q.dn = *reinterpret_cast<const uint32_t*>(gb + 6 * tpitch + 4);
       return q;
     };
-    auto gtest = [&](const GroupWords& q, uint8_t* zp, uint32_t ebase, uint32_t ttl, bool zf) {
+    // the cardinal test of one group: clo / chi hold pixels 0, 2 / 1, 3 in
+    // 16-bit lanes, nonzero = survivor
+    auto gcore = [&](const GroupWords& q, uint8_t* zp, uint32_t ttl, bool zf, uint32_t& clo,
+                     uint32_t& chi) {
       const uint32_t w0 = q.w0, w1 = q.w1, w2 = q.w2, up = q.up, dn = q.dn;
-      uint32_t clo = 0, chi = 0;  // candidate words: pixels 0,2 / 1,3 (16-bit lanes)
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
         const uint32_t sel = h ? 0x0c030c01u : 0x0c020c00u;
@@ -633,6 +635,20 @@ __device__ __forceinline__ void fs_strip_body(
         if (h) chi = x; else clo = x;
       }
       if (zf) *reinterpret_cast<uint32_t*>(zp) = 0u;
+    };
+    auto l1_flush = [&]() {
+      if (n1 >= FS_L1FLUSH) {  // wave-uniform
+        wave_sync_lds();
+        while (n1 >= 64) {
+          n1 -= 64;
+          even_batch(L1[n1 + lane], true);
+        }
+        wave_sync_lds();
+      }
+    };
+    auto gtest = [&](const GroupWords& q, uint8_t* zp, uint32_t ebase, uint32_t ttl, bool zf) {
+      uint32_t clo, chi;
+      gcore(q, zp, ttl, zf, clo, chi);
       // append: the ballot is the compare's SGPR result, the lane's slot is
       // mbcnt of it from 0 at the uniform L1 + n1, only survivors store
       // (stores of every lane to a dummy slot measured 13 % slower).
@@ -664,14 +680,7 @@ __device__ __forceinline__ void fs_strip_body(
         n1 += __builtin_amdgcn_readfirstlane((int)(vv == 0xFFFFFFFEu));
       }
 #endif
-      if (n1 >= FS_L1FLUSH) {  // wave-uniform
-        wave_sync_lds();
-        while (n1 >= 64) {
-          n1 -= 64;
-          even_batch(L1[n1 + lane], true);
-        }
-        wave_sync_lds();
-      }
+      l1_flush();
     };
     auto group = [&](const uint8_t* gb, uint8_t* zp, uint32_t ebase, uint32_t ttl, bool zf) {
       gtest(gload(gb), zp, ebase, ttl, zf);

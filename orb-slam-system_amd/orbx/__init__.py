@@ -291,10 +291,10 @@ class Extractor:
         _check(_lib.orbx_extractor_level(self._h, l, _p(out), w.value, None, None))
         return out
 
-    def set_options(self, pyramid_to_host=False, pageable_h2d=False):
+    def set_options(self, pyramid_to_host=False, pinned_h2d=False):
         """ORBX_EXTRACTOR_* options (include/orbx.h)"""
         _check(_lib.orbx_extractor_set_options(self._h, (1 if pyramid_to_host else 0)
-                                               | (2 if pageable_h2d else 0)), "orbx_extractor_set_options")
+                                               | (2 if pinned_h2d else 0)), "orbx_extractor_set_options")
 
     def level_host(self, l):
         """copy of the host pyramid level the last extract() brought back

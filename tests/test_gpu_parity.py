@@ -51,13 +51,13 @@ def test_extract_matches_oracle(gpu, oracle, w, h, nf, L, guard, kind, idx):
                                            (642, 361, 1000, "strict")])
 def test_extractor_options_match_oracle(gpu, oracle, w, h, nf, guard):
     """ORBX_EXTRACTOR_PYRAMID_TO_HOST (the compat operator()'s mvImagePyramid,
-    brought back with the call) and the pageable-H2D upload give the same
+    brought back with the call) and the pinned-staging upload give the same
     keypoints / descriptors; the host levels equal the oracle's pyramid and
     follow the next call."""
     ref = oracle.Extractor(nf, 1.2, 8, 20, 7, cell_guard=guard)
     ex = gpu.Extractor(nf, 1.2, 8, 20, 7, cell_guard=guard)
-    for i, opts in enumerate(({"pyramid_to_host": True}, {"pyramid_to_host": True},
-                              {"pageable_h2d": True}, {})):
+    for i, opts in enumerate(({"pyramid_to_host": True}, {"pyramid_to_host": True, "pinned_h2d": True},
+                              {"pinned_h2d": True}, {})):
         img = synth.frame(w, h, 90 + i, "pan" if i % 2 else "noise")
         ex.set_options(**opts)
         k, d = ex.extract(img)
@@ -290,7 +290,7 @@ def test_match_plan_matches_oracle(gpu, oracle, W, H, nf, kind, first, opts):
         rm, rnm = oracle.search_by_bow(_topn_bow(ka, da, nf), _topn_bow(kb, db, nf), 0.75, True)
         assert nm[p] == rnm
         assert np.array_equal(m12[p, :len(ka)], rm)
-    if kind == "pan":
+    if kind == "pan" and not opts.get("tail"):
         assert int(nm[0]) >= 100, nm  # the resolver is exercised at real density
 
 
