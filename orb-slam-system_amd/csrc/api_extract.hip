@@ -19,10 +19,10 @@ __global__ void k_pyramid(const uint8_t*, size_t, size_t, uint8_t*, size_t, cons
                           const int4*, const int4*, const uint4*, const int*, int);
 __global__ void k_fast_strips(const uint8_t*, size_t, size_t, const uint8_t*, size_t,
                               const LevelArgs, const CellInfo*, const StripInfo*, uint32_t*,
-                              size_t, uint32_t*, int, int, int, int, int, int, int, int*, int);
+                              size_t, uint32_t*, int, int, int, int, int, int, int, int*, int, int);
 __global__ void k_fast_strips_p288(const uint8_t*, size_t, size_t, const uint8_t*, size_t,
                               const LevelArgs, const CellInfo*, const StripInfo*, uint32_t*,
-                              size_t, uint32_t*, int, int, int, int, int, int, int, int*, int);
+                              size_t, uint32_t*, int, int, int, int, int, int, int, int*, int, int);
 __global__ void k_quadtree(const LevelInfo*, const CellInfo*, const uint32_t*, size_t,
                            const uint32_t*, int, uint32_t*, int32_t*, size_t, uint32_t*, size_t,
                            int*, int, int, int, int*);
@@ -135,6 +135,9 @@ static void plan_free(orbx_plan* p) {
   p->timer.release();
   if (p->h_err) hipHostFree(p->h_err);
   if (p->stream) hipStreamDestroy(p->stream);
+  if (p->s_aux) hipStreamDestroy(p->s_aux);
+  if (p->ev_aux0) hipEventDestroy(p->ev_aux0);
+  if (p->ev_aux1) hipEventDestroy(p->ev_aux1);
   delete p;
 }
 
@@ -164,6 +167,7 @@ extern "C" int orbx_plan_create(const orbx_params* prm, int width, int height, i
   if (const char* e = getenv("ORBX_DEBUG_STOP")) p->dbg = atoi(e);
   if (const char* e = getenv("ORBX_DEBUG_OBDIV")) p->ob_div = atoi(e);
   if (const char* e = getenv("ORBX_CHUNK")) p->chunk = atoi(e);
+  if (const char* e = getenv("ORBX_DEBUG_OVERLAP")) p->overlap = atoi(e); /* profiling: FAST level 0 beside the pyramid */
   p->fs_ccap = FS_CCAP;
   /* testing only: a smaller FAST corner list, so the overflow path runs */
   if (const char* e = getenv("ORBX_DEBUG_CCAP")) p->fs_ccap = std::max(0, std::min(FS_CCAP, atoi(e)));
@@ -181,6 +185,12 @@ extern "C" int orbx_plan_create(const orbx_params* prm, int width, int height, i
       set_max_dynamic_lds((const void*)k_fast_strips, device) ||
       set_max_dynamic_lds((const void*)k_fast_strips_p288, device) ||
       set_max_dynamic_lds((const void*)k_pyramid, device)) { plan_free(p); return ORBX_ERR_HIP; }
+  if (p->overlap && (hipStreamCreateWithFlags(&p->s_aux, hipStreamNonBlocking) != hipSuccess ||
+                     hipEventCreateWithFlags(&p->ev_aux0, hipEventDisableTiming) != hipSuccess ||
+                     hipEventCreateWithFlags(&p->ev_aux1, hipEventDisableTiming) != hipSuccess)) {
+    plan_free(p);
+    return ORBX_ERR_HIP;
+  }
   if (hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking) != hipSuccess ||
       hipHostMalloc((void**)&p->h_err, 64, hipHostMallocDefault) != hipSuccess) { plan_free(p); return ORBX_ERR_HIP; }
   memset(&p->bargs, 0, sizeof(p->bargs));
@@ -299,6 +309,24 @@ static int extract_pass(orbx_plan* p, const uint8_t* frames, int n, size_t fstri
   int32_t* const d_qnode = p->d_qnode + f0 * p->qk_stride;
   uint32_t* const d_qout = p->d_qout + f0 * p->qout_stride;
   int* const d_lcount = p->d_lcount + f0 * (size_t)L;
+  auto fast_launch = [&](int strip0, int nstrips, hipStream_t st) {
+    if (nstrips <= 0) return;
+    hipLaunchKernelGGL(p->fs_tpitch == 288 ? k_fast_strips_p288 : k_fast_strips, dim3((unsigned)nstrips, n), dim3(FS_NT), p->fs_lds, st,
+                       frames, fstride, rstride, d_pyr, p->pyr_stride, p->largs, p->d_cells,
+                       p->d_strips, d_slots, p->slot_stride, d_ccount, P.ncells, P.ini_th,
+                       P.min_th, p->fs_tpitch, p->fs_tmaxh, p->fs_mcells, p->fs_ccap,
+                       p->d_err + ORBX_ERRW_FAST_OVF, strip0, p->dbg);
+  };
+  const int nstrips = (int)P.strips.size();
+  const bool overlap = p->overlap && p->s_aux && P.nstrips_l0 > 0;
+  if (overlap) {
+    // FAST on level 0 (which needs no pyramid) runs on the auxiliary stream
+    // beside the pyramid kernel; the other levels' strips follow the pyramid
+    if (hipEventRecord(p->ev_aux0, s) != hipSuccess || hipStreamWaitEvent(p->s_aux, p->ev_aux0, 0) != hipSuccess)
+      return ORBX_ERR_HIP;
+    fast_launch(0, P.nstrips_l0, p->s_aux);
+    if (hipEventRecord(p->ev_aux1, p->s_aux) != hipSuccess) return ORBX_ERR_HIP;
+  }
   // K1 pyramid
   p->timer.begin(ORBX_STAGE_RESIZE, s);
   for (const PyrSeg& g : P.segs) {
@@ -312,12 +340,11 @@ static int extract_pass(orbx_plan* p, const uint8_t* frames, int n, size_t fstri
   if (p->ev_after_pyr && hipEventRecord(p->ev_after_pyr, s) != hipSuccess) return ORBX_ERR_HIP;
   // K2 FAST cells
   p->timer.begin(ORBX_STAGE_FAST, s);
-  if (!P.strips.empty()) {
-    hipLaunchKernelGGL(p->fs_tpitch == 288 ? k_fast_strips_p288 : k_fast_strips, dim3((unsigned)P.strips.size(), n), dim3(FS_NT), p->fs_lds, s,
-                       frames, fstride, rstride, d_pyr, p->pyr_stride, p->largs, p->d_cells,
-                       p->d_strips, d_slots, p->slot_stride, d_ccount, P.ncells, P.ini_th,
-                       P.min_th, p->fs_tpitch, p->fs_tmaxh, p->fs_mcells, p->fs_ccap,
-                       p->d_err + ORBX_ERRW_FAST_OVF, p->dbg);
+  if (overlap) {
+    fast_launch(P.nstrips_l0, nstrips - P.nstrips_l0, s);
+    if (hipStreamWaitEvent(s, p->ev_aux1, 0) != hipSuccess) return ORBX_ERR_HIP;
+  } else {
+    fast_launch(0, nstrips, s);
   }
   p->timer.end(ORBX_STAGE_FAST, s);
   if (p->dbg && p->dbg < 20) return ORBX_OK; /* phase probe: later stages would read partial results */

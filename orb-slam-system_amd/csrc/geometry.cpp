@@ -362,6 +362,7 @@ int plan_geometry(const orbx_params& p, int width, int height, Plan& P) {
   P.cells.clear();
   P.strips.clear();
   P.strip_max_w = P.strip_max_h = P.strip_max_cells = 0;
+  P.nstrips_l0 = 0;
   P.xofs.clear(); P.xofs1.clear(); P.alpha.clear(); P.yofs.clear(); P.beta.clear();
   memset(&P.geo, 0, sizeof(P.geo));
   P.geo.nlevels = L;
@@ -491,6 +492,8 @@ int plan_geometry(const orbx_params& p, int width, int height, Plan& P) {
   }
   P.nslots = slots;
   P.ncells = (int)P.cells.size();
+  P.nstrips_l0 = 0;
+  while (P.nstrips_l0 < (int)P.strips.size() && P.strips[P.nstrips_l0].level == 0) ++P.nstrips_l0;
   int bt = 0;
   for (int l = 0; l < L; ++l) {
     LevelInfo& lv = P.levels[l];

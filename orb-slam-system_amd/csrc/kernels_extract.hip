@@ -862,7 +862,7 @@ __device__ __forceinline__ void fs_kernel(
     const CellInfo* __restrict__ cells, const StripInfo* __restrict__ strips,
     uint32_t* __restrict__ slots, size_t slot_stride, uint32_t* __restrict__ ccount, int ncells,
     int ini_th, int min_th, int tpitch_rt, int tmax_h, int mcells, int ccap, int* __restrict__ ovf,
-    int dbg) {
+    int strip0, int dbg) {
   const int tpitch = TP ? TP : tpitch_rt;
   // LDS (occupancy is LDS-bound and the kernel is latency-bound: +12 KB per
   // workgroup measured +38 % time): tile | strength map of the band rows only
@@ -889,8 +889,9 @@ __device__ __forceinline__ void fs_kernel(
 #ifdef FS_FRAME_UNIT  // profiling variant: every strip of frame f on XCD f % 8
   int sx, f;
   frame_unit(sx, f);
+  sx += strip0;
 #else
-  const int sx = blockIdx.x, f = blockIdx.y;
+  const int sx = blockIdx.x + strip0, f = blockIdx.y;
 #endif
   const StripInfo st = strips[sx];
   const int pitch = st.level == 0 ? (int)rstride : LA.pitch[st.level];
@@ -924,9 +925,9 @@ __device__ __forceinline__ void fs_kernel(
       size_t pstride, const LevelArgs LA, const CellInfo *__restrict__ cells,                       \
       const StripInfo *__restrict__ strips, uint32_t *__restrict__ slots, size_t slot_stride,      \
       uint32_t *__restrict__ ccount, int ncells, int ini_th, int min_th, int tpitch, int tmax_h,   \
-      int mcells, int ccap, int *__restrict__ ovf, int dbg
+      int mcells, int ccap, int *__restrict__ ovf, int strip0, int dbg
 #define FS_KERNEL_PASS \
-  frames, fstride, rstride, pyr, pstride, LA, cells, strips, slots, slot_stride, ccount, ncells, ini_th, min_th, tpitch, tmax_h, mcells, ccap, ovf, dbg
+  frames, fstride, rstride, pyr, pstride, LA, cells, strips, slots, slot_stride, ccount, ncells, ini_th, min_th, tpitch, tmax_h, mcells, ccap, ovf, strip0, dbg
 
 #ifdef FS_WPE  // profiling variant: occupancy target
 #define FS_ATTR __attribute__((amdgpu_waves_per_eu(FS_WPE)))

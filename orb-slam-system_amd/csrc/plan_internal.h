@@ -38,6 +38,9 @@ struct orbx_plan {
   int fs_ccap = 0; /* FAST per-strip corner list entries used (FS_CCAP; ORBX_DEBUG_CCAP lowers it) */
   int chunk = 0;  /* frames per extraction pass (0 = the whole batch in one pass) */
   hipEvent_t ev_after_pyr = nullptr; /* recorded after the pyramid launch when set (orbx_extract) */
+  int overlap = 0; /* FAST on level 0 beside the pyramid on s_aux */
+  hipStream_t s_aux = nullptr;
+  hipEvent_t ev_aux0 = nullptr, ev_aux1 = nullptr;
 };
 
 struct orbx_extractor {
