@@ -25,13 +25,13 @@ __global__ void k_fast_strips_p288(const uint8_t*, size_t, size_t, const uint8_t
                               size_t, uint32_t*, int, int, int, int, int, int, int, int*, int, int);
 __global__ void k_quadtree(const LevelInfo*, const CellInfo*, const uint32_t*, size_t,
                            const uint32_t*, int, uint32_t*, int32_t*, size_t, uint32_t*, size_t,
-                           int*, int, int, int, int*);
+                           int*, int, int, int, int*, uint32_t*);
 __global__ void k_quadtree_j6(const LevelInfo*, const CellInfo*, const uint32_t*, size_t,
                               const uint32_t*, int, uint32_t*, int32_t*, size_t, uint32_t*, size_t,
-                              int*, int, int, int, int*);
+                              int*, int, int, int, int*, uint32_t*);
 __global__ void k_orient_brief(const uint8_t*, size_t, size_t, const uint8_t*, size_t,
                                const BriefArgs, const uint32_t*, size_t, const int*,
-                               orbx_keypoint*, uint8_t*, int*, int);
+                               orbx_keypoint*, uint8_t*, int*, const uint32_t*, int);
 __global__ void k_synth(uint8_t*, int, int, size_t, int, int);
 __global__ void k_selftest_sincos(const float*, int, float*);
 __global__ void k_selftest_sincos_range(uint32_t, int, float*);
@@ -128,7 +128,7 @@ static void plan_free(orbx_plan* p) {
   if (!p) return;
   hipSetDevice(p->device);
   void* bufs[] = {p->d_lv, p->d_cells, p->d_strips, p->d_xofs, p->d_xofs1, p->d_yofs, p->d_alpha, p->d_beta,
-                  p->d_pyr, p->d_blur, p->d_slots, p->d_ccount, p->d_qkeys, p->d_qout,
+                  p->d_pyr, p->d_blur, p->d_slots, p->d_ccount, p->d_qkeys, p->d_qout, p->d_qperm,
                   p->d_qnode, p->d_lcount, p->d_err, p->d_pyr_xs, p->d_pyr_ys, p->d_pyr_bo, p->d_pyr_blob};
   for (void* b : bufs)
     if (b) hipFree(b);
@@ -259,6 +259,7 @@ extern "C" int orbx_plan_create(const orbx_params* prm, int width, int height, i
       dev_alloc((void**)&p->d_qkeys, B * p->qk_stride * 4) ||
       dev_alloc((void**)&p->d_qnode, B * p->qk_stride * 4) ||
       dev_alloc((void**)&p->d_qout, B * p->qout_stride * 4) ||
+      dev_alloc((void**)&p->d_qperm, B * p->qout_stride * 4) ||
       dev_alloc((void**)&p->d_lcount, B * (size_t)P.params.nlevels * 4) ||
       dev_alloc((void**)&p->d_err, 16)) {
     plan_free(p);
@@ -355,7 +356,7 @@ static int extract_pass(orbx_plan* p, const uint8_t* frames, int n, size_t fstri
                      dim3(256), p->qt_lds, s, p->d_lv, p->d_cells,
                      d_slots, p->slot_stride, d_ccount, P.ncells, d_qkeys, d_qnode,
                      p->qk_stride, d_qout, p->qout_stride, d_lcount, L, P.qt_smax,
-                     P.qt_max_cells, p->d_err);
+                     P.qt_max_cells, p->d_err, p->d_qperm + f0 * p->qout_stride);
   p->timer.end(ORBX_STAGE_QUADTREE, s);
   // K4+K5+K6+K7 orientation, blur-at-sample descriptors, assembly
   p->timer.begin(ORBX_STAGE_BRIEF, s);
@@ -371,7 +372,7 @@ static int extract_pass(orbx_plan* p, const uint8_t* frames, int n, size_t fstri
   hipLaunchKernelGGL(k_orient_brief, dim3((ob_waves + 3) / 4, n),
                      dim3(256), 0, s, frames, fstride, rstride, d_pyr, p->pyr_stride, p->bargs,
                      d_qout, p->qout_stride, d_lcount, kps, desc,
-                     counts, p->dbg);
+                     counts, p->d_qperm + f0 * p->qout_stride, p->dbg);
   p->timer.end(ORBX_STAGE_BRIEF, s);
   if (hipGetLastError() != hipSuccess) return ORBX_ERR_HIP;
   return ORBX_OK;

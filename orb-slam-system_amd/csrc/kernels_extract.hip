@@ -1005,9 +1005,9 @@ __device__ __forceinline__ int upper_bound_i(const int* a, int n, int v) {
       const uint32_t *__restrict__ ccount, int ncells_total, uint32_t *__restrict__ qkeys, \
       int32_t *__restrict__ qnode, size_t qk_stride, uint32_t *__restrict__ qout,          \
       size_t qout_stride, int *__restrict__ lcount, int nlevels, int smax, int maxcells,   \
-      int *__restrict__ err
+      int *__restrict__ err, uint32_t *__restrict__ qperm
 #define QT_KERNEL_PASS \
-  lv, cells, slots, slot_stride, ccount, ncells_total, qkeys, qnode, qk_stride, qout, qout_stride, lcount, nlevels, smax, maxcells, err
+  lv, cells, slots, slot_stride, ccount, ncells_total, qkeys, qnode, qk_stride, qout, qout_stride, lcount, nlevels, smax, maxcells, err, qperm
 
 // QJ: keys per thread held in registers (256 QJ per level; more spill to the
 // global keys/node arrays).  Both instantiations are built for 8 waves per
@@ -1207,6 +1207,38 @@ __device__ __forceinline__ void qt_body(QT_KERNEL_ARGS) {
     const uint32_t k = 0xFFFFFFu - (best[i] & 0xFFFFFFu);
     out[i] = keys[k];
   }
+  // k_orient_brief's processing order: the winners by key index.  Keys are
+  // cell-major (cell rows top to bottom, raster within a cell), so the
+  // keypoints BRIEF works on at the same time lie in the same band of rows
+  // and their patches share 128-B lines in L2 (the output order -- node
+  // order, the reference's -- is unchanged).  rank = winners with a smaller
+  // key index: a bitmap over the key indices and a scan of its popcounts.
+  uint32_t* perm = qperm + (size_t)f * qout_stride + L.kout_off;
+  const int nw = (C + 31) >> 5;
+#ifdef OB_NO_PERM  // profiling variant: BRIEF in output order
+  if (false) {
+#else
+  if (nw <= 3 * smax) {  // rx / ry / cnt hold the counts, nrx.. the bitmap (dead node arrays)
+#endif
+    uint32_t* bm = reinterpret_cast<uint32_t*>(nrx);
+    int* pc = rx;
+    for (int w = tid; w < nw; w += 256) bm[w] = 0u;
+    __syncthreads();
+    for (int i = tid; i < newS; i += 256) {
+      const uint32_t k = 0xFFFFFFu - (best[i] & 0xFFFFFFu);
+      atomicOr(&bm[k >> 5], 1u << (k & 31));
+    }
+    __syncthreads();
+    for (int w = tid; w < nw; w += 256) pc[w] = __popc(bm[w]);
+    __syncthreads();
+    block_scan_excl(pc, nw, wtmp);
+    for (int i = tid; i < newS; i += 256) {
+      const uint32_t k = 0xFFFFFFu - (best[i] & 0xFFFFFFu);
+      perm[pc[k >> 5] + __popc(bm[k >> 5] & ((1u << (k & 31)) - 1u))] = (uint32_t)i;
+    }
+  } else {
+    for (int i = tid; i < newS; i += 256) perm[i] = (uint32_t)i;
+  }
   if (tid == 0) lcount[(size_t)f * nlevels + l] = newS;
 }
 
@@ -1319,6 +1351,7 @@ __device__ constexpr uint32_t kb_w(int m, int d) {
 // One keypoint of the frame's level-major output list: where its level
 // lives and where its patch starts (all wave-uniform).
 struct BriefKp {
+  int oi;  // output position (levels concatenated, node order within a level)
   int l, x, y, score, patch_size;
   float scale;
   const uint8_t* img;
@@ -1393,7 +1426,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OB_WPE))) v
     const uint8_t* __restrict__ pyr, size_t pstride, const BriefArgs A,
     const uint32_t* __restrict__ qout, size_t qout_stride, const int* __restrict__ lcount,
     orbx_keypoint* __restrict__ kps, uint8_t* __restrict__ desc, int* __restrict__ counts,
-    int dbg) {
+    const uint32_t* __restrict__ qperm, int dbg) {
   __shared__ uint32_t patch[4][KP_ROWS][KP_PSTRIDE];
   // horizontally blurred patch, column-major: hblur[w][patch col][row pair]
   // = (H(row 2k), H(row 2k+1)) as u16 pair, H = sum_i k_i p (7 taps)
@@ -1410,6 +1443,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OB_WPE))) v
   if (bx == 0 && threadIdx.x == 0) counts[f] = total;
   const int excl = incl - lcv;
   const uint32_t* Q = qout + (size_t)f * qout_stride;
+  const uint32_t* QP = qperm + (size_t)f * qout_stride;
   uint32_t(*P)[KP_PSTRIDE] = patch[wave];
   // sincos exception keys, entries lane and lane + 64 (brief_sincos)
   const uint32_t exk0 = ORBX_SINCOS_EXC[lane < ORBX_SINCOS_NEXC ? lane : 0][0];
@@ -1433,9 +1467,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OB_WPE))) v
   // keypoint's patch (vmcnt stays exact; nothing waits on it early).
   auto locate = [&](int o) {
     const int l = __builtin_amdgcn_readfirstlane(__popcll(__ballot(lane < nlevels && incl <= o)));
-    const int i = o - __builtin_amdgcn_readlane(excl, l);  // l is uniform
+    const int e = __builtin_amdgcn_readlane(excl, l);  // l is uniform
+    // position o of the processing order (qperm, k_quadtree) -> winner i of
+    // level l, written at output position e + i
+    const int i = (int)__builtin_amdgcn_readfirstlane(QP[A.kout_off[l] + (o - e)]);
     const uint32_t key = __builtin_amdgcn_readfirstlane(Q[A.kout_off[l] + i]);
     BriefKp k;
+    k.oi = e + i;
     k.l = l;
     k.x = (int)(key >> 20) + ORBX_MINB;
     k.y = (int)((key >> 8) & 0xFFF) + ORBX_MINB;
@@ -1584,7 +1622,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OB_WPE))) v
   }
   if (lane < 4) {
     const uint64_t w = lane == 0 ? words[0] : lane == 1 ? words[1] : lane == 2 ? words[2] : words[3];
-    reinterpret_cast<uint64_t*>(desc + ((size_t)f * kcap + o) * 32)[lane] = w;
+    reinterpret_cast<uint64_t*>(desc + ((size_t)f * kcap + me.oi) * 32)[lane] = w;
   }
   if (lane == 0) {
     orbx_keypoint kp;
@@ -1599,7 +1637,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OB_WPE))) v
     kp.response = (float)score;
     kp.octave = l;
     kp.class_id = -1;
-    kps[(size_t)f * kcap + o] = kp;
+    kps[(size_t)f * kcap + me.oi] = kp;
   }
   }
 }

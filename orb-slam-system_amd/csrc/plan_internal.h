@@ -25,6 +25,7 @@ struct orbx_plan {
   int16_t *d_alpha = nullptr, *d_beta = nullptr;
   uint8_t *d_pyr = nullptr, *d_blur = nullptr;
   uint32_t *d_slots = nullptr, *d_ccount = nullptr, *d_qkeys = nullptr, *d_qout = nullptr;
+  uint32_t* d_qperm = nullptr; /* per level: k_orient_brief's processing order (k_quadtree) */
   int32_t* d_qnode = nullptr;
   int *d_lcount = nullptr, *d_err = nullptr;
   int* h_err = nullptr; /* pinned: orbx_plan_check reads the error word without a blocking copy */

@@ -1,0 +1,40 @@
+// pyr_census -- computed vs owned pixels of the fused pyramid tiling
+// (geometry.cpp plan_pyramid), per level: how much of k_pyramid's arithmetic
+// is halo recompute.  Host-only, profiling tool:
+//   g++ -O2 -std=c++17 -Iorb-slam-system_amd/csrc -Iinclude tools/pyr_census.cpp \
+//       orb-slam-system_amd/csrc/geometry.cpp -o /tmp/pyr_census && /tmp/pyr_census 1920 1080
+#include <stdio.h>
+#include <stdlib.h>
+
+#include "geometry.h"
+
+using namespace orbx;
+
+int main(int argc, char** argv) {
+  const int W = argc > 1 ? atoi(argv[1]) : 1920, H = argc > 2 ? atoi(argv[2]) : 1080;
+  orbx_params p = {2000, 1.2f, 8, 20, 7, 1};
+  Plan P;
+  if (int rc = plan_geometry(p, W, H, P)) {
+    printf("plan_geometry: %d\n", rc);
+    return 1;
+  }
+  for (const PyrSeg& g : P.segs) {
+    long long comp = 0, own = 0;
+    printf("segment: %d levels, %d x %d tiles, LDS %d + %d B\n", g.nl, g.ntx, g.nty, g.lds_a, g.lds_b);
+    for (int s = 0; s <= g.nl; ++s) {
+      long long c = 0, o = 0;
+      for (int tx = 0; tx < g.ntx; ++tx)
+        for (int ty = 0; ty < g.nty; ++ty) {
+          const int* X = &P.pyr_xs[4 * (g.xs_off + s * g.ntx + tx)];
+          const int* Y = &P.pyr_ys[4 * (g.ys_off + s * g.nty + ty)];
+          c += (long long)(X[1] - X[0]) * (Y[1] - Y[0]);
+          o += (long long)(X[3] - X[2]) * (Y[3] - Y[2]);
+        }
+      printf("  level %d (%dx%d): %s %lld, owned %lld\n", g.lev[s], g.w[s], g.h[s],
+             s ? "computed" : "staged", c, o);
+      if (s) { comp += c; own += o; }
+    }
+    printf("  computed / owned = %.3f\n", own ? (double)comp / own : 0.0);
+  }
+  return 0;
+}
