@@ -50,6 +50,7 @@ def lib():
         L.oo_fast_atan2.argtypes = [f, f]
         L.oo_fast_detect.argtypes = [P, i, i, i, i, i, P, i]
         L.oo_resize_linear.argtypes = [P, i, i, i, P, i, i, i]
+        L.oo_resize_area2.argtypes = [P, i, i, i, P, i, i, i]
         L.oo_gaussian_blur7.argtypes = [P, i, i, i, P, i]
         L.oo_gaussian_kernel7.argtypes = [P]
         L.oo_brief_descriptor.argtypes = [P, i, i, i, f, P]
@@ -157,6 +158,16 @@ def resize_linear(src, dw, dh):
     sh, sw = src.shape
     dst = np.zeros((dh, dw), np.uint8)
     lib().oo_resize_linear(_p(src), sw, sh, sw, _p(dst), dw, dh, dw)
+    return dst
+
+
+def resize_area2(src):
+    """cv::resize to exactly half size (the INTER_AREA fast path)"""
+    src = np.ascontiguousarray(src, dtype=np.uint8)
+    sh, sw = src.shape
+    dh, dw = sh // 2, sw // 2
+    dst = np.zeros((dh, dw), np.uint8)
+    lib().oo_resize_area2(_p(src), sw, sh, sw, _p(dst), dw, dh, dw)
     return dst
 
 

@@ -190,6 +190,25 @@ void oo_resize_linear(const uint8_t* src, int sw, int sh, int sstride, uint8_t* 
   free(xofs); free(ialpha); free(yofs); free(ibeta); free(rows0); free(rows1);
 }
 
+/* ---------- cv::resize, exact 2x downscale (OpenCV 3.4 INTER_AREA fast path) --
+ * resize() switches INTER_LINEAR to INTER_AREA when both scale factors are
+ * exactly 2 (resize_is_area_fast2), and resizeAreaFast_'s 2x2 vector op
+ * ResizeAreaFastVec<uchar> -- its SIMD part and its scalar remainder alike
+ * -- writes (S[2x] + S[2x+1] + S'[2x] + S'[2x+1] + 2) >> 2 for every
+ * destination pixel of a full 2x2 block; with sw = 2 dw and sh = 2 dh there
+ * are no partial blocks. */
+void oo_resize_area2(const uint8_t* src, int sw, int sh, int sstride, uint8_t* dst, int dw, int dh,
+                     int dstride) {
+  (void)sw;
+  (void)sh;
+  for (int y = 0; y < dh; ++y) {
+    const uint8_t* a = src + (size_t)(2 * y) * sstride;
+    const uint8_t* b = a + sstride;
+    uint8_t* o = dst + (size_t)y * dstride;
+    for (int x = 0; x < dw; ++x) o[x] = (uint8_t)((a[2 * x] + a[2 * x + 1] + b[2 * x] + b[2 * x + 1] + 2) >> 2);
+  }
+}
+
 /* ---------- cv::FAST (OpenCV 3.4 FAST_t<16>, scalar path) ------------------ */
 static void make_offsets16(int pixel[25], int step) {
   static const int offsets16[16][2] = {{0, 3},  {1, 3},   {2, 2},   {3, 1},   {3, 0},  {3, -1},
@@ -673,8 +692,10 @@ static int compute_pyramid(oo_extractor* e, const uint8_t* img, int w, int h, in
       for (int y = 0; y < h; ++y) memcpy(e->lev[0] + (size_t)y * w, img + (size_t)y * stride, w);
     } else {
       int pw = e->lw[level - 1], ph = e->lh[level - 1];
-      if (!(pw == sw && ph == sh) && resize_is_area_fast2(pw, ph, sw, sh)) return OO_ERR_UNSUPPORTED;
-      oo_resize_linear(e->lev[level - 1], pw, ph, pw, e->lev[level], sw, sh, sw);
+      if (!(pw == sw && ph == sh) && resize_is_area_fast2(pw, ph, sw, sh))
+        oo_resize_area2(e->lev[level - 1], pw, ph, pw, e->lev[level], sw, sh, sw);
+      else
+        oo_resize_linear(e->lev[level - 1], pw, ph, pw, e->lev[level], sw, sh, sw);
     }
   }
   return OO_OK;

@@ -74,6 +74,10 @@ int oo_fast_detect(const uint8_t* img, int w, int h, int stride, int threshold, 
                    oo_keypoint* out, int cap);
 void oo_resize_linear(const uint8_t* src, int sw, int sh, int sstride, uint8_t* dst, int dw,
                       int dh, int dstride);
+/* exact 2x downscale: OpenCV's INTER_AREA fast path that resize(INTER_LINEAR)
+ * switches to when both ratios are exactly 2 */
+void oo_resize_area2(const uint8_t* src, int sw, int sh, int sstride, uint8_t* dst, int dw, int dh,
+                     int dstride);
 void oo_gaussian_blur7(const uint8_t* src, int w, int h, int stride, uint8_t* dst, int dstride);
 void oo_gaussian_kernel7(int raw[7]);
 void oo_brief_descriptor(const uint8_t* blurred, int stride, int cx, int cy, float angle_deg,

@@ -17,6 +17,7 @@
 namespace orbx {
 __global__ void k_pyramid(const uint8_t*, size_t, size_t, uint8_t*, size_t, const PyrSeg,
                           const int4*, const int4*, const uint4*, const int*, int);
+__global__ void k_pyr_area2(const uint8_t*, size_t, size_t, uint8_t*, size_t, const PyrSeg);
 __global__ void k_fast_strips(const uint8_t*, size_t, size_t, const uint8_t*, size_t,
                               const LevelArgs, const CellInfo*, const StripInfo*, uint32_t*,
                               size_t, uint32_t*, int, int, int, int, int, int, int, int*, int, int);
@@ -331,6 +332,11 @@ static int extract_pass(orbx_plan* p, const uint8_t* frames, int n, size_t fstri
   // K1 pyramid
   p->timer.begin(ORBX_STAGE_RESIZE, s);
   for (const PyrSeg& g : P.segs) {
+    if (g.area) {
+      hipLaunchKernelGGL(k_pyr_area2, dim3((unsigned)((g.w[1] + 1023) / 1024), (unsigned)g.h[1], (unsigned)n),
+                         dim3(256), 0, s, frames, fstride, rstride, d_pyr, p->pyr_stride, g);
+      continue;
+    }
     hipLaunchKernelGGL(k_pyramid, dim3(g.ntx * g.nty, n), dim3(256),
                        g.lds_a + g.lds_b + g.lds_yl, s, frames, fstride, rstride,
                        d_pyr, p->pyr_stride, g, reinterpret_cast<const int4*>(p->d_pyr_xs),

@@ -325,8 +325,27 @@ static int plan_pyramid(Plan& P) {
   if (const char* e = getenv("ORBX_DEBUG_PYR_MAXSEG")) maxseg = (size_t)std::max(atoi(e), 2);
   size_t i = 1;
   while (i < uniq.size()) {
+    if (P.area2[uniq[i]]) {  /* exact 2x: its own launch of k_pyr_area2 */
+      PyrSeg g;
+      memset(&g, 0, sizeof(g));
+      g.nl = 1;
+      g.area = 1;
+      for (int s = 0; s < 2; ++s) {
+        const LevelInfo& lv = P.levels[uniq[i - 1 + s]];
+        g.lev[s] = uniq[i - 1 + s];
+        g.w[s] = lv.w;
+        g.h[s] = lv.h;
+        g.pitch[s] = lv.pitch;
+        g.off[s] = g.lev[s] == 0 ? -1 : lv.pyr_off;
+      }
+      P.segs.push_back(g);
+      ++i;
+      continue;
+    }
+    size_t lim = i; /* the linear chain stops before the next 2x level */
+    while (lim < uniq.size() && !P.area2[uniq[lim]]) ++lim;
     bool done = false;
-    for (size_t j = std::min(uniq.size(), i - 1 + maxseg); j > i && !done; --j) {
+    for (size_t j = std::min(lim, i - 1 + maxseg); j > i && !done; --j) {
       std::vector<int> lev(uniq.begin() + (i - 1), uniq.begin() + j);
       const int ntile = (j == i + 1) ? 9 : 6;
       for (int k = std::min(k0, ntile - 1); k < ntile && !done; ++k) {
@@ -359,6 +378,7 @@ int plan_geometry(const orbx_params& p, int width, int height, Plan& P) {
   P.min_th = std::min(std::max(p.min_th_fast, 0), 255);
   const int L = p.nlevels;
   P.levels.assign(L, LevelInfo());
+  P.area2.assign(L, 0);
   P.cells.clear();
   P.strips.clear();
   P.strip_max_w = P.strip_max_h = P.strip_max_cells = 0;
@@ -380,8 +400,8 @@ int plan_geometry(const orbx_params& p, int width, int height, Plan& P) {
       lv.unique = P.levels[l - 1].unique; /* cv::resize: dsize == ssize -> copyTo */
     } else {
       lv.unique = l;
-      if (l > 0 && area_fast_2x(P.levels[l - 1].w, P.levels[l - 1].h, lv.w, lv.h))
-        return ORBX_ERR_UNSUPPORTED; /* OpenCV would switch to INTER_AREA */
+      /* cv::resize switches to its INTER_AREA fast path for exact 2x ratios */
+      if (l > 0 && area_fast_2x(P.levels[l - 1].w, P.levels[l - 1].h, lv.w, lv.h)) P.area2[l] = 1;
     }
     if (lv.unique == l) {
       lv.pitch = (l == 0) ? 0 /* caller's row stride */ : pitch_of(lv.w);

@@ -34,6 +34,7 @@ struct Plan {
   std::vector<StripInfo> strips;
   int strip_max_w = 0, strip_max_h = 0, strip_max_cells = 0;
   int nstrips_l0 = 0;  /* strips of level 0 (strips are level-major) */
+  std::vector<char> area2; /* per level: resized from the previous one by OpenCV's 2x INTER_AREA path */
   int blur_tiles = 0;
   std::vector<int32_t> xofs;   /* concatenated per unique level >= 1 */
   std::vector<int16_t> alpha;  /* 2 per x */

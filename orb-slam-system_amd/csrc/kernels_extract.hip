@@ -336,6 +336,45 @@ __global__ __launch_bounds__(256) void k_pyramid(const uint8_t* __restrict__ fra
 }
 
 // ---------------------------------------------------------------------------
+// k_pyr_area2: one exact-2x level (cv::resize's INTER_AREA fast path, which
+// resize(INTER_LINEAR) takes when both ratios are exactly 2: OpenCV 3.4
+// resizeAreaFast_ with ResizeAreaFastVec, SIMD part and scalar remainder
+// both (S[2x] + S[2x+1] + S'[2x] + S'[2x+1] + 2) >> 2).  Thread = 4
+// destination pixels of a row (a dword: level pitches are 16-B multiples);
+// grid (row groups, rows, frames).  Only for scale factors of exactly 2,
+// outside every benchmark configuration.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_pyr_area2(const uint8_t* __restrict__ frames, size_t fstride,
+                                                   size_t rstride, uint8_t* __restrict__ pyr,
+                                                   size_t pstride, const PyrSeg S) {
+  const int f = blockIdx.z, y = blockIdx.y;
+  const int x4 = (blockIdx.x * 256 + threadIdx.x) * 4;
+  const int dw = S.w[1];
+  if (x4 >= dw) return;
+  const uint8_t* src;
+  size_t sp;
+  if (S.off[0] < 0) {
+    src = frames + (size_t)f * fstride;
+    sp = rstride;
+  } else {
+    src = pyr + (size_t)f * pstride + S.off[0];
+    sp = (size_t)S.pitch[0];
+  }
+  const uint8_t* a = src + (size_t)(2 * y) * sp + 2 * x4;
+  const uint8_t* b = a + sp;
+  const int n = min(4, dw - x4);
+  uint32_t w = 0;
+  for (int k = 0; k < n; ++k)
+    w |= (uint32_t)((a[2 * k] + a[2 * k + 1] + b[2 * k] + b[2 * k + 1] + 2) >> 2) << (8 * k);
+  uint8_t* o = pyr + (size_t)f * pstride + S.off[1] + (size_t)y * S.pitch[1] + x4;
+  if (n == 4) {
+    *reinterpret_cast<uint32_t*>(o) = w;
+  } else {
+    for (int k = 0; k < n; ++k) o[k] = (uint8_t)(w >> (8 * k));
+  }
+}
+
+// ---------------------------------------------------------------------------
 // k_fast_cells: one workgroup per (FAST cell, frame).
 // FAST-9/16 "strength" A(p) = max(0, max_arc min_k I_k - p, p - min_arc max_k I_k)
 // over the 16 arcs of 9 contiguous circle pixels.  cv::FAST at threshold t

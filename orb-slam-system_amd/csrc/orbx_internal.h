@@ -130,6 +130,7 @@ struct BriefArgs {
  * s-1's region; blobs are padded to 16 B */
 struct PyrSeg {
   int nl;
+  int area;           /* 1: one exact-2x level by INTER_AREA (k_pyr_area2; nl = 1, no tiling) */
   int ntx, nty;
   int xs_off, ys_off; /* in quads; table index (s * ntx + tx) / (s * nty + ty) */
   int lds_a, lds_b;   /* ping-pong buffer bytes (source staged in A) */

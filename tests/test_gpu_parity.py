@@ -83,6 +83,11 @@ SCALE_CASES = [
     (752, 480, 1200, 1.5, 6, "rects", 32),
     (1241, 376, 2000, 1.7, 4, "noise", 33),
     (640, 480, 800, 1.95, 3, "rects", 34),
+    # exact 2x ratios: cv::resize takes its INTER_AREA fast path (k_pyr_area2);
+    # 1280x600 mixes area levels with a linear one (75 -> 38 rows, x exactly 2)
+    (640, 480, 1000, 2.0, 4, "rects", 35),
+    (1280, 600, 1000, 2.0, 6, "noise", 36),
+    (1920, 1080, 2000, 2.0, 6, "pan", 37),
 ]
 
 

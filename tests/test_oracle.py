@@ -222,3 +222,20 @@ def test_oracle_search_by_bow_golden(oracle):
         # by the rotation check): it holds -1 there
         assert (m == -2).any() == (ori and bool((m == -2).any()))
         assert np.array_equal(np.where(m == -2, -1, m), g["match_" + tag])
+
+
+def test_oracle_resize_area2_matches_definition(oracle):
+    """cv::resize to exactly half size (INTER_AREA fast path): rounded 2x2 means"""
+    rng = np.random.default_rng(7)
+    a = rng.integers(0, 256, (38, 54), dtype=np.uint8)
+    ref = (a[0::2, 0::2].astype(np.int32) + a[0::2, 1::2] + a[1::2, 0::2] + a[1::2, 1::2] + 2) >> 2
+    assert np.array_equal(oracle.resize_area2(a), ref.astype(np.uint8))
+    # the extractor takes that path for a scale factor of 2: level 2 of a
+    # 640x480 frame is the 2x2 mean of level 0 (= level 1)
+    e = oracle.Extractor(1000, 2.0, 4, 20, 7)
+    e.extract(synth.frame(640, 480, 3, "rects"))
+    assert np.array_equal(e.level(2), oracle.resize_area2(e.level(1)))
+    # at exactly 2x the INTER_LINEAR arithmetic gives the same bytes
+    # (a0 = a1 = b0 = b1 = 1024: ((a+b) + (c+d) + 2) >> 2)
+    assert np.array_equal(e.level(2), oracle.resize_linear(e.level(1), 320, 240))
+
