@@ -590,7 +590,8 @@ __device__ __forceinline__ void fs_strip_body(
   const int ntask = ng * bh;
   uint16_t* L1 = wlist1[wave];
   uint16_t* L2 = wlist2[wave];
-  int n1 = 0, n2 = 0;  // wave-uniform list lengths
+  int n2 = 0;  // wave-uniform list length of L2
+  int n1 = 0;  // wave-uniform L1 length
   auto strength_batch = [&](int e, bool act) {
     bool corner = false;
     if (act) {
@@ -708,7 +709,7 @@ __device__ __forceinline__ void fs_strip_body(
         int sv = __builtin_amdgcn_readfirstlane(n1);
 #pragma unroll
         for (int q = 0; q < FS_PROBE_SALU; ++q) asm volatile("s_add_u32 %0, %0, 1" : "+s"(sv));
-        n1 += (sv == -12345);
+        if (sv == -12345) asm volatile("s_nop 0");
       }
 #endif
 #ifdef FS_PROBE_VALU  // profiling only: FS_PROBE_VALU extra independent VALU per group
@@ -716,7 +717,7 @@ __device__ __forceinline__ void fs_strip_body(
         uint32_t vv = ebase;
 #pragma unroll
         for (int q = 0; q < FS_PROBE_VALU; ++q) asm volatile("v_xor_b32 %0, 1, %0" : "+v"(vv));
-        n1 += __builtin_amdgcn_readfirstlane((int)(vv == 0xFFFFFFFEu));
+        if (__builtin_amdgcn_readfirstlane((int)(vv == 0xFFFFFFFEu))) asm volatile("s_nop 0");
       }
 #endif
       l1_flush();
