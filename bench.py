@@ -78,7 +78,7 @@ def parse():
     ap.add_argument("--batch", type=int, default=0, help="frames per GPU per step (0: workload default)")
     ap.add_argument("--kind", default="pan", help="synthetic stream (orbx/synth.py)")
     ap.add_argument("--nnratio", type=float, default=0.75)
-    ap.add_argument("--cpu-seconds", type=float, default=25.0)
+    ap.add_argument("--cpu-seconds", type=float, default=40.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-latency", action="store_true")
     ap.add_argument("--serial", action="store_true",
@@ -229,10 +229,25 @@ def _topn_sel(k, topn):
     return np.sort(np.array(order, np.uint32))
 
 
+def _pinned(fn):
+    """run fn on one host core (taskset -c 0 equivalent), then
+    restore the process's affinity; returns (result, core)"""
+    try:
+        old = os.sched_getaffinity(0)
+        core = min(old)
+        os.sched_setaffinity(0, {core})
+    except (AttributeError, OSError):
+        return fn(), None
+    try:
+        return fn(), core
+    finally:
+        os.sched_setaffinity(0, old)
+
+
 def _timed_median(fn, seconds, warm=20, want=256):
     """BASELINE.md protocol: 20 untimed warm-up frames, then the median of
-    per-frame times over >= 256 frames -- bounded to `seconds` of CPU work
-    (fewer frames at 1080p; the count is reported)."""
+    per-frame times over 256 frames -- bounded to `seconds` of CPU work as a
+    guard (the count is reported)."""
     i = 0
     t_end = time.perf_counter() + seconds
     while i < warm and time.perf_counter() < t_end:
@@ -266,12 +281,12 @@ def cpu_baseline(args, wl):
                 O.search_by_bow(cur, state["prev"], args.nnratio, True)
             state["prev"] = cur
 
-    med, n, warm = _timed_median(one, args.cpu_seconds)
+    (med, n, warm), core = _pinned(lambda: _timed_median(one, args.cpu_seconds))
     return {"value": round(1.0 / med, 3), "unit": "frames/s", "cores": 1, "kind": "port",
-            "cpu": cpu_model(), "median_ms_per_frame": round(med * 1e3, 3),
+            "cpu": cpu_model(), "pinned_core": core, "median_ms_per_frame": round(med * 1e3, 3),
             "sample": "median per-frame time over %d timed frames after %d warm-up (synthetic %s "
-                      "%dx%d, %d levels), oracle ORBextractor%s, single thread (scalar C "
-                      "restatement of the reference, gcc -O2)" %
+                      "%dx%d, %d levels), oracle ORBextractor%s, single thread pinned to one core "
+                      "(scalar C restatement of the reference, gcc -O3 -mfma -ffp-contract=off)" %
                       (n, warm, args.kind, wl["W"], wl["H"], wl["nlevels"],
                        " + top-%d single-node SearchByBoW vs previous frame" % wl["topn"]
                        if wl["match"] else "")}
@@ -302,13 +317,13 @@ def cpu_baseline_c5(args, wl):
             O.search_by_bow(cur, state["prev"], args.nnratio, True)
         state["prev"] = cur
 
-    med, n, warm = _timed_median(one, args.cpu_seconds)
+    (med, n, warm), core = _pinned(lambda: _timed_median(one, args.cpu_seconds))
     return {"value": round(1.0 / med, 3), "unit": "stereo frames/s", "cores": 1, "kind": "port",
-            "cpu": cpu_model(), "median_ms_per_frame": round(med * 1e3, 3),
+            "cpu": cpu_model(), "pinned_core": core, "median_ms_per_frame": round(med * 1e3, 3),
             "sample": "median per-pair time over %d timed pairs after %d warm-up (synthetic "
                       "%dx%d stereo pairs), oracle ORBextractor (left + right) + "
                       "ComputeStereoMatches + top-%d single-node SearchByBoW vs previous left "
-                      "frame, single thread (scalar C restatement, gcc -O2)" %
+                      "frame, single thread pinned to one core (scalar C restatement, gcc -O3 -mfma)" %
                       (n, warm, wl["W"], wl["H"], wl["topn"])}
 
 

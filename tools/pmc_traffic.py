@@ -3,7 +3,9 @@
 bytes per bench stage (bench.py reads the result as roofline.traffic).
 
 Corrections (MI355X_MICROARCH.md, HBM section): both counters are in KiB;
-on gfx950 FETCH_SIZE reports 1/2 of the bytes of wide coalesced reads, so it
+on gfx950 FETCH_SIZE tallies 64 B per 128-B line fetched -- calibrated for
+16-B / 4-B streams, BRIEF-shaped patch rows and FAST-shaped tiles
+(tools/probe/fetch_calib.hip, profiles/r03_fetch_calibration.json) -- so it
 is doubled.  WRITE_SIZE is taken as is.
 
 usage: pmc_traffic.py PROFDIR [OUT.json]   (PROFDIR has fetch/ and write/)
@@ -21,8 +23,14 @@ STAGE_OF = {
     "k_quadtree": "quadtree",
     "k_orient_brief": "orient_brief",
     "k_match_select": "match_select",
+    "k_pyr_area2": "resize",
+    "k_match_setup": "match_select",
     "k_match_cand_rows": "match_candidates",
     "k_match_candidates": "match_candidates",
+    "k_match_cand_lds": "match_candidates",
+    "k_match_cand_mfma": "match_candidates",
+    "k_match_expand2": "match_candidates",
+    "k_match_gather2": "match_candidates",
     "k_match_resolve_spec": "match_resolve",
     "k_match_resolve": "match_resolve",
     "k_match_finalize": "match_finalize",
@@ -39,15 +47,23 @@ def stage(name):
 
 
 def load(path, counter):
-    per = defaultdict(list)
+    """stage -> kernel -> [bytes per dispatch]"""
+    per = defaultdict(lambda: defaultdict(list))
     with open(path) as f:
         for row in csv.DictReader(f):
             if row["Counter_Name"] != counter:
                 continue
-            s = stage(row["Kernel_Name"])
+            name = row["Kernel_Name"]
+            s = stage(name)
             if s:
-                per[s].append(float(row["Counter_Value"]) * 1024.0)
+                per[s][name.split("(")[0].strip()].append(float(row["Counter_Value"]) * 1024.0)
     return per
+
+
+def per_stage_launch(kernels):
+    # a stage launch = one dispatch of each of its kernels (e.g. expand2 +
+    # cand_mfma for match_candidates): sum of the kernels' means
+    return sum(sum(v) / len(v) for v in kernels.values()), max(len(v) for v in kernels.values())
 
 
 def summarise(d):
@@ -55,13 +71,14 @@ def summarise(d):
     write = load("%s/write/run_counter_collection.csv" % d, "WRITE_SIZE")
     out = {}
     for s in sorted(set(fetch) | set(write)):
-        fr, wr = fetch.get(s, []), write.get(s, [])
-        if not fr or not wr:
+        if not fetch.get(s) or not write.get(s):
             continue
-        rd = 2.0 * sum(fr) / len(fr)
-        wb = sum(wr) / len(wr)
+        fr, n = per_stage_launch(fetch[s])
+        wb, _ = per_stage_launch(write[s])
+        rd = 2.0 * fr  # FETCH_SIZE = 64 B per 128-B line (profiles/r03_fetch_calibration.json)
         out[s] = {"bytes_per_launch": round(rd + wb), "read_bytes_per_launch": round(rd),
-                  "write_bytes_per_launch": round(wb), "launches": len(fr)}
+                  "write_bytes_per_launch": round(wb), "launches": n,
+                  "kernels": sorted(fetch[s])}
     return out
 
 
