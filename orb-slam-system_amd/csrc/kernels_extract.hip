@@ -543,6 +543,9 @@ struct GroupWords {
 #endif
 #define FS_L1CAP (FS_L1FLUSH + 256) /* per-wave cardinal survivors: < FS_L1FLUSH carried + <= 256 new */
 #define FS_L2CAP 128 /* per-wave even-test survivors: < 64 carried + <= 64 new */
+#ifndef FS_CW_RMAX
+#define FS_CW_RMAX 8 /* column walk: band rows per wave (registers hold FS_CW_RMAX + 6 rows) */
+#endif
 
 
 // ---------------------------------------------------------------------------
@@ -559,7 +562,7 @@ __device__ __forceinline__ void fs_strip_body(
     int* __restrict__ cslot, int& ncorner, const StripInfo& st, int f, int lead, int xal,
     int slot_pref, uint32_t* __restrict__ slots, size_t slot_stride,
     uint32_t* __restrict__ ccount, int ncells, int ini_th, int min_th, int tpitch_rt, int ccap,
-    int* __restrict__ ovf, int dbg) {
+    int* __restrict__ ovf, int dbg, const uint8_t* __restrict__ gsrc, int gpitch, bool cw) {
   const int tpitch = TP ? TP : tpitch_rt;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // uniform: list bases in SGPRs
@@ -592,6 +595,9 @@ __device__ __forceinline__ void fs_strip_body(
   uint16_t* L2 = wlist2[wave];
   int n2 = 0;  // wave-uniform list length of L2
   int n1 = 0;  // wave-uniform L1 length
+#ifdef FS_PROBE_NOAPP
+  uint32_t probe_sink = 0;
+#endif
   auto strength_batch = [&](int e, bool act) {
     bool corner = false;
     if (act) {
@@ -681,7 +687,9 @@ __device__ __forceinline__ void fs_strip_body(
         wave_sync_lds();
         while (n1 >= 64) {
           n1 -= 64;
+#ifndef FS_PROBE_NOB  // profiling only: appends without stages B / C
           even_batch(L1[n1 + lane], true);
+#endif
         }
         wave_sync_lds();
       }
@@ -693,6 +701,10 @@ __device__ __forceinline__ void fs_strip_body(
       // mbcnt of it from 0 at the uniform L1 + n1, only survivors store
       // (stores of every lane to a dummy slot measured 13 % slower).
       // Columns outside [c0, c1) are appended too and rejected in stage B.
+#ifdef FS_PROBE_NOAPP  // profiling only: stage A tests without appends
+      probe_sink |= clo | chi;
+      return;
+#endif
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const uint32_t x = (j & 1) ? chi : clo;
@@ -725,7 +737,49 @@ __device__ __forceinline__ void fs_strip_body(
     auto group = [&](const uint8_t* gb, uint8_t* zp, uint32_t ebase, uint32_t ttl, bool zf) {
       gtest(gload(gb), zp, ebase, ttl, zf);
     };
-    if (ng <= 64) {
+    if (cw) {
+      // column walk (no block-wide staging): lane l <-> tile dword column
+      // gb + l (gb = g0, or g0 - 1 when the band's first pixel needs the
+      // dword left of it); wave w owns band rows [rb, re) and loads tile rows
+      // [rb, re + 6) straight into registers, writes them to the tile for
+      // stages B / C (rows shared with the neighbouring waves are written
+      // twice with the same bytes) and runs stage A from the registers: the
+      // row's own dword, rows -3 / +3 of the column, and the neighbouring
+      // columns' dwords by DPP wave shifts (no LDS reads, no barrier)
+      const int gb = g0 - ((c0 & 3) != 3 ? 1 : 0);
+      const int rpwv = (bh + FS_NW - 1) / FS_NW;
+      const int rb = wave * rpwv, re = min(bh, rb + rpwv);
+      const int gl = min(gb + lane, g1);  // lanes past the right halo repeat it
+      const bool lact = gb + lane >= g0 && gb + lane < g1;
+      const uint32_t tl = lact ? tt : 0xFF00FF00u;
+      if (rb < re) {  // wave-uniform
+        uint32_t V[FS_CW_RMAX + 6];
+        const uint8_t* src = gsrc + 4 * gl;
+#pragma unroll
+        for (int k = 0; k < FS_CW_RMAX + 6; ++k)  // unconditional: rows past the tile repeat its last
+          V[k] = *reinterpret_cast<const uint32_t*>(src + __umul24((uint32_t)min(rb + k, st.h - 1), (uint32_t)gpitch));
+        uint8_t* trow = tile + __mul24(rb, tpitch) + 4 * gl;
+        const int nr = re - rb;
+#pragma unroll
+        for (int k = 0; k < FS_CW_RMAX + 6; ++k)
+          if (k < nr + 6) *reinterpret_cast<uint32_t*>(trow + k * tpitch) = V[k];
+        if (dbg == 5) return;  // profiling only: loads and tile stores
+        uint8_t* zrow = amap + __mul24(3 + rb, tpitch) + 4 * gl;
+        uint32_t er = ((uint32_t)(3 + rb) << 9) | (uint32_t)(4 * gl);
+#pragma unroll
+        for (int k = 0; k < FS_CW_RMAX; ++k) {
+          if (k < nr) {  // wave-uniform
+            GroupWords q;
+            q.up = V[k];
+            q.w1 = V[k + 3];
+            q.dn = V[k + 6];
+            q.w0 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)V[k + 3], 0x138, 0xf, 0xf, false);  // wave_shr:1
+            q.w2 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)V[k + 3], 0x130, 0xf, 0xf, false);  // wave_shl:1
+            gtest(q, zrow + k * tpitch, er + ((uint32_t)k << 9), tl, lact);
+          }
+        }
+      }
+    } else if (ng <= 64) {
       // row-mapped: lane = (row lr of the step, group lg); a step covers
       // rpw = 64 / ngp rows (ngp = 16 / 32 / 64 >= ng); offsets and entries
       // are lane constants plus a uniform row term, the loop is scalar
@@ -777,6 +831,9 @@ __device__ __forceinline__ void fs_strip_body(
     wave_sync_lds();
     if (n2 > 0) strength_batch(lane < n2 ? (int)L2[lane] : 0, lane < n2);
   }
+#ifdef FS_PROBE_NOAPP
+  if (probe_sink == 0x9E3779B9u) ovf[1] = 1;
+#endif
   __syncthreads();
   if (dbg == 2) return;
   for (int i = tid; i < st.ncells * bh; i += FS_NT) mask[i] = mask2[i] = 0ull;  // over the dead tile
@@ -949,15 +1006,25 @@ __device__ __forceinline__ void fs_kernel(
   const int xal = aligned16 ? (st.x & ~15) : aligned ? (st.x & ~3) : st.x;
   const int lead = st.x - xal;          // tile col of global st.x
   const int tw = lead + st.w;           // columns in use
-  {
-    const uint8_t* s0 = base + (size_t)st.y * pitch + xal;
+  const uint8_t* s0 = base + (size_t)st.y * pitch + xal;
+  // column walk (fs_strip_body): dword-aligned rows, band rows <= 4 waves x
+  // FS_CW_RMAX, and the band's dword columns plus both halo dwords within
+  // the 64 lanes (every strip of the bench workloads but wCell-32 levels)
+#ifdef FS_NO_COLWALK  // profiling variant: block-wide staging for every strip
+  const bool cw = false;
+#else
+  const int cg0 = (lead + 3) >> 2, cg1 = (lead + st.w) >> 2;
+  const int cgb = cg0 - (((lead + 3) & 3) != 3 ? 1 : 0);
+  const bool cw = FS_NW == 4 && aligned && st.h - 6 <= FS_NW * FS_CW_RMAX && cg1 - cgb <= 63;
+#endif
+  if (!cw) {
     if (aligned16) stage_region<v4u, 4, FS_NT>(tile, tpitch, s0, pitch, st.h, (tw + 15) >> 4, tid);
     else if (aligned) stage_region<uint32_t, 12, FS_NT>(tile, tpitch, s0, pitch, st.h, (tw + 3) >> 2, tid);
     else stage_rows_u32<12, FS_NT>(tile, tpitch, s0, pitch, st.h, tw, tid);
   }
   fs_strip_body<TP>(tile, amap_mem, cnt, mask, mask2, wlist1, wlist2, clist, cslot, ncorner, st, f,
                     lead, xal, slot_pref, slots, slot_stride, ccount, ncells, ini_th, min_th, tpitch,
-                    ccap, ovf, dbg);
+                    ccap, ovf, dbg, s0, pitch, cw);
 }
 
 #define FS_KERNEL_ARGS                                                                              \
