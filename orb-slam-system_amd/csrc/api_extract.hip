@@ -207,6 +207,8 @@ extern "C" int orbx_plan_create(const orbx_params* prm, int width, int height, i
     p->largs.pyr_off[l] = u.pyr_off;
     p->largs.pitch[l] = u.pitch;
   }
+  p->largs.key_xs = P.levels[0].key_xs;
+  p->bargs.key_xs = P.levels[0].key_xs;
   p->bargs.nlevels = P.params.nlevels;
   p->bargs.kcap = P.kcap;
   for (int l = 0; l < P.params.nlevels; ++l) {

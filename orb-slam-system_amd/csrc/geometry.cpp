@@ -389,13 +389,21 @@ int plan_geometry(const orbx_params& p, int width, int height, Plan& P) {
 
   /* ComputePyramid sizes (:501-502) and storage */
   long long pyr = 0, blur = 0;
+  int key_xs = 20;
   for (int l = 0; l < L; ++l) {
     LevelInfo& lv = P.levels[l];
     float s = P.tables.inv_scale[l];
     lv.w = round_f((float)width * s);
     lv.h = round_f((float)height * s);
     if (lv.h <= 32 || lv.w < 32) return ORBX_ERR_LEVEL_SIZE;
-    if (lv.w - 32 > 4095 || lv.h - 32 > 4095) return ORBX_ERR_UNSUPPORTED; /* 12-bit packing */
+    if (l == 0) { /* FAST key packing (orbx_pack_key): coordinate bits for level 0 */
+      const int xw = lv.w - 32, yh = lv.h - 32;
+      if (xw <= 4095 && yh <= 4095) key_xs = 20;
+      else if (xw <= 8191 && yh <= 2047) key_xs = 19;
+      else if (xw <= 2047 && yh <= 8191) key_xs = 21;
+      else return ORBX_ERR_UNSUPPORTED;
+    }
+    lv.key_xs = key_xs;
     if (l > 0 && lv.w == P.levels[l - 1].w && lv.h == P.levels[l - 1].h) {
       lv.unique = P.levels[l - 1].unique; /* cv::resize: dsize == ssize -> copyTo */
     } else {

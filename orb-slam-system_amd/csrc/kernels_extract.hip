@@ -562,7 +562,7 @@ __device__ __forceinline__ void fs_strip_body(
     int* __restrict__ cslot, int& ncorner, const StripInfo& st, int f, int lead, int xal,
     int slot_pref, uint32_t* __restrict__ slots, size_t slot_stride,
     uint32_t* __restrict__ ccount, int ncells, int ini_th, int min_th, int tpitch_rt, int ccap,
-    int* __restrict__ ovf, int dbg, const uint8_t* __restrict__ gsrc, int gpitch, bool cw) {
+    int* __restrict__ ovf, int dbg, const uint8_t* __restrict__ gsrc, int gpitch, bool cw, int kxs) {
   const int tpitch = TP ? TP : tpitch_rt;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // uniform: list bases in SGPRs
@@ -919,7 +919,7 @@ __device__ __forceinline__ void fs_strip_body(
         m &= m - 1;
         const int c = cb0 + b;
         const int gx = xal + c - ORBX_MINB;
-        fslots[so + off++] = orbx_pack_key((uint32_t)gx, (uint32_t)gy, (uint32_t)arow[c] - 1u);
+        fslots[so + off++] = orbx_pack_key((uint32_t)gx, (uint32_t)gy, (uint32_t)arow[c] - 1u, kxs);
       }
       if (lane == 0) ccount[(size_t)f * ncells + st.cell_begin + kk] = (uint32_t)tlo;
       if (lane == 32 && kk + 1 < st.ncells)
@@ -944,7 +944,7 @@ __device__ __forceinline__ void fs_strip_body(
         const int c = cb0 + b;
         const int gx = xal + c - ORBX_MINB;
         fslots[so + off++] =
-            orbx_pack_key((uint32_t)gx, (uint32_t)gy, (uint32_t)amap[(3 + br) * tpitch + c] - 1u);
+            orbx_pack_key((uint32_t)gx, (uint32_t)gy, (uint32_t)amap[(3 + br) * tpitch + c] - 1u, kxs);
       }
       carry += tot;
     }
@@ -1024,7 +1024,7 @@ __device__ __forceinline__ void fs_kernel(
   }
   fs_strip_body<TP>(tile, amap_mem, cnt, mask, mask2, wlist1, wlist2, clist, cslot, ncorner, st, f,
                     lead, xal, slot_pref, slots, slot_stride, ccount, ncells, ini_th, min_th, tpitch,
-                    ccap, ovf, dbg, s0, pitch, cw);
+                    ccap, ovf, dbg, s0, pitch, cw, LA.key_xs);
 }
 
 #define FS_KERNEL_ARGS                                                                              \
@@ -1080,8 +1080,8 @@ __device__ int block_scan_excl(int* a, int n, int* wtmp) {
 // so keys never move; each node keeps the first maximal response of its
 // keys (ties -> lowest key index = earliest in vToDistributeKeys).
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ int quadrant(uint32_t key, int rx, int ry) {
-  const int x = (int)(key >> 20), y = (int)((key >> 8) & 0xFFF);
+__device__ __forceinline__ int quadrant(uint32_t key, int rx, int ry, int kxs) {
+  const int x = orbx_key_x(key, kxs), y = orbx_key_y(key, kxs);
   const int x0 = rx & 0xFFFF, x1 = rx >> 16, y0 = ry & 0xFFFF, y1 = ry >> 16;
   const int hx = (x1 - x0) / 2, hy = (y1 - y0) / 2;
   const int right = x >= x0 + hx, bottom = y >= y0 + hy;
@@ -1212,7 +1212,7 @@ __device__ __forceinline__ void qt_body(QT_KERNEL_ARGS) {
   for_keys([&](int, uint32_t key, int& n) {
     n = -1;
     if (nIni > 0) {
-      const float x = (float)(key >> 20);
+      const float x = (float)orbx_key_x(key, L.key_xs);
       const int idx = (int)(x / L.hX);
       if (idx >= 0 && idx < nIni) n = idx;
     }
@@ -1231,7 +1231,7 @@ __device__ __forceinline__ void qt_body(QT_KERNEL_ARGS) {
     if (tid == 0) s_flag = 0;
     __syncthreads();
     for_keys([&](int, uint32_t key, int& n) {
-      if (n >= 0 && cnt[n] >= 2) atomicAdd(&child[4 * n + quadrant(key, rx[n], ry[n])], 1);
+      if (n >= 0 && cnt[n] >= 2) atomicAdd(&child[4 * n + quadrant(key, rx[n], ry[n], L.key_xs)], 1);
     });
     __syncthreads();
     for (int i = tid; i < S; i += 256) {
@@ -1280,7 +1280,7 @@ __device__ __forceinline__ void qt_body(QT_KERNEL_ARGS) {
     }
     __syncthreads();
     for_keys([&](int, uint32_t key, int& n) {
-      if (n >= 0) n = (cnt[n] >= 2) ? child[4 * n + quadrant(key, rx[n], ry[n])] : child[4 * n];
+      if (n >= 0) n = (cnt[n] >= 2) ? child[4 * n + quadrant(key, rx[n], ry[n], L.key_xs)] : child[4 * n];
     });
     const bool finish = (newS >= L.N) || (s_flag == 0);
     __syncthreads();
@@ -1582,8 +1582,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OB_WPE))) v
     BriefKp k;
     k.oi = e + i;
     k.l = l;
-    k.x = (int)(key >> 20) + ORBX_MINB;
-    k.y = (int)((key >> 8) & 0xFFF) + ORBX_MINB;
+    k.x = orbx_key_x(key, A.key_xs) + ORBX_MINB;
+    k.y = orbx_key_y(key, A.key_xs) + ORBX_MINB;
     k.score = (int)(key & 0xFF);
     k.scale = A.scale[l];
     k.patch_size = A.patch[l];

@@ -50,7 +50,7 @@ struct LevelInfo {
   int blur_tile_begin; /* first blur tile of this unique level (ORBX_BLUR_TW x ORBX_BLUR_TH) */
   int blur_tiles_x;
   int wcell;
-  int pad;
+  int key_xs;          /* FAST key packing shift (orbx_pack_key)                 */
 };
 
 #define ORBX_BLUR_TW 128
@@ -80,6 +80,7 @@ struct StripInfo {
 struct LevelArgs {
   long long pyr_off[ORBX_MAX_LEVELS];
   int pitch[ORBX_MAX_LEVELS];
+  int key_xs; /* orbx_pack_key shift */
 };
 #define ORBX_STRIP_MAXCELLS 64 /* cells per FAST strip (>= 256 / min cell width) */
 
@@ -114,6 +115,7 @@ struct BriefArgs {
   float scale[ORBX_MAX_LEVELS];
   int patch[ORBX_MAX_LEVELS];
   uint32_t umaxw[4]; /* IC_Angle umax[0..15], one byte each */
+  int key_xs;        /* orbx_pack_key shift */
 };
 
 /* fused pyramid segment: destination levels lev[1..nl] computed in one
@@ -147,8 +149,13 @@ struct PyrSeg {
 #define ORBX_HDI inline
 #endif
 
-static ORBX_HDI uint32_t orbx_pack_key(uint32_t x, uint32_t y, uint32_t score) {
-  return (x << 20) | (y << 8) | score;
+/* FAST keys: (x - 16) << xs | (y - 16) << 8 | score.  xs = 20 (12 + 12
+ * coordinate bits) unless the frame is wider or taller than 4127 px: then 19
+ * (13-bit x, 11-bit y) or 21 (11-bit x, 13-bit y), chosen by the planner */
+static ORBX_HDI uint32_t orbx_pack_key(uint32_t x, uint32_t y, uint32_t score, int xs) {
+  return (x << xs) | (y << 8) | score;
 }
+static ORBX_HDI int orbx_key_x(uint32_t key, int xs) { return (int)(key >> xs); }
+static ORBX_HDI int orbx_key_y(uint32_t key, int xs) { return (int)((key >> 8) & ((1u << (xs - 8)) - 1u)); }
 
 #endif

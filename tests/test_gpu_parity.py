@@ -22,6 +22,11 @@ EXTRACT_CASES = [
     (642, 361, 1000, 8, "strict", "rects", 9),     # rows 2 mod 4: unaligned dword staging
     (1920, 1080, 2000, 8, "empty", "rects", 6),    # config 3 (cell_guard=empty)
     (1920, 1080, 2000, 8, "empty", "noise", 7),
+    # large frames: 4096 wide (12-bit key coordinates), wider / taller than
+    # 4127 (13-bit x or y in the FAST keys, orbx_pack_key)
+    (4096, 400, 2000, 8, "empty", "noise", 40),
+    (5000, 720, 3000, 8, "empty", "rects", 41),
+    (600, 4400, 2000, 8, "empty", "noise", 42),
 ]
 
 

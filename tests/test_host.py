@@ -57,6 +57,21 @@ def test_strict_guard_geometry(orbx_mod):
     assert [g.ncells_bad[l] > 0 for l in range(8)] == [True, True, True, True] + [False] * 4
 
 
+@pytest.mark.parametrize("w,h,ok", [(4127, 4127, True), (4128, 1000, True), (8223, 2079, True),
+                                    (2079, 8223, True), (8224, 600, False), (4200, 4200, False)])
+def test_large_frame_geometry(orbx_mod, w, h, ok):
+    """Frames past 4127 px: the FAST key packing trades coordinate bits
+    (13-bit x / 11-bit y or the reverse); beyond both it is unsupported."""
+    prm = orbx_mod.params(2000, 1.2, 8, 20, 7, "empty")
+    if ok:
+        g = orbx_mod.geometry(prm, w, h)
+        assert (g.width[0], g.height[0]) == (w, h)
+    else:
+        with pytest.raises(orbx_mod.OrbxError) as e:
+            orbx_mod.geometry(prm, w, h)
+        assert e.value.code == orbx_mod.ERR_UNSUPPORTED
+
+
 def test_level_too_small(orbx_mod):
     with pytest.raises(orbx_mod.OrbxError) as e:
         orbx_mod.geometry(orbx_mod.params(1000, 1.2, 14, 20, 7), 320, 240)
