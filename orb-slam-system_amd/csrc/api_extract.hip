@@ -373,9 +373,17 @@ static int extract_pass(orbx_plan* p, const uint8_t* frames, int n, size_t fstri
   // next patch's loads overlap the current keypoint and the per-wave setup
   // -- pattern registers, exception keys, level scan -- is amortised; 4 / 8
   // / 12 / 16 / 24 per wave measured 0.535 / 0.522 / 0.521 / 0.531 / 0.538 ms
-  // at c4, 1.004 / 0.961 / 0.947 / 0.946 / 0.956 at c1)
+  // at c4, 1.004 / 0.961 / 0.947 / 0.946 / 0.956 at c1).  Frames of 1 Mpx
+  // and more take about 6: the frames of an XCD are dispatched one after
+  // the other (frame_unit), so more waves per frame means fewer frames'
+  // patch bands resident in its L2 at once and more of the patches' line
+  // overlap caught there -- c4 HBM reads 1726 -> 1311 MB per launch (1.58x
+  // -> 1.20x the algorithmic bytes) for +1.2 % BRIEF time
+  // (tools/obdiv_fetch.sh: ~12 / 6 / 3 / 2 / 1 per wave read 1726 / 1311 /
+  // 1091 / 1119 / 1003 MB in 0.544 / 0.551 / 0.576 / 0.599 / 0.653 ms)
   const int ob_full = std::max(4, std::min(P.kcap, P.params.nfeatures + 256));
-  int ob_waves = std::min(ob_full, std::max((ob_full + 11) / 12, (16384 + n - 1) / n));
+  const int ob_kpw = (long long)P.levels[0].w * P.levels[0].h >= (1 << 20) ? 6 : 12;
+  int ob_waves = std::min(ob_full, std::max((ob_full + ob_kpw - 1) / ob_kpw, (16384 + n - 1) / n));
   if (p->ob_div > 0) ob_waves = std::max(4, ob_full / p->ob_div); /* profiling only */
   hipLaunchKernelGGL(k_orient_brief, dim3((ob_waves + 3) / 4, n),
                      dim3(256), 0, s, frames, fstride, rstride, d_pyr, p->pyr_stride, p->bargs,

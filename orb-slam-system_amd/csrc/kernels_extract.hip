@@ -1601,20 +1601,29 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OB_WPE))) v
   // the frame's keypoints, so the grid is sized by nfeatures, not capacity.
   // Software pipeline: keypoint o is computed while the patch of o+stride
   // is loading into registers.
-  const int stride = (int)gridDim.x * 4;
+  const int nwv = (int)gridDim.x * 4;
+#ifdef OB_CONTIG  // profiling variant: each wave walks a contiguous run of the processing order
+  const int per = (total + nwv - 1) / nwv;
+  const int stride = 1;
+  int o = g * per;
+  const int oend = min(total, o + per);
+#else
+  const int stride = nwv;
   int o = g;
-  if (o >= total) return;
+  const int oend = total;
+#endif
+  if (o >= oend) return;
   BriefKp cur = locate(o);
   BriefRegs R;
   brief_issue(cur, R, lane);
-  for (; o < total; o += stride) {  // wave-uniform
+  for (; o < oend; o += stride) {  // wave-uniform
   // ---- stage this keypoint's patch (unblurred level), reflect-101 outside ----
   brief_commit(R, &P[0][0], lane);
   const uint32_t hte = R.ht;  // before the next keypoint's issue overwrites R
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   const BriefKp me = cur;
-  if (o + stride < total) {  // next keypoint: its patch loads stay in flight
+  if (o + stride < oend) {  // next keypoint: its patch loads stay in flight
     cur = locate(o + stride);
     brief_issue(cur, R, lane);
   }
