@@ -611,15 +611,11 @@ extern "C" int orbx_extract(orbx_extractor* e, const uint8_t* img, int W, int H,
                          e->d_count, s);
   p->ev_after_pyr = nullptr;
   if (rc) return rc;
-  if (to_host) {
-    // the levels come back on the copy stream while FAST, the quadtree and
-    // BRIEF run: level 0 (= level 1) from the uploaded image, the level
-    // buffer (levels >= 2) once the pyramid kernel is done
+  if (to_host && e->pyr_bytes) {
+    // the level buffer (levels >= 2) comes back on the copy stream while
+    // FAST, the quadtree and BRIEF run, once the pyramid kernel is done
     ORBX_TRY(hipStreamWaitEvent(e->s_copy, e->ev_pyr, 0));
-    if (!(e->flags & ORBX_EXTRACTOR_PINNED_H2D))
-      ORBX_TRY(hipMemcpyAsync(e->h_img, e->d_img, (size_t)W * H, hipMemcpyDeviceToHost, e->s_copy));
-    if (e->pyr_bytes)
-      ORBX_TRY(hipMemcpyAsync(e->h_pyr, p->d_pyr, e->pyr_bytes, hipMemcpyDeviceToHost, e->s_copy));
+    ORBX_TRY(hipMemcpyAsync(e->h_pyr, p->d_pyr, e->pyr_bytes, hipMemcpyDeviceToHost, e->s_copy));
   }
   // one round trip in the common case: the error word, the count and a
   // speculative prefix of the rows (sized by the previous call) come back
@@ -634,6 +630,16 @@ extern "C" int orbx_extract(orbx_extractor* e, const uint8_t* img, int W, int H,
   ORBX_TRY(hipMemcpyAsync(h_kps, e->d_kps, sizeof(orbx_keypoint) * (size_t)guess,
                           hipMemcpyDeviceToHost, s));
   ORBX_TRY(hipMemcpyAsync(h_desc, e->d_desc, 32 * (size_t)guess, hipMemcpyDeviceToHost, s));
+  if (to_host && !(e->flags & ORBX_EXTRACTOR_PINNED_H2D)) {
+    // level 0 (= level 1) of the host pyramid: a host copy of the caller's
+    // rows made while the GPU works (the thread would only wait), instead of
+    // a D2H of the uploaded image on the copy stream ahead of the levels
+    if (stride == (size_t)W) {
+      memcpy(e->h_img, img, (size_t)W * H);
+    } else {
+      for (int r = 0; r < H; ++r) memcpy(e->h_img + (size_t)r * W, img + (size_t)r * stride, (size_t)W);
+    }
+  }
   ORBX_TRY(stream_wait(s));
   if (to_host) ORBX_TRY(stream_wait(e->s_copy));
   if (*p->h_err) {
