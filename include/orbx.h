@@ -35,8 +35,9 @@ enum {
                                 src/ORBextractor.cc:230) or < 32 cols                     */
   ORBX_ERR_QUADTREE = -4,    /* DistributeOctTree would never terminate */
   ORBX_ERR_CAPACITY = -5,    /* caller buffer too small (*n holds the required count)     */
-  ORBX_ERR_UNSUPPORTED = -6, /* exact 2x level ratio (OpenCV switches to INTER_AREA) or a
-                                configuration beyond the kernels' static limits          */
+  ORBX_ERR_UNSUPPORTED = -6, /* a configuration beyond the kernels' static limits (level
+                                ratio > ~2.3 other than exactly 2, frame > 4127 px on
+                                both sides or > 8223 px on one, ...)                    */
   ORBX_ERR_HIP = -7,         /* HIP runtime error                                         */
   ORBX_ERR_NO_DEVICE = -8,   /* no gfx950 device / bad device ordinal                     */
 };

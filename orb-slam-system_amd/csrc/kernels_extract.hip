@@ -168,6 +168,11 @@ __device__ __forceinline__ uint32_t as_u32(us2 x) { return __builtin_bit_cast(ui
 #ifndef PYR_U
 #define PYR_U 1
 #endif
+#ifdef PYR_PROBE_NOSTORE  // profiling only: no HBM stores of the levels
+#define PYR_STORE_ON 0
+#else
+#define PYR_STORE_ON 1
+#endif
 // PYR_U: rows in flight per thread (more measured slower)
 
 __global__ __launch_bounds__(256) void k_pyramid(const uint8_t* __restrict__ frames, size_t fstride,
@@ -309,7 +314,7 @@ __global__ __launch_bounds__(256) void k_pyramid(const uint8_t* __restrict__ fra
             if (r >= nrows) break;
             const int y = Y.x + r;
             *reinterpret_cast<uint32_t*>(nxt + r * dpitch + 4 * cg) = packed[u];
-            if (y >= Y.z && y < Y.w && any_x) {
+            if (PYR_STORE_ON && y >= Y.z && y < Y.w && any_x) {
               uint8_t* o = gdst + (uint32_t)(y * gp + gx0);  // a level is < 4 GB
               if (in_x) {
                 *reinterpret_cast<uint32_t*>(o) = packed[u];  // pyr offsets/pitches are 16-B multiples
@@ -323,7 +328,9 @@ __global__ __launch_bounds__(256) void k_pyramid(const uint8_t* __restrict__ fra
         }
       }
     }
+#ifndef PYR_PROBE_NOSYNC  // profiling only: level passes without the block barrier (wrong pixels)
     __syncthreads();
+#endif
     uint8_t* t = cur;
     cur = nxt;
     nxt = t;
