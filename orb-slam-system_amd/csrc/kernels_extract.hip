@@ -1535,6 +1535,9 @@ __device__ __forceinline__ void brief_commit(const BriefRegs& R, uint32_t* P, in
 #ifndef OB_WPE
 #define OB_WPE 7
 #endif
+#ifndef OB_PROBE
+#define OB_PROBE 0 /* profiling only: 1 / 2 / 3 skip the horizontal pass / IC_Angle sums / samples */
+#endif
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OB_WPE))) void k_orient_brief(
     const uint8_t* __restrict__ frames, size_t fstride, size_t rstride,
     const uint8_t* __restrict__ pyr, size_t pstride, const BriefArgs A,
@@ -1656,7 +1659,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OB_WPE))) v
     // this lane's task of round k: byte k of hte (loaded with the patch;
     // LDS holds patch + 40-column hblur only: 22.3 KB, 7 workgroups per CU)
 #pragma unroll
-    for (int k = 0; k < 3; ++k) {
+    for (int k = 0; k < (OB_PROBE == 1 ? 0 : 3); ++k) {  // OB_PROBE 1: no horizontal pass (profiling only)
       const uint32_t e = (hte >> (8 * k)) & 0xFFu;
       if (e == 0xFFu) continue;
       const int rp = (int)((e * 205u) >> 11), qi = (int)e - 10 * rp;  // e / 10 (exact for e < 256)
@@ -1685,7 +1688,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OB_WPE))) v
   const int cc = x - px0, cr = KP_R;
   const int hcc = cc - 4 * ((cc - 18) >> 2);  // hblur column of the keypoint (column 4 qlo is 0)
   int m10 = 0, m01 = 0;
-  if (lane < 62) {
+  if (OB_PROBE != 2 && lane < 62) {  // OB_PROBE 2: no IC_Angle sums (profiling only)
     const int v = (lane >> 1) - 15, av = v < 0 ? -v : v;
     const uint32_t uw = (av >> 2) == 0 ? A.umaxw[0] : (av >> 2) == 1 ? A.umaxw[1]
                       : (av >> 2) == 2 ? A.umaxw[2] : A.umaxw[3];
@@ -1721,7 +1724,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OB_WPE))) v
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   uint64_t words[4] = {0, 0, 0, 0};
 #pragma unroll
-  for (int rr = 0; rr < 3; ++rr) {
+  for (int rr = 0; rr < (OB_PROBE == 3 ? 0 : 3); ++rr) {  // OB_PROBE 3: no samples (profiling only)
     int t[2];
 #pragma unroll
     for (int e = 0; e < 2; ++e) {
