@@ -452,10 +452,16 @@ def host_fed_leg(torch, orbx, plan, mp, wl, args, dev, ref_counts, steps=6, warm
     hc = torch.empty((2, B), dtype=torch.int32).pin_memory()
     hm = torch.empty((2, B, R), dtype=torch.int32).pin_memory()
     s_in, s_c, s_out = (torch.cuda.Stream(device=dev) for _ in range(3))
+    # the frames' H2D split into chunks over NS copy streams (one DMA queue
+    # per stream; ORBX_BENCH_H2D_STREAMS, default 2)
+    ns = max(1, int(os.environ.get("ORBX_BENCH_H2D_STREAMS", "2")))
+    s_ins = [s_in] + [torch.cuda.Stream(device=dev) for _ in range(ns - 1)]
+    ev_ins = [[torch.cuda.Event() for _ in range(ns)] for _ in range(2)]
+    bounds = [B * j // ns for j in range(ns + 1)]
     ev_in = [torch.cuda.Event() for _ in range(2)]
     ev_c = [torch.cuda.Event() for _ in range(2)]
     ev_out = [torch.cuda.Event() for _ in range(2)]
-    for s in (s_in, s_c, s_out):
+    for s in s_ins + [s_c, s_out]:
         s.wait_stream(torch.cuda.current_stream())
     for i in range(2):
         ev_c[i].record(s_c)
@@ -463,12 +469,15 @@ def host_fed_leg(torch, orbx, plan, mp, wl, args, dev, ref_counts, steps=6, warm
 
     def step(k):
         i = k & 1
-        with torch.cuda.stream(s_in):
-            s_in.wait_event(ev_c[i])  # the compute of step k-2 has read dfr[i]
-            dfr[i].copy_(host[k & 1], non_blocking=True)
-            ev_in[i].record(s_in)
+        for j, sj in enumerate(s_ins):
+            with torch.cuda.stream(sj):
+                sj.wait_event(ev_c[i])  # the compute of step k-2 has read dfr[i]
+                a, b = bounds[j], bounds[j + 1]
+                dfr[i][a:b].copy_(host[k & 1][a:b], non_blocking=True)
+                ev_ins[i][j].record(sj)
         with torch.cuda.stream(s_c):
-            s_c.wait_event(ev_in[i])
+            for e in ev_ins[i]:
+                s_c.wait_event(e)
             s_c.wait_event(ev_out[i])  # the D2H of step k-2 has read buffer i
             kps[i][0].copy_(kps[1 - i][B])
             desc[i][0].copy_(desc[1 - i][B])
@@ -507,8 +516,8 @@ def host_fed_leg(torch, orbx, plan, mp, wl, args, dev, ref_counts, steps=6, warm
             "pcie_d2h_gbs": round(d2h * steps / el / 1e9, 2),
             "bytes_per_step": {"h2d": h2d, "d2h": d2h}, "rows_returned_per_frame": R,
             "max_keypoints_per_frame": maxk, "rows_cover_all_keypoints": maxk <= R,
-            "counts_equal_resident_run": same,
-            "note": "frames from pinned host memory (H2D on a copy stream), extraction + SearchByBoW "
+            "counts_equal_resident_run": same, "h2d_streams": ns,
+            "note": "frames from pinned host memory (H2D in chunks over h2d_streams copy streams), extraction + SearchByBoW "
                     "on a compute stream, keypoints/descriptors/matches back to pinned host memory "
                     "on a third stream; steps overlap on double buffers (bound: the PCIe H2D of the "
                     "frames)"}

@@ -916,11 +916,21 @@ __device__ __forceinline__ void fs_strip_body(
       unsigned long long m = act ? mk[br] : 0ull;
       const int n = __popcll(m);
       const int incl = wave_incl_scan(n);
-      const int tlo = lane_value(incl, 31), tall = lane_value(incl, 63);
+      int tlo = lane_value(incl, 31), tall = lane_value(incl, 63);
       int off = incl - n - (lane >= 32 ? tlo : 0);
       const int cb0 = c0 + k * wcell, so = cslot[kc];
       const int gy = st.y + 3 + br - ORBX_MINB;
       const uint8_t* arow = amap + __mul24(3 + br, tpitch);
+#ifdef FS_PROBE_NOOUT  // profiling only: no key stores (a dependent sink instead)
+      uint32_t sink = 0;
+      while (m) {
+        const int b = __ffsll(m) - 1;
+        m &= m - 1;
+        sink += (uint32_t)arow[cb0 + b] + (uint32_t)off++;
+      }
+      if (sink == 0x9E3779B9u) fslots[so] = sink;
+      tall = tlo = 0;  // no keypoints downstream
+#else
       while (m) {
         const int b = __ffsll(m) - 1;
         m &= m - 1;
@@ -928,6 +938,7 @@ __device__ __forceinline__ void fs_strip_body(
         const int gx = xal + c - ORBX_MINB;
         fslots[so + off++] = orbx_pack_key((uint32_t)gx, (uint32_t)gy, (uint32_t)arow[c] - 1u, kxs);
       }
+#endif
       if (lane == 0) ccount[(size_t)f * ncells + st.cell_begin + kk] = (uint32_t)tlo;
       if (lane == 32 && kk + 1 < st.ncells)
         ccount[(size_t)f * ncells + st.cell_begin + kk + 1] = (uint32_t)(tall - tlo);
