@@ -1157,8 +1157,8 @@ __device__ __forceinline__ void qt_body(QT_KERNEL_ARGS) {
   // cell offsets live only through the key gather: the node arrays reuse
   // their LDS (max(maxcells + 1, 11 smax) ints: one round of workgroups)
   int* cell_off = smem;                       // maxcells + 1
-  int* rx = smem;                             // smax
-  int* ry = rx + smax;                        // smax
+  int* rx = smem;                             // smax  (rx / ry / cnt and nrx / nry / ncnt
+  int* ry = rx + smax;                        // smax   swap roles every pass)
   int* cnt = ry + smax;                       // smax
   int* child = cnt + smax;                    // 4*smax (counts, then positions; then best)
   int* nrx = child + 4 * smax;                // smax
@@ -1303,6 +1303,7 @@ __device__ __forceinline__ void qt_body(QT_KERNEL_ARGS) {
     const bool finish = (newS >= L.N) || (s_flag == 0);
     __syncthreads();
     if (finish) break;
+#ifdef QT_COPY_NODES  // profiling variant: copy the new node arrays back (one more barrier per pass)
     for (int i = tid; i < newS; i += 256) {
       rx[i] = nrx[i];
       ry[i] = nry[i];
@@ -1310,6 +1311,15 @@ __device__ __forceinline__ void qt_body(QT_KERNEL_ARGS) {
     }
     S = newS;
     __syncthreads();
+#else
+    // ping-pong: the new node arrays become the current ones (every read of
+    // the old ones is before the barrier above; the next pass writes the
+    // other set only after its first barrier)
+    int* t = rx; rx = nrx; nrx = t;
+    t = ry; ry = nry; nry = t;
+    t = cnt; cnt = ncnt; ncnt = t;
+    S = newS;
+#endif
   }
 #if defined(QT_PROBE_STOP) && QT_PROBE_STOP == 2  // profiling only: gather + passes
   if (tid == 0) lcount[(size_t)f * nlevels + l] = 0;
