@@ -67,3 +67,26 @@ def test_bench_two_ranks_pipelined_on_one_gpu():
         assert r.returncode == 0, r.stderr[-3000:]
         d = json.loads(r.stdout.strip().splitlines()[-1])
         assert d["n_gpus"] == 2 and d["value"] > 0 and d["serial"]["value"] > 0
+
+
+@pytest.mark.gpu
+def test_bench_c4_host_fed_and_latency_legs():
+    # the c4 line's extra legs at a small batch: frames fed from pinned host
+    # memory over two copy streams must give the resident run's keypoint
+    # counts with every keypoint row returned; the drop-in latency leg (C ABI
+    # and the reference-shaped compat operator()) reports every call site
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--workload", "c4", "--batch", "8",
+                        "--steps", "2", "--warmup", "1", "--no-cpu-baseline"],
+                       env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    hf = d["host_fed"]
+    assert hf["value"] > 0 and hf["counts_equal_resident_run"] and hf["rows_cover_all_keypoints"]
+    assert hf["h2d_streams"] == 2
+    lat = d["latency"]
+    for k in ("extract_640x480", "extract_1920x1080", "search_by_bow_2000x2000"):
+        assert lat[k]["p50_us"] > 0 and lat[k]["p99_us"] >= lat[k]["p50_us"]
+    co = lat["compat_operator_1920x1080"]
+    assert co["operator_with_mvImagePyramid"]["checksum"] != 0
+    assert co["operator_with_mvImagePyramid"]["keypoints"] == co["operator_no_pyramid"]["keypoints"]
