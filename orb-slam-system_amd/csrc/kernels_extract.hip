@@ -1557,7 +1557,7 @@ __device__ __forceinline__ void brief_commit(const BriefRegs& R, uint32_t* P, in
 #define OB_WPE 7
 #endif
 #ifndef OB_PROBE
-#define OB_PROBE 0 /* profiling only: 1 / 2 / 3 skip the horizontal pass / IC_Angle sums / samples */
+#define OB_PROBE 0 /* profiling only: 1 / 2 / 3 skip the horizontal pass / IC_Angle sums / samples, 4 / 5 the fastAtan2 + sincos chain / sincos */
 #endif
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OB_WPE))) void k_orient_brief(
     const uint8_t* __restrict__ frames, size_t fstride, size_t rstride,
@@ -1736,10 +1736,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OB_WPE))) v
   // wave sums (uniform: scalar angle / sincos table) without LDS round trips
   m10 = wave_sum(m10);
   m01 = wave_sum(m01);
+#if OB_PROBE == 4  // profiling only: no fastAtan2 / sincos chain (wrong descriptors)
+  (void)exk0, (void)exk1;
+  const float angle = (float)m01 * 1e-3f;
+  float sn = (float)m10 * 1e-6f, cs = 1.0f - sn;
+#elif OB_PROBE == 5  // profiling only: fastAtan2 but no sincos (wrong descriptors)
+  (void)exk0, (void)exk1;
+  const float angle = fast_atan2((float)m01, (float)m10);
+  float sn = angle * 1e-3f, cs = 1.0f - sn;
+#else
   const float angle = fast_atan2((float)m01, (float)m10);
   const float factorPI = (float)(3.1415926535897932384626433832795 / 180.f);
   float sn, cs;
   brief_sincos(angle * factorPI, exk0, exk1, &sn, &cs);
+#endif
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
