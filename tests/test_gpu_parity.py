@@ -109,6 +109,29 @@ def test_extract_scales_match_oracle(gpu, oracle, w, h, nf, sc, L, kind, idx):
     assert np.array_equal(d, rd), "descriptors differ"
 
 
+# other FAST thresholds (ORBextractor.cc:330-331 runs iniThFAST first and
+# minThFAST only for cells left empty): a lower pair, minThFAST above
+# iniThFAST (the retry then looks for stronger corners), and equal ones
+THRESHOLD_CASES = [
+    # (w, h, nfeatures, nlevels, iniThFAST, minThFAST, kind, frame_idx)
+    (640, 480, 1000, 8, 12, 5, "rects", 50),
+    (1241, 376, 2000, 8, 9, 15, "noise", 51),
+    (752, 480, 1200, 8, 7, 7, "pan", 52),
+    (1920, 1080, 2000, 8, 31, 10, "pan", 53),
+]
+
+
+@pytest.mark.parametrize("w,h,nf,L,ini,mn,kind,idx", THRESHOLD_CASES)
+def test_extract_thresholds_match_oracle(gpu, oracle, w, h, nf, L, ini, mn, kind, idx):
+    img = synth.frame(w, h, idx, kind)
+    ref = oracle.Extractor(nf, 1.2, L, ini, mn, cell_guard="empty")
+    rk, rd = ref.extract(img)
+    ex = gpu.Extractor(nf, 1.2, L, ini, mn, cell_guard="empty")
+    k, d = ex.extract(img)
+    _cmp_kps(k, rk, "keypoints")
+    assert np.array_equal(d, rd), "descriptors differ"
+
+
 def test_strict_guard_1080p_raises(gpu):
     ex = gpu.Extractor(2000, 1.2, 8, 20, 7, cell_guard="strict")
     with pytest.raises(gpu.OrbxError) as e:
