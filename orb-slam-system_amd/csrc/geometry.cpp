@@ -165,6 +165,18 @@ static int chain_1d(const Plan& P, const std::vector<int>& lev, bool isx, int T,
   for (int t = 0; t < nt; ++t) {
     int clo = out[(size_t)(ns - 1) * nt + t].plo, chi = out[(size_t)(ns - 1) * nt + t].phi;
     for (int s = ns - 1; s >= 1; --s) {
+      if (isx) {
+        /* every 4-pixel group holding an owned pixel is computed whole (or
+         * ends past the level's last column): k_pyramid stores such groups as
+         * one dword, the bytes it does not own carrying the same values the
+         * owner writes (the LDS pitch is unchanged: clo & ~3 and the rounded
+         * chi stay; only the footprint in level s-1 grows) */
+        const Iv& o = out[(size_t)s * nt + t];
+        if (o.phi > o.plo) {
+          clo = std::min(clo, o.plo & ~3);
+          chi = std::max(chi, std::min((o.phi + 3) & ~3, size(s)));
+        }
+      }
       out[(size_t)s * nt + t].clo = clo;
       out[(size_t)s * nt + t].chi = chi;
       int flo = 1 << 30, fhi = -1;

@@ -32,6 +32,7 @@ int main(int argc, char** argv) {
   if (rc) { printf("rc %d\n", rc); return 3; }
   std::vector<uint8_t> pyr(P.pyr_bytes + 16, 0xCD);
   std::vector<uint8_t> owner(P.pyr_bytes + 16, 0);
+  std::vector<std::pair<size_t, uint8_t>> shadow;  // non-owned bytes of edge dwords
   for (const PyrSeg& g : P.segs) {
     if (g.lds_a + g.lds_b + g.lds_xl + g.lds_yl > ORBX_PYR_LDS_MAX) fail("lds total", 0, 0);
     for (int ty = 0; ty < g.nty; ++ty)
@@ -88,7 +89,12 @@ int main(int argc, char** argv) {
                 if (v < 0) fail("uninit", rr + cay, cc + cax);
                 return v;
               };
-              if (c < X[0] || c >= X[1]) continue;  // pad columns: garbage in the kernel
+              const int gx0 = c & ~3;  // k_pyramid stores a group with an owned pixel as one dword
+              const bool any_x = gx0 + 4 > X[2] && gx0 < X[3];
+              if (c < X[0] || c >= X[1]) {  // pad columns: garbage in the kernel
+                if (y >= Y[2] && y < Y[3] && any_x && c < g.w[s]) fail("unsafe dword", y, c);
+                continue;
+              }
               const int d0 = rd(ry0, sx) * a0 + rd(ry0, sx1) * a1;
               const int d1 = rd(ry1, sx) * a0 + rd(ry1, sx1) * a1;
               const int v = (((b0 * (d0 >> 4)) >> 16) + ((b1 * (d1 >> 4)) >> 16) + 2) >> 2;
@@ -98,6 +104,9 @@ int main(int argc, char** argv) {
                 if (owner[o]) fail("double write", y, c);
                 owner[o] = 1;
                 pyr[o] = (uint8_t)v;
+              } else if (y >= Y[2] && y < Y[3] && any_x && c < g.w[s]) {
+                // a byte of an edge group this tile does not own: must equal its owner's
+                shadow.push_back({g.off[s] + (size_t)y * g.pitch[s] + c, (uint8_t)v});
               }
             }
           }
@@ -110,6 +119,8 @@ int main(int argc, char** argv) {
         }
       }
   }
+  for (const auto& sw : shadow)
+    if (pyr[sw.first] != sw.second) fail("edge dword byte differs from its owner", (int)(sw.first >> 16), (int)(sw.first & 0xFFFF));
   FILE* o = fopen(argv[7], "wb");
   for (int l = 1; l < prm.nlevels; ++l) {
     const LevelInfo& lv = P.levels[l];
