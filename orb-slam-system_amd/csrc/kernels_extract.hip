@@ -313,7 +313,10 @@ __global__ __launch_bounds__(256) void k_pyramid(const uint8_t* __restrict__ fra
             if (r >= nrows) break;
             const int y = Y.x + r;
             *reinterpret_cast<uint32_t*>(nxt + r * dpitch + 4 * cg) = packed[u];
-            if (PYR_STORE_ON && y >= Y.z && y < Y.w && any_x) {
+            // every computed row, also the ones another tile owns: computed
+            // rows are exact, so their bytes equal the owner's (benign; no
+            // per-row ownership test: 0.679 -> 0.666 ms at c4)
+            if (PYR_STORE_ON && any_x) {
               uint8_t* o = gdst + (uint32_t)(y * gp + gx0);  // a level is < 4 GB
               // the whole group, also at the owned interval's edges: the
               // planner computes every group holding an owned pixel whole, so

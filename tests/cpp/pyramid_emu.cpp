@@ -92,7 +92,7 @@ int main(int argc, char** argv) {
               const int gx0 = c & ~3;  // k_pyramid stores a group with an owned pixel as one dword
               const bool any_x = gx0 + 4 > X[2] && gx0 < X[3];
               if (c < X[0] || c >= X[1]) {  // pad columns: garbage in the kernel
-                if (y >= Y[2] && y < Y[3] && any_x && c < g.w[s]) fail("unsafe dword", y, c);
+                if (any_x && c < g.w[s]) fail("unsafe dword", y, c);
                 continue;
               }
               const int d0 = rd(ry0, sx) * a0 + rd(ry0, sx1) * a1;
@@ -104,8 +104,9 @@ int main(int argc, char** argv) {
                 if (owner[o]) fail("double write", y, c);
                 owner[o] = 1;
                 pyr[o] = (uint8_t)v;
-              } else if (y >= Y[2] && y < Y[3] && any_x && c < g.w[s]) {
-                // a byte of an edge group this tile does not own: must equal its owner's
+              } else if (any_x && c < g.w[s]) {
+                // a byte k_pyramid stores that this tile does not own (edge
+                // group, or a computed row of another tile): must equal its owner's
                 shadow.push_back({g.off[s] + (size_t)y * g.pitch[s] + c, (uint8_t)v});
               }
             }
