@@ -161,8 +161,10 @@ __device__ __forceinline__ uint32_t as_u32(us2 x) { return __builtin_bit_cast(ui
 // dst = (((b0*(D0>>4))>>16) + ((b1*(D1>>4))>>16) + 2) >> 2.
 // Workgroup = one tile of the segment's last level.  The source region is
 // staged in LDS once; every finer level is computed into the other LDS
-// buffer (ping-pong) and only the owned interval goes to HBM, so each level
-// is written once and the intermediate levels are never re-read from HBM.
+// buffer (ping-pong); the tile's computed rows of every 4-pixel group that
+// holds an owned column go to HBM as dwords (bytes it does not own are exact
+// recomputations, equal to their owner's), and the intermediate levels are
+// never re-read from HBM.
 // Thread = 4 consecutive columns (dword in LDS and HBM) of a row.
 // ---------------------------------------------------------------------------
 #ifndef PYR_U
