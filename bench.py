@@ -81,6 +81,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=40.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-latency", action="store_true")
+    ap.add_argument("--pyramid", choices=["auto", "tiles", "stream"], default="auto",
+                    help="pyramid kernel (orbx_plan_set_options; identical results)")
     ap.add_argument("--serial", action="store_true",
                     help="time only the serial step (no extraction/matching overlap across steps)")
     ap.add_argument("--traffic", default="", help="PMC traffic summary (default profiles/traffic_<workload>.json)")
@@ -572,6 +574,7 @@ def main_mono(args, wl):
     B, W, H = args.batch, wl["W"], wl["H"]
     prm = orbx.params(wl["nfeatures"], 1.2, wl["nlevels"], 20, 7, wl["guard"])
     plan = orbx.Plan(prm, W, H, B, device=local)
+    plan.set_options(pyramid=args.pyramid)
     kcap = plan.kcap
     match = wl["match"]
     mp = orbx.MatchPlan(B, kcap, wl["topn"], device=local, zero_tail=True) if match else None
@@ -750,6 +753,8 @@ def main_c5(args, wl):
     prm = orbx.params(wl["nfeatures"], 1.2, wl["nlevels"], 20, 7)
     pl = orbx.Plan(prm, W, H, B, device=local)
     pr = orbx.Plan(prm, W, H, B, device=local)
+    pl.set_options(pyramid=args.pyramid)
+    pr.set_options(pyramid=args.pyramid)
     sp = orbx.StereoPlan(pl, device=local)
     kcap = pl.kcap
     mp = orbx.MatchPlan(B, kcap, wl["topn"], device=local, zero_tail=True)

@@ -177,6 +177,29 @@ int orbx_plan_check(orbx_plan* plan, void* stream);
  * capacity so the scan runs on ordinary frames. */
 int orbx_plan_debug_counters(orbx_plan* plan, int* fast_overflow_strips);
 
+/* Kernel-path options of a plan (default 0 = automatic; persistent).  Every
+ * path gives bit-identical results; they differ in speed only.
+ *   ORBX_PLAN_PYR_TILES   the pyramid by k_pyramid (2-D tiles of the level
+ *                         chain, halo recompute) for every batch size;
+ *   ORBX_PLAN_PYR_STREAM  the row-streaming pyramid (k_pyr_stream, one
+ *                         workgroup per frame) for every batch size.
+ * Automatic: k_pyr_stream for batches of >= 64 frames when the planner
+ * could schedule it (no exact-2x level, rings within the LDS budget), else
+ * k_pyramid.  Returns ORBX_ERR_ARG for unknown flags or both at once,
+ * ORBX_ERR_UNSUPPORTED for ORBX_PLAN_PYR_STREAM on a plan the streaming
+ * schedule does not cover (the options are then unchanged). */
+#define ORBX_PLAN_PYR_TILES 1
+#define ORBX_PLAN_PYR_STREAM 2
+int orbx_plan_set_options(orbx_plan* plan, int flags);
+
+/* mvImagePyramid[level] of frame `frame` of the last orbx_plan_extract on
+ * this plan, copied to host rows of dst_stride bytes (synchronises `stream`,
+ * which must be the stream of that extraction or ordered after it; NULL =
+ * the default stream).  Level 0 (and levels aliasing it) are the caller's
+ * frame and are not held by the plan: ORBX_ERR_ARG. */
+int orbx_plan_level(orbx_plan* plan, int frame, int level, uint8_t* dst, size_t dst_stride,
+                    int* width, int* height, void* stream);
+
 /* Per-stage device timing (HIP events around every launch of a stage). */
 int orbx_stage_count(void);
 const char* orbx_stage_name(int stage);

@@ -33,6 +33,13 @@ __global__ void k_quadtree_j6(const LevelInfo*, const CellInfo*, const uint32_t*
 __global__ void k_orient_brief(const uint8_t*, size_t, size_t, const uint8_t*, size_t,
                                const BriefArgs, const uint32_t*, size_t, const int*,
                                orbx_keypoint*, uint8_t*, int*, const uint32_t*, int);
+#define PS_DECL(name)                                                                                 \
+  __global__ void name(const uint8_t*, size_t, size_t, uint8_t*, size_t, const PyrStream, const uint2*, \
+                       const int*, const uint4*, const uint2*, int)
+PS_DECL(k_pyr_stream_1024);
+PS_DECL(k_pyr_stream_512);
+PS_DECL(k_pyr_stream_256);
+#undef PS_DECL
 __global__ void k_synth(uint8_t*, int, int, size_t, int, int);
 __global__ void k_selftest_sincos(const float*, int, float*);
 __global__ void k_selftest_sincos_range(uint32_t, int, float*);
@@ -130,7 +137,8 @@ static void plan_free(orbx_plan* p) {
   hipSetDevice(p->device);
   void* bufs[] = {p->d_lv, p->d_cells, p->d_strips, p->d_xofs, p->d_xofs1, p->d_yofs, p->d_alpha, p->d_beta,
                   p->d_pyr, p->d_blur, p->d_slots, p->d_ccount, p->d_qkeys, p->d_qout, p->d_qperm,
-                  p->d_qnode, p->d_lcount, p->d_err, p->d_pyr_xs, p->d_pyr_ys, p->d_pyr_bo, p->d_pyr_blob};
+                  p->d_qnode, p->d_lcount, p->d_err, p->d_pyr_xs, p->d_pyr_ys, p->d_pyr_bo, p->d_pyr_blob,
+                  p->d_ps_tasks, p->d_ps_xlut, p->d_ps_ylut, p->d_ps_tick_end};
   for (void* b : bufs)
     if (b) hipFree(b);
   p->timer.release();
@@ -165,10 +173,15 @@ extern "C" int orbx_plan_create(const orbx_params* prm, int width, int height, i
   int ndev = orbx_device_count();
   if (device < 0 || device >= ndev) return ORBX_ERR_NO_DEVICE;
   orbx_plan* p = new orbx_plan();
+#ifdef ORBX_PROFILING
+  /* profiling builds only (tools/variant.sh): kernel phase early exits, grid
+   * divisors, chunked passes; a release library never reads these (an
+   * inherited environment cannot change its results) */
   if (const char* e = getenv("ORBX_DEBUG_STOP")) p->dbg = atoi(e);
   if (const char* e = getenv("ORBX_DEBUG_OBDIV")) p->ob_div = atoi(e);
   if (const char* e = getenv("ORBX_CHUNK")) p->chunk = atoi(e);
-  if (const char* e = getenv("ORBX_DEBUG_OVERLAP")) p->overlap = atoi(e); /* profiling: FAST level 0 beside the pyramid */
+  if (const char* e = getenv("ORBX_DEBUG_OVERLAP")) p->overlap = atoi(e); /* FAST level 0 beside the pyramid */
+#endif
   p->fs_ccap = FS_CCAP;
   /* testing only: a smaller FAST corner list, so the overflow path runs */
   if (const char* e = getenv("ORBX_DEBUG_CCAP")) p->fs_ccap = std::max(0, std::min(FS_CCAP, atoi(e)));
@@ -185,7 +198,10 @@ extern "C" int orbx_plan_create(const orbx_params* prm, int width, int height, i
       set_max_dynamic_lds((const void*)k_quadtree_j6, device) ||
       set_max_dynamic_lds((const void*)k_fast_strips, device) ||
       set_max_dynamic_lds((const void*)k_fast_strips_p288, device) ||
-      set_max_dynamic_lds((const void*)k_pyramid, device)) { plan_free(p); return ORBX_ERR_HIP; }
+      set_max_dynamic_lds((const void*)k_pyramid, device) ||
+      set_max_dynamic_lds((const void*)k_pyr_stream_1024, device) ||
+      set_max_dynamic_lds((const void*)k_pyr_stream_512, device) ||
+      set_max_dynamic_lds((const void*)k_pyr_stream_256, device)) { plan_free(p); return ORBX_ERR_HIP; }
   if (p->overlap && (hipStreamCreateWithFlags(&p->s_aux, hipStreamNonBlocking) != hipSuccess ||
                      hipEventCreateWithFlags(&p->ev_aux0, hipEventDisableTiming) != hipSuccess ||
                      hipEventCreateWithFlags(&p->ev_aux1, hipEventDisableTiming) != hipSuccess)) {
@@ -246,7 +262,9 @@ extern "C" int orbx_plan_create(const orbx_params* prm, int width, int height, i
       upload(&p->d_xofs1, P.xofs1, us) || upload(&p->d_yofs, P.yofs, us) ||
       upload(&p->d_alpha, P.alpha, us) || upload(&p->d_beta, P.beta, us) ||
       upload(&p->d_pyr_xs, P.pyr_xs, us) || upload(&p->d_pyr_ys, P.pyr_ys, us) ||
-      upload(&p->d_pyr_bo, P.pyr_bo, us) || upload(&p->d_pyr_blob, P.pyr_blob, us)) {
+      upload(&p->d_pyr_bo, P.pyr_bo, us) || upload(&p->d_pyr_blob, P.pyr_blob, us) ||
+      upload(&p->d_ps_tasks, P.ps_tasks, us) || upload(&p->d_ps_xlut, P.ps_xlut, us) ||
+      upload(&p->d_ps_ylut, P.ps_ylut, us) || upload(&p->d_ps_tick_end, P.ps_tick_end, us)) {
     plan_free(p);
     return ORBX_ERR_HIP;
   }
@@ -331,9 +349,28 @@ static int extract_pass(orbx_plan* p, const uint8_t* frames, int n, size_t fstri
     fast_launch(0, P.nstrips_l0, p->s_aux);
     if (hipEventRecord(p->ev_aux1, p->s_aux) != hipSuccess) return ORBX_ERR_HIP;
   }
-  // K1 pyramid
+  // K1 pyramid: row-streaming (one workgroup per frame) for batches, or the
+  // tile chain (many small workgroups per frame) for single frames
   p->timer.begin(ORBX_STAGE_RESIZE, s);
+  const bool stream = P.ps_ok && !(p->options & ORBX_PLAN_PYR_TILES) &&
+                      (n >= 64 || (p->options & ORBX_PLAN_PYR_STREAM));
+  if (stream) {
+    // waves per frame: 16 up to 256 frames (one workgroup per CU), fewer for
+    // larger batches (several frames per CU)
+    const int nt = n > 512 ? 256 : n > 256 ? 512 : 1024;
+    const int al16 = ((reinterpret_cast<uintptr_t>(frames) | fstride | rstride) & 15) == 0;
+    auto ps_launch = [&](auto kern) {
+      hipLaunchKernelGGL(kern, dim3((unsigned)n), dim3((unsigned)nt), P.ps.lds_bytes, s, frames, fstride,
+                         rstride, d_pyr, p->pyr_stride, P.ps, reinterpret_cast<const uint2*>(p->d_ps_tasks),
+                         p->d_ps_tick_end, reinterpret_cast<const uint4*>(p->d_ps_xlut),
+                         reinterpret_cast<const uint2*>(p->d_ps_ylut), al16);
+    };
+    if (nt == 1024) ps_launch(k_pyr_stream_1024);
+    else if (nt == 512) ps_launch(k_pyr_stream_512);
+    else ps_launch(k_pyr_stream_256);
+  }
   for (const PyrSeg& g : P.segs) {
+    if (stream) break;
     if (g.area) {
       hipLaunchKernelGGL(k_pyr_area2, dim3((unsigned)((g.w[1] + 1023) / 1024), (unsigned)g.h[1], (unsigned)n),
                          dim3(256), 0, s, frames, fstride, rstride, d_pyr, p->pyr_stride, g);
@@ -430,6 +467,33 @@ extern "C" int orbx_plan_check(orbx_plan* p, void* stream) {
     if (err & ORBX_DEVERR_QUADTREE) return ORBX_ERR_QUADTREE;
     return ORBX_ERR_CAPACITY;
   }
+  return ORBX_OK;
+}
+
+extern "C" int orbx_plan_set_options(orbx_plan* p, int flags) {
+  if (!p || (flags & ~(ORBX_PLAN_PYR_TILES | ORBX_PLAN_PYR_STREAM)) ||
+      (flags & (ORBX_PLAN_PYR_TILES | ORBX_PLAN_PYR_STREAM)) == (ORBX_PLAN_PYR_TILES | ORBX_PLAN_PYR_STREAM))
+    return ORBX_ERR_ARG;
+  if ((flags & ORBX_PLAN_PYR_STREAM) && !p->P.ps_ok) return ORBX_ERR_UNSUPPORTED;
+  p->options = flags;
+  return ORBX_OK;
+}
+
+extern "C" int orbx_plan_level(orbx_plan* p, int frame, int level, uint8_t* dst, size_t dst_stride, int* width,
+                               int* height, void* stream) {
+  if (!p || frame < 0 || frame >= p->max_batch || level < 0 || level >= p->P.params.nlevels) return ORBX_ERR_ARG;
+  const LevelInfo& L = p->P.levels[level];
+  if (width) *width = L.w;
+  if (height) *height = L.h;
+  if (L.unique == 0) return ORBX_ERR_ARG;
+  if (!dst) return ORBX_OK;
+  if (dst_stride < (size_t)L.w) return ORBX_ERR_ARG;
+  ORBX_TRY(hipSetDevice(p->device));
+  hipStream_t s = (hipStream_t)stream;
+  const uint8_t* src = p->d_pyr + (size_t)frame * p->pyr_stride + p->P.levels[L.unique].pyr_off;
+  ORBX_TRY(hipMemcpy2DAsync(dst, dst_stride, src, (size_t)L.pitch, (size_t)L.w, (size_t)L.h,
+                            hipMemcpyDeviceToHost, s));
+  ORBX_TRY(hipStreamSynchronize(s));
   return ORBX_OK;
 }
 

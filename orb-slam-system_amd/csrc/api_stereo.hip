@@ -89,7 +89,9 @@ static int splan_create(const orbx_plan* g, int max_batch, orbs_plan** out) {
   const int span = (int)std::ceil(4.0 * smax) + 3;
   A.rcap = P.kcap * span;
   sp->waves = std::max(4, std::min(P.kcap, P.params.nfeatures + 256));
-  if (const char* e = getenv("ORBX_DEBUG_SMDIV")) sp->sm_div = atoi(e); /* profiling only */
+#ifdef ORBX_PROFILING
+  if (const char* e = getenv("ORBX_DEBUG_SMDIV")) sp->sm_div = atoi(e); /* profiling builds only */
+#endif
   hipSetDevice(sp->device);
   const size_t B = (size_t)max_batch;
   const size_t K = (size_t)std::max(P.kcap, 1);

@@ -332,9 +332,11 @@ static int plan_pyramid(Plan& P) {
   static const int tiles[][2] = {{64, 16}, {128, 16}, {128, 8}, {64, 8}, {64, 32}, {32, 16},
                                  {16, 16}, {16, 8}, {8, 8}};
   int k0 = 0; /* ORBX_DEBUG_PYR_TILE=k: start the tile search at tiles[k] (profiling only) */
-  if (const char* e = getenv("ORBX_DEBUG_PYR_TILE")) k0 = std::min(std::max(atoi(e), 0), 8);
   size_t maxseg = 1 << 20; /* ORBX_DEBUG_PYR_MAXSEG=n: at most n levels per segment, source included (profiling only) */
+#ifdef ORBX_PROFILING
+  if (const char* e = getenv("ORBX_DEBUG_PYR_TILE")) k0 = std::min(std::max(atoi(e), 0), 8);
   if (const char* e = getenv("ORBX_DEBUG_PYR_MAXSEG")) maxseg = (size_t)std::max(atoi(e), 2);
+#endif
   size_t i = 1;
   while (i < uniq.size()) {
     if (P.area2[uniq[i]]) {  /* exact 2x: its own launch of k_pyr_area2 */
@@ -377,6 +379,164 @@ static int plan_pyramid(Plan& P) {
     if (!done) return ORBX_ERR_UNSUPPORTED; /* level ratio too large for one tile */
   }
   return ORBX_OK;
+}
+
+/* ---- row-streaming pyramid (k_pyr_stream) ------------------------------
+ * Same arithmetic and coefficient packing as k_pyramid's blobs (origin =
+ * column 0 of the full-width source row).  The schedule: level-0 rows
+ * [r0 k, r0 (k+1)) arrive in tick k; level j produces, in tick k, every row
+ * whose two source rows were produced before tick k.  A level's ring holds
+ * the rows live in any tick: the ones written in it and the ones its
+ * successor reads in it, so a slot is never rewritten while a later tick
+ * still reads it (rows read at tick k are >= that tick's lowest read row). */
+bool plan_pyr_stream(Plan& P, int r0, int rpt) {
+  P.ps_ok = false;
+  P.ps_tasks.clear();
+  P.ps_tick_end.clear();
+  P.ps_xlut.clear();
+  P.ps_ylut.clear();
+  if (r0 < 1 || rpt < 1 || rpt > 255) return false;
+  std::vector<int> ch;
+  for (int l = 0; l < (int)P.levels.size(); ++l)
+    if (P.levels[l].unique == l) ch.push_back(l);
+  const int n = (int)ch.size();
+  if (n < 2 || n > ORBX_PS_MAXL) return false;
+  for (int j = 1; j < n; ++j)
+    if (P.area2[ch[j]] || P.levels[ch[j]].src_level != ch[j - 1]) return false;
+  PyrStream S;
+  memset(&S, 0, sizeof(S));
+  S.nl = n;
+  S.r0 = r0;
+  for (int j = 0; j < n; ++j) {
+    const LevelInfo& lv = P.levels[ch[j]];
+    S.lev[j] = ch[j];
+    S.w[j] = lv.w;
+    S.h[j] = lv.h;
+    S.ng[j] = (lv.w + 3) >> 2;
+    if (j > 0) {
+      S.gpitch[j] = lv.pitch;
+      S.goff[j] = lv.pyr_off;
+      if (lv.h > 8191 || (S.ng[j] + 63) / 64 > 127) return false; /* task word fields */
+    }
+  }
+  /* column LUT: uint2 per column, 4 per group (build_blobs layout, origin 0) */
+  for (int j = 1; j < n; ++j) {
+    const LevelInfo& lv = P.levels[ch[j]];
+    S.xl[j] = (int)(P.ps_xlut.size() / 2);
+    for (int g = 0; g < S.ng[j]; ++g) {
+      int glo = 0;
+      for (int k = 0; k < 4; ++k) {
+        const int d = std::min(4 * g + k, lv.w - 1);
+        const int lo = P.xofs[lv.lut_x + d], hi = P.xofs1[lv.lut_x + d];
+        const int16_t* cf = &P.alpha[2 * (lv.lut_x + d)];
+        if (cf[0] < 0 || cf[0] > 4095 || cf[1] < 0 || cf[1] > 4095) return false;
+        if (k == 0) glo = lo;
+        if (hi - glo > 7 || lo < glo) return false;
+        if (k == 0)
+          P.ps_xlut.push_back((uint32_t)lo | ((uint32_t)(hi - lo) << 16));
+        else
+          P.ps_xlut.push_back((uint32_t)(lo - glo) | 0x0C00u | ((uint32_t)(hi - glo) << 16) | 0x0C000000u);
+        P.ps_xlut.push_back((uint32_t)(uint16_t)cf[0] | ((uint32_t)(uint16_t)cf[1] << 16));
+      }
+    }
+  }
+  /* source rows of destination row y of chain level j (clamped as cv::resize) */
+  auto src_rows = [&](int j, int y, int& s0, int& s1) {
+    const int sy = P.yofs[P.levels[ch[j]].lut_y + y];
+    s0 = std::min(std::max(sy, 0), S.h[j - 1] - 1);
+    s1 = std::min(std::max(sy + 1, 0), S.h[j - 1] - 1);
+  };
+  /* schedule */
+  std::vector<int> nxt(n, 0), span(n, 0);
+  struct Tick { std::vector<int> a, b; };
+  std::vector<Tick> ticks;
+  for (int k = 0;; ++k) {
+    bool done = true;
+    for (int j = 0; j < n; ++j) done = done && nxt[j] >= S.h[j];
+    if (done) break;
+    if (k > 4 * S.h[0] + 64) return false; /* no progress: cannot happen for a chain */
+    Tick t;
+    t.a = nxt;
+    t.b = nxt;
+    t.b[0] = std::min(S.h[0], r0 * (k + 1));
+    t.a[0] = std::min(S.h[0], r0 * k);
+    std::vector<int> readlo(n, 1 << 30);
+    for (int j = 1; j < n; ++j) {
+      int y = nxt[j];
+      while (y < S.h[j]) {
+        int s0, s1;
+        src_rows(j, y, s0, s1);
+        if (std::max(s0, s1) >= nxt[j - 1]) break; /* produced before this tick? */
+        readlo[j - 1] = std::min(readlo[j - 1], s0);
+        ++y;
+      }
+      t.b[j] = y;
+    }
+    for (int j = 0; j < n; ++j) {
+      const int lo = std::min(readlo[j], t.a[j]);
+      span[j] = std::max(span[j], t.b[j] - lo);
+    }
+    nxt = t.b;
+    ticks.push_back(t);
+  }
+  S.nticks = (int)ticks.size();
+  /* LDS: column LUT, then one ring per chain level, 16 B slack (the
+   * horizontal pass reads up to 12 bytes past a row), then the ticket */
+  long long off = ((long long)P.ps_xlut.size() * 4 + 15) & ~15LL;
+  S.lut_lds = 0;
+  S.lut_bytes = (int)off;
+  for (int j = 0; j < n; ++j) {
+    S.rrows[j] = std::max(span[j], 1);
+    if (S.rrows[j] > 255) return false;
+    S.rpitch[j] = (S.w[j] + 15) & ~15;
+    S.roff[j] = (int)off;
+    off += (long long)S.rrows[j] * S.rpitch[j];
+  }
+  off += 16 + 16;
+  if (off > ORBX_PS_LDS_MAX) return false;
+  S.lds_bytes = (int)off;
+  /* row LUT: ring slots of both source rows and of the destination row,
+   * coefficient pair; the kernel's vertical step needs b0, b1 < 4096 */
+  for (int j = 1; j < n; ++j) {
+    const LevelInfo& lv = P.levels[ch[j]];
+    S.yl[j] = (int)(P.ps_ylut.size() / 2);
+    for (int y = 0; y < S.h[j]; ++y) {
+      int s0, s1;
+      src_rows(j, y, s0, s1);
+      const int16_t* cf = &P.beta[2 * (lv.lut_y + y)];
+      if (cf[0] < 0 || cf[0] > 4095 || cf[1] < 0 || cf[1] > 4095) return false;
+      P.ps_ylut.push_back((uint32_t)(s0 % S.rrows[j - 1]) | ((uint32_t)(s1 % S.rrows[j - 1]) << 8) |
+                          ((uint32_t)(y % S.rrows[j]) << 16));
+      P.ps_ylut.push_back((uint32_t)(uint16_t)cf[0] | ((uint32_t)(uint16_t)cf[1] << 16));
+    }
+  }
+  /* tasks: per tick, every (level, 64-group chunk, run of <= rpt rows) of the
+   * rows produced in it, largest runs first (the ticket hands them out in
+   * this order, so the tick's tail is made of small tasks) */
+  for (const Tick& t : ticks) {
+    std::vector<std::pair<int, uint64_t>> tk;
+    for (int j = 1; j < n; ++j) {
+      const int nch = (S.ng[j] + 63) / 64;
+      for (int y0 = t.a[j]; y0 < t.b[j]; y0 += rpt) {
+        const int nr = std::min(rpt, t.b[j] - y0);
+        for (int c = 0; c < nch; ++c) {
+          const uint32_t x = ORBX_PS_RESIZE | ((uint32_t)j << 4) | ((uint32_t)c << 9) | ((uint32_t)nr << 16);
+          tk.push_back({-nr * 64 * 1024 + j, ((uint64_t)x << 32) | (uint32_t)y0});
+        }
+      }
+    }
+    std::stable_sort(tk.begin(), tk.end(), [](const std::pair<int, uint64_t>& a, const std::pair<int, uint64_t>& b) {
+      return a.first < b.first;
+    });
+    for (auto& e : tk) {
+      P.ps_tasks.push_back((uint32_t)(e.second >> 32));
+      P.ps_tasks.push_back((uint32_t)e.second);
+    }
+    P.ps_tick_end.push_back((int)(P.ps_tasks.size() / 2));
+  }
+  P.ps = S;
+  P.ps_ok = true;
+  return true;
 }
 
 int plan_geometry(const orbx_params& p, int width, int height, Plan& P) {
@@ -580,6 +740,10 @@ int plan_geometry(const orbx_params& p, int width, int height, Plan& P) {
   }
   P.geo.pixels = px;
   P.geo.bytes_pyr_fast = bytes;
+  /* row-streaming pyramid: the longest tick whose rings fit the LDS budget */
+  static const int ticks[] = {8, 6, 4, 3, 2, 1};
+  for (int r0 : ticks)
+    if (plan_pyr_stream(P, r0, 4)) break;
   return ORBX_OK;
 }
 

@@ -143,6 +143,38 @@ struct PyrSeg {
   long long off[ORBX_MAX_LEVELS]; /* pyr offset; -1 = the caller's frame (level 0) */
 };
 
+/* row-streaming pyramid (k_pyr_stream): one workgroup per frame walks the
+ * frame top to bottom in ticks.  Tick k: the loader wave brings level-0 rows
+ * [r0 k, r0 (k+1)) into their LDS ring; the worker waves take the tick's
+ * tasks (a level, a chunk of 64 four-pixel groups, a run of destination
+ * rows) by an LDS ticket and compute those rows from source rows that earlier
+ * ticks left in the source level's ring; one barrier per tick.  Every level
+ * row is computed once (no halo recompute) and written to HBM once; source
+ * rows' horizontal passes are reused across consecutive destination rows of
+ * a task.  Chain index j: 0 = level 0 (the caller's frame), j >= 1 the
+ * unique levels in order. */
+#define ORBX_PS_MAXL 16
+#define ORBX_PS_LDS_MAX (150 * 1024)
+struct PyrStream {
+  int nl;         /* chain length incl. level 0 */
+  int nticks;     /* barriers = ticks */
+  int r0;         /* level-0 rows per tick */
+  int lut_lds;    /* LDS byte offset of the column LUT (uint2 entries, 4 per group) */
+  int lut_bytes;  /* its size (16-B multiple) */
+  int lds_bytes;  /* total dynamic LDS, the ticket word included */
+  int w[ORBX_PS_MAXL], h[ORBX_PS_MAXL], ng[ORBX_PS_MAXL]; /* ng = four-pixel groups per row */
+  int rrows[ORBX_PS_MAXL];  /* ring rows (row y lives in slot y % rrows) */
+  int rpitch[ORBX_PS_MAXL]; /* ring row pitch, 16-B multiple */
+  int roff[ORBX_PS_MAXL];   /* ring LDS byte offset */
+  int gpitch[ORBX_PS_MAXL]; /* HBM row pitch (j >= 1) */
+  long long goff[ORBX_PS_MAXL]; /* offset in the frame's pyramid buffer (j >= 1) */
+  int xl[ORBX_PS_MAXL];     /* first LUT entry (uint2) of level j's groups (j >= 1) */
+  int yl[ORBX_PS_MAXL];     /* first row-LUT entry of level j (j >= 1) */
+  int lev[ORBX_PS_MAXL];    /* level index of chain entry j */
+};
+/* task word x: type (bits 0-3) | chain level (4-8) | chunk (9-15) | rows (16-23); y = first row */
+#define ORBX_PS_RESIZE 1
+
 #if defined(__HIPCC__)
 #define ORBX_HDI __host__ __device__ inline
 #else

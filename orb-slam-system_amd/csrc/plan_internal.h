@@ -42,6 +42,10 @@ struct orbx_plan {
   int overlap = 0; /* FAST on level 0 beside the pyramid on s_aux */
   hipStream_t s_aux = nullptr;
   hipEvent_t ev_aux0 = nullptr, ev_aux1 = nullptr;
+  /* row-streaming pyramid tables (k_pyr_stream) and the path choice */
+  uint32_t *d_ps_tasks = nullptr, *d_ps_xlut = nullptr, *d_ps_ylut = nullptr;
+  int32_t* d_ps_tick_end = nullptr;
+  int options = 0; /* ORBX_PLAN_* (include/orbx.h) */
 };
 
 struct orbx_extractor {

@@ -42,6 +42,7 @@ assert KEYPOINT_DTYPE.itemsize == 28
 OK, ERR_ARG, ERR_CELL_ROI, ERR_LEVEL_SIZE, ERR_QUADTREE, ERR_CAPACITY, ERR_UNSUPPORTED, \
     ERR_HIP, ERR_NO_DEVICE = 0, -1, -2, -3, -4, -5, -6, -7, -8
 ORBM_PLAN_ZERO_TAIL, ORBM_PLAN_VALU = 1, 2  # orbm_plan_set_options flags (include/orbx.h)
+ORBX_PLAN_PYR_TILES, ORBX_PLAN_PYR_STREAM = 1, 2  # orbx_plan_set_options flags
 
 EXPORTED = [
     "orbx_abi_version", "orbx_status_string", "orbx_device_count", "orbx_tables",
@@ -50,7 +51,7 @@ EXPORTED = [
     "orbx_extractor_set_options", "orbx_extractor_level_host", "orbx_extractor_stats",
     "orbx_boundary_record_bytes", "orbx_boundary_pack", "orbx_boundary_unpack",
     "orbx_plan_create", "orbx_plan_destroy", "orbx_plan_geometry", "orbx_plan_extract",
-    "orbx_plan_check", "orbx_plan_debug_counters", "orbx_stage_count", "orbx_stage_name", "orbx_plan_set_timing",
+    "orbx_plan_check", "orbx_plan_debug_counters", "orbx_plan_set_options", "orbx_plan_level", "orbx_stage_count", "orbx_stage_name", "orbx_plan_set_timing",
     "orbx_plan_stage_times", "orbx_synth_frames", "orbm_search_by_bow",
     "orbm_descriptor_distance_batch", "orbm_plan_create", "orbm_plan_destroy",
     "orbm_plan_match_frames", "orbm_plan_set_timing", "orbm_plan_stage_times", "orbm_plan_set_options",
@@ -132,6 +133,8 @@ _sig = {
     "orbx_plan_extract": (I, [P, P, I, SZ, SZ, P, P, P, P]),
     "orbx_plan_check": (I, [P, P]),
     "orbx_plan_debug_counters": (I, [P, P]),
+    "orbx_plan_set_options": (I, [P, I]),
+    "orbx_plan_level": (I, [P, I, I, P, SZ, P, P, P]),
     "orbx_stage_count": (I, []),
     "orbx_stage_name": (ctypes.c_char_p, [I]),
     "orbx_plan_set_timing": (I, [P, I]),
@@ -563,6 +566,23 @@ class Plan:
         v = ctypes.c_int(0)
         _check(_lib.orbx_plan_debug_counters(self._h, ctypes.byref(v)), "orbx_plan_debug_counters")
         return {"fast_overflow_strips": v.value}
+
+    def set_options(self, pyramid="auto"):
+        """pyramid: 'auto' (row-streaming for batches of >= 64 frames), 'tiles'
+        (k_pyramid) or 'stream' (k_pyr_stream for any batch); same results"""
+        flags = {"auto": 0, "tiles": ORBX_PLAN_PYR_TILES, "stream": ORBX_PLAN_PYR_STREAM}[pyramid]
+        _check(_lib.orbx_plan_set_options(self._h, flags), "orbx_plan_set_options")
+
+    def level(self, frame, lvl, stream=None):
+        """pyramid level `lvl` (>= 1, not aliasing level 0) of frame `frame` of
+        the last extract, as a host array (synchronises the stream)"""
+        w, h = ctypes.c_int(0), ctypes.c_int(0)
+        _check(_lib.orbx_plan_level(self._h, frame, lvl, None, 0, ctypes.byref(w), ctypes.byref(h),
+                                    _stream_handle(stream)), "orbx_plan_level")
+        out = np.empty((h.value, w.value), np.uint8)
+        _check(_lib.orbx_plan_level(self._h, frame, lvl, _p(out), w.value, None, None,
+                                    _stream_handle(stream)), "orbx_plan_level")
+        return out
 
     def set_timing(self, enable):
         _check(_lib.orbx_plan_set_timing(self._h, 1 if enable else 0))

@@ -34,6 +34,19 @@ int main(int argc, char** argv) {
   std::vector<uint8_t> owner(P.pyr_bytes + 16, 0);
   std::vector<std::pair<size_t, uint8_t>> shadow;  // non-owned bytes of edge dwords
   for (const PyrSeg& g : P.segs) {
+    if (g.area) {  // k_pyr_area2: one exact-2x level, (a + b + c + d + 2) >> 2
+      auto src = [&](int y, int x) {
+        return g.off[0] < 0 ? (int)img[(size_t)y * W + x] : (int)pyr[g.off[0] + (size_t)y * g.pitch[0] + x];
+      };
+      for (int y = 0; y < g.h[1]; ++y)
+        for (int x = 0; x < g.w[1]; ++x) {
+          const size_t o = g.off[1] + (size_t)y * g.pitch[1] + x;
+          pyr[o] = (uint8_t)((src(2 * y, 2 * x) + src(2 * y, 2 * x + 1) + src(2 * y + 1, 2 * x) +
+                              src(2 * y + 1, 2 * x + 1) + 2) >> 2);
+          owner[o] = 1;
+        }
+      continue;
+    }
     if (g.lds_a + g.lds_b + g.lds_xl + g.lds_yl > ORBX_PYR_LDS_MAX) fail("lds total", 0, 0);
     for (int ty = 0; ty < g.nty; ++ty)
       for (int tx = 0; tx < g.ntx; ++tx) {

@@ -107,6 +107,19 @@ def test_resize_tables_reproduce_oracle_resize(orbx_mod, oracle, w, h):
         prev = ref
 
 
+def test_release_library_reads_no_profiling_knobs():
+    """The ORBX_DEBUG_* / ORBX_CHUNK environment knobs (phase early exits, grid
+    divisors, chunked passes) exist only in profiling builds (-DORBX_PROFILING,
+    tools/variant.sh): the release liborbx.so does not contain their names, so
+    an inherited environment cannot change its results.  ORBX_DEBUG_CCAP stays
+    (a test hook that moves the FAST corner-list overflow path, results equal)."""
+    blob = open(os.path.join(PKG, "liborbx.so"), "rb").read()
+    for knob in (b"ORBX_DEBUG_STOP", b"ORBX_DEBUG_OBDIV", b"ORBX_CHUNK", b"ORBX_DEBUG_OVERLAP",
+                 b"ORBX_DEBUG_SMDIV", b"ORBX_DEBUG_PYR_TILE", b"ORBX_DEBUG_PYR_MAXSEG"):
+        assert knob not in blob, knob
+    assert b"ORBX_DEBUG_CCAP" in blob
+
+
 def test_no_device_fails_loudly(orbx_mod):
     if orbx_mod.device_count() > 0:
         pytest.skip("GPU visible")
@@ -134,9 +147,16 @@ def test_sincos_exception_table_is_current(tmp_path):
     assert out.read_text() == committed
 
 
+# every geometry the GPU parity suite runs (test_gpu_parity.py), so the
+# tile kernel's duplicate-store invariant (non-owned edge-dword bytes equal
+# their owner's) is checked wherever the kernel runs
 PYR_CASES = [(640, 480, 1000, 8, 1.2), (1241, 376, 2000, 8, 1.2), (1920, 1080, 2000, 8, 1.2),
              (752, 480, 1200, 4, 1.5), (640, 480, 500, 14, 1.1), (1000, 700, 500, 3, 1.9),
-             (320, 240, 500, 2, 1.2)]
+             (320, 240, 500, 2, 1.2), (4096, 400, 2000, 8, 1.2), (5000, 720, 2000, 8, 1.2),
+             (600, 4400, 2000, 8, 1.2), (642, 361, 1000, 8, 1.2), (644, 362, 1000, 8, 1.2),
+             (640, 480, 1000, 12, 1.1), (640, 480, 1000, 8, 1.3), (752, 480, 1200, 6, 1.5),
+             (1241, 376, 2000, 4, 1.7), (640, 480, 800, 3, 1.95), (1280, 600, 1000, 6, 2.0),
+             (1920, 1080, 2000, 6, 2.0)]
 
 
 @pytest.mark.parametrize("W,H,nf,L,sf", PYR_CASES)
@@ -162,6 +182,66 @@ def test_fused_pyramid_tiling_matches_oracle(oracle, tmp_path, W, H, nf, L, sf):
         lv = ref.level(l)
         if lv.shape == ref.level(l - 1).shape:
             continue  # alias of the previous level (cv::resize copy)
+        assert np.array_equal(raw[off:off + lv.size].reshape(lv.shape), lv), "level %d" % l
+        off += lv.size
+    assert off == raw.size
+
+
+# k_pyr_stream: (W, H, nfeatures, nlevels, scale, r0, rows per task); r0 = 0 is
+# the planner's own choice (the largest tick that fits the LDS budget)
+STREAM_CASES = [(1920, 1080, 2000, 8, 1.2, 0, 4), (640, 480, 1000, 8, 1.2, 0, 4),
+                (1241, 376, 2000, 8, 1.2, 0, 4), (1920, 1080, 2000, 8, 1.2, 1, 1),
+                (1920, 1080, 2000, 8, 1.2, 3, 2), (642, 361, 1000, 8, 1.2, 2, 3),
+                (752, 480, 1200, 4, 1.5, 0, 4), (640, 480, 500, 14, 1.1, 0, 4),
+                (1000, 700, 500, 3, 1.9, 0, 4), (1241, 376, 2000, 4, 1.7, 5, 4),
+                (600, 4400, 2000, 8, 1.2, 0, 4), (644, 362, 1000, 8, 1.2, 0, 4),
+                (640, 480, 800, 3, 1.95, 0, 4), (640, 480, 1000, 8, 1.3, 0, 4)]
+
+
+@pytest.mark.parametrize("W,H,nf,L,sf", [(4096, 400, 2000, 8, 1.2), (1280, 600, 1000, 6, 2.0),
+                                         (320, 240, 500, 2, 1.2)])
+def test_stream_pyramid_not_planned(tmp_path, W, H, nf, L, sf):
+    """No streaming schedule where it cannot apply: rings + column LUT past
+    the LDS budget (4096 wide), an exact-2x level (INTER_AREA path), no
+    resized level at all; those plans keep k_pyramid."""
+    exe = tmp_path / "pse"
+    csrc = os.path.join(PKG, "csrc")
+    subprocess.check_call(["g++", "-O2", "-std=c++17", "-I", csrc,
+                           os.path.join(ROOT, "tests", "cpp", "pyr_stream_emu.cpp"),
+                           os.path.join(csrc, "geometry.cpp"), "-o", str(exe)])
+    (tmp_path / "in.raw").write_bytes(synth.frame(W, H, 5, "noise").tobytes())
+    r = subprocess.run([str(exe), str(tmp_path / "in.raw"), str(W), str(H), str(nf), str(L), repr(sf),
+                        str(tmp_path / "o.bin")], capture_output=True, text=True)
+    assert r.returncode == 4 and "no stream plan" in r.stdout
+
+
+@pytest.mark.parametrize("W,H,nf,L,sf,r0,rpt", STREAM_CASES)
+def test_stream_pyramid_schedule_matches_oracle(oracle, tmp_path, W, H, nf, L, sf, r0, rpt):
+    """Host emulation of k_pyr_stream's ticks on the planner's tables: every
+    ring read finds the row it expects, written in an earlier tick; no slot is
+    written in a tick that reads it; every level row is computed once; the
+    levels equal the oracle's pyramid."""
+    exe = tmp_path / "pse"
+    csrc = os.path.join(PKG, "csrc")
+    subprocess.check_call(["g++", "-O2", "-std=c++17", "-I", csrc,
+                           os.path.join(ROOT, "tests", "cpp", "pyr_stream_emu.cpp"),
+                           os.path.join(csrc, "geometry.cpp"), "-o", str(exe)])
+    img = synth.frame(W, H, 5, "noise")
+    (tmp_path / "in.raw").write_bytes(img.tobytes())
+    out = tmp_path / "out.bin"
+    args = [str(exe), str(tmp_path / "in.raw"), str(W), str(H), str(nf), str(L), repr(sf), str(out)]
+    if r0:
+        args += [str(r0), str(rpt)]
+    r = subprocess.run(args, capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout + r.stderr
+    raw = np.frombuffer(out.read_bytes(), np.uint8)
+    ref = oracle.Extractor(nf, sf, L, 20, 7, cell_guard="empty")
+    ref.extract(img)
+    off = 0
+    for l in range(1, L):
+        lv = ref.level(l)
+        if lv.shape == ref.level(l - 1).shape:
+            continue
         assert np.array_equal(raw[off:off + lv.size].reshape(lv.shape), lv), "level %d" % l
         off += lv.size
     assert off == raw.size
