@@ -551,6 +551,20 @@ def dist_setup(args):
     return torch, dist, world, rank, local
 
 
+def dist_record(torch, dist, world, local):
+    """What the process group actually formed, for the bench line: backend,
+    world size and every rank's device (gathered), so a multi-GPU record
+    shows by itself that RCCL saw N ranks on N distinct GPUs."""
+    props = torch.cuda.get_device_properties(local)
+    me = {"local_rank": local, "device": props.name,
+          "uuid": str(getattr(props, "uuid", "")), "pci_bus": getattr(props, "pci_bus_id", None)}
+    if world == 1 or not dist.is_initialized():
+        return {"backend": "none (single process)", "world_size": 1, "ranks": [me]}
+    ranks = [None] * dist.get_world_size()
+    dist.all_gather_object(ranks, me)
+    return {"backend": dist.get_backend(), "world_size": dist.get_world_size(), "ranks": ranks}
+
+
 def xch_device(torch, dev):
     """Where the boundary exchange buffers live: HBM for RCCL, host for gloo."""
     return torch.device("cpu") if _share_gpu() else dev
@@ -692,6 +706,7 @@ def main_mono(args, wl):
         same = bool(torch.equal(mp.match12[:B], ref12))
         if not same:
             raise SystemExit("bench.py: pipelined matches differ from the serial step")
+    drec = dist_record(torch, dist, world, local)  # collective: every rank
     if rank != 0:
         if world > 1:
             dist.destroy_process_group()
@@ -734,6 +749,7 @@ def main_mono(args, wl):
     if world == 1 and not args.no_latency and args.workload == "c4":
         out["host_fed"] = host_fed_leg(torch, orbx, plan, mp, wl, args, dev, counts[1:])
         out["latency"] = latency_leg()
+    out["distributed"] = drec
     if world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args, wl)
     print(json.dumps(out), flush=True)
@@ -875,6 +891,7 @@ def main_c5(args, wl):
         sp.check()
         if not torch.equal(mp.match12[:B], ref12):
             raise SystemExit("bench.py: pipelined matches differ from the serial step")
+    drec = dist_record(torch, dist, world, local)  # collective: every rank
     if rank != 0:
         if world > 1:
             dist.destroy_process_group()
@@ -917,6 +934,7 @@ def main_c5(args, wl):
                          "ms_per_step": round(el_serial / args.steps * 1e3, 3),
                          "note": "stage times and roofline entries come from this serial timed loop "
                                  "(kernels alone on the GPU)"}
+    out["distributed"] = drec
     if world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline_c5(args, wl)
     print(json.dumps(out), flush=True)

@@ -35,9 +35,12 @@ enum {
                                 src/ORBextractor.cc:230) or < 32 cols                     */
   ORBX_ERR_QUADTREE = -4,    /* DistributeOctTree would never terminate */
   ORBX_ERR_CAPACITY = -5,    /* caller buffer too small (*n holds the required count)     */
-  ORBX_ERR_UNSUPPORTED = -6, /* a configuration beyond the kernels' static limits (level
-                                ratio > ~2.3 other than exactly 2, frame > 4127 px on
-                                both sides or > 8223 px on one, ...)                    */
+  ORBX_ERR_UNSUPPORTED = -6, /* a configuration beyond the kernels' static limits: a level
+                                ratio > ~2.3 other than exactly 2, or a level-0 size
+                                outside the FAST key packing -- supported are
+                                (w-32 <= 4095 and h-32 <= 4095), (w-32 <= 8191 and
+                                h-32 <= 2047) or (w-32 <= 2047 and h-32 <= 8191), so
+                                e.g. 4200x2100 is refused; ...                        */
   ORBX_ERR_HIP = -7,         /* HIP runtime error                                         */
   ORBX_ERR_NO_DEVICE = -8,   /* no gfx950 device / bad device ordinal                     */
 };
@@ -260,7 +263,9 @@ int orbm_descriptor_distance_batch(const uint8_t* a, int na, const uint8_t* b, i
  * reduced to its top `topn` keypoints by (response desc, index asc) and
  * placed in ONE vocabulary node in ascending index order (brute force).
  * match12 rows are indexed by keypoint index of frame A (cap kcap), value =
- * keypoint index in frame B or -1.  Frame p of side A is d_kps_a + p*kcap,
+ * keypoint index in frame B, -1 for no match, or -2 where a match was found
+ * and the rotation check (check_ori) reset it (as orbm_search_by_bow; test
+ * `< 0` for "no match").  Frame p of side A is d_kps_a + p*kcap,
  * d_desc_a + p*kcap*32, d_count_a[p] (side B likewise), i.e. the layout of
  * orbx_plan_extract outputs; d_match12 is [npairs][kcap], d_nmatches
  * [npairs].  Asynchronous on `stream`.  Descriptors are arbitrary 32-byte

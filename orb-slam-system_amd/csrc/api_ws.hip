@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <chrono>
+#include <thread>
 #include <map>
 #include <mutex>
 #include <utility>
@@ -83,16 +84,27 @@ void ws_release(CallWs* w) {
   (*g_pool)[w->device].push_back(w);
 }
 
+// Spin budget: about twice the p99 of the slowest synchronous call (the
+// compat operator() with the pyramid, ~270 us at 1080p), so a call that
+// completes on time never pays the blocking wake-up, and a caller on a
+// shared or busy GPU holds a core for at most this long before sleeping in
+// hipStreamSynchronize (it was 20 ms: the Tracking, LocalMapping and
+// LoopClosing threads could each spin a core that long).  After the first
+// 50 us the loop yields between polls.
 #ifndef ORBX_SPIN_US
-#define ORBX_SPIN_US 20000
+#define ORBX_SPIN_US 600
 #endif
 hipError_t stream_wait(hipStream_t s) {
-  const auto t_end = std::chrono::steady_clock::now() + std::chrono::microseconds(ORBX_SPIN_US);
+  const auto t0 = std::chrono::steady_clock::now();
+  const auto t_yield = t0 + std::chrono::microseconds(50);
+  const auto t_end = t0 + std::chrono::microseconds(ORBX_SPIN_US);
   for (;;) {
     const hipError_t q = hipStreamQuery(s);
     if (q != hipErrorNotReady) return q;
-    if (std::chrono::steady_clock::now() >= t_end) return hipStreamSynchronize(s);
-    __builtin_ia32_pause();
+    const auto now = std::chrono::steady_clock::now();
+    if (now >= t_end) return hipStreamSynchronize(s);
+    if (now >= t_yield) std::this_thread::yield();
+    else __builtin_ia32_pause();
   }
 }
 

@@ -33,10 +33,21 @@ class BoundaryExchange:
         self._step = 0
         self.gathered = self._bufs[0]
 
-    def _native(self, *ts):
+    def _native(self, kps, desc, count, src=None):
         # device-resident exchange (RCCL): one liborbx launch per pack /
-        # unpack (orbx_boundary_pack / _unpack) instead of three tensor copies
-        return self.mine.is_cuda and all(t.is_cuda and t.is_contiguous() for t in ts)
+        # unpack (orbx_boundary_pack / _unpack) instead of three tensor copies.
+        # The launch trusts its pointers, so every size and the device are
+        # checked here; anything else takes the (checked) tensor copies.
+        ts = (kps, desc, count) + ((src,) if src is not None else ())
+        if not (self.mine.is_cuda and all(t.is_cuda and t.is_contiguous() for t in ts)):
+            return False
+        cur = torch.cuda.current_device()
+        k = self.kcap
+        return (all(t.device.index == cur for t in ts + (self.mine,))
+                and kps.numel() * kps.element_size() >= k * 28
+                and desc.numel() * desc.element_size() >= k * 32
+                and count.numel() * count.element_size() >= 4
+                and (src is None or src.numel() * src.element_size() >= self.nbytes))
 
     def pack(self, kps, desc, count):
         k = self.kcap
@@ -72,7 +83,7 @@ class BoundaryExchange:
 
     def _unpack(self, src, kps, desc, count):
         k = self.kcap
-        if self._native(src, kps, desc, count):
+        if self._native(kps, desc, count, src):
             import orbx
             orbx._check(orbx.lib().orbx_boundary_unpack(
                 ctypes.c_void_p(src.data_ptr()), k, ctypes.c_void_p(kps.data_ptr()),

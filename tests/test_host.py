@@ -58,7 +58,8 @@ def test_strict_guard_geometry(orbx_mod):
 
 
 @pytest.mark.parametrize("w,h,ok", [(4127, 4127, True), (4128, 1000, True), (8223, 2079, True),
-                                    (2079, 8223, True), (8224, 600, False), (4200, 4200, False)])
+                                    (2079, 8223, True), (8224, 600, False), (4200, 4200, False),
+                                    (4200, 2100, False), (2100, 4200, False), (4127, 2079, True)])
 def test_large_frame_geometry(orbx_mod, w, h, ok):
     """Frames past 4127 px: the FAST key packing trades coordinate bits
     (13-bit x / 11-bit y or the reverse); beyond both it is unsupported."""

@@ -214,14 +214,24 @@ def _golden_kfs(g):
 def test_oracle_search_by_bow_golden(oracle):
     g = np.load(os.path.join(GOLDEN, "search_by_bow_multinode.npz"))
     kf1, kf2 = _golden_kfs(g)
+    rejected = 0
     for ratio, ori in ((0.6, True), (0.75, True), (0.75, False)):
         tag = "r%02d_o%d" % (int(ratio * 100), int(ori))
         m, n = oracle.search_by_bow(kf1, kf2, ratio, ori)
         assert n == int(g["n_" + tag][0])
         # the fixture predates the -2 marker (matched, then reset to nullptr
         # by the rotation check): it holds -1 there
-        assert (m == -2).any() == (ori and bool((m == -2).any()))
         assert np.array_equal(np.where(m == -2, -1, m), g["match_" + tag])
+        m0, _ = oracle.search_by_bow(kf1, kf2, ratio, False)
+        if ori:
+            # the rotation check runs after the matching (ORBmatcher.cc:349-363):
+            # -2 exactly where the unchecked run matched and this one reset it
+            assert np.array_equal(m == -2, (m0 >= 0) & (m < 0))
+            assert np.array_equal(m[m >= 0], m0[m >= 0])
+            rejected += int((m == -2).sum())
+        else:
+            assert not (m == -2).any()
+    assert rejected > 0, "no case reaches the rotation check's reset"
 
 
 def test_oracle_resize_area2_matches_definition(oracle):
