@@ -81,7 +81,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=40.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-latency", action="store_true")
-    ap.add_argument("--pyramid", choices=["auto", "tiles", "stream"], default="auto",
+    ap.add_argument("--pyramid", choices=["auto", "tiles", "stream", "fused"], default="auto",
                     help="pyramid kernel (orbx_plan_set_options; identical results)")
     ap.add_argument("--serial", action="store_true",
                     help="time only the serial step (no extraction/matching overlap across steps)")

@@ -185,14 +185,18 @@ int orbx_plan_debug_counters(orbx_plan* plan, int* fast_overflow_strips);
  *   ORBX_PLAN_PYR_TILES   the pyramid by k_pyramid (2-D tiles of the level
  *                         chain, halo recompute) for every batch size;
  *   ORBX_PLAN_PYR_STREAM  the row-streaming pyramid (k_pyr_stream, one
- *                         workgroup per frame) for every batch size.
+ *                         workgroup per frame) for every batch size;
+ *   ORBX_PLAN_FUSED       pyramid and cell FAST in one kernel (k_pyrfast:
+ *                         one workgroup per frame streams every level once
+ *                         through LDS, FAST on the rows as they pass).
  * Automatic: k_pyr_stream for batches of >= 64 frames when the planner
  * could schedule it (no exact-2x level, rings within the LDS budget), else
  * k_pyramid.  Returns ORBX_ERR_ARG for unknown flags or both at once,
- * ORBX_ERR_UNSUPPORTED for ORBX_PLAN_PYR_STREAM on a plan the streaming
- * schedule does not cover (the options are then unchanged). */
+ * ORBX_ERR_UNSUPPORTED for ORBX_PLAN_PYR_STREAM / ORBX_PLAN_FUSED on a plan
+ * the streaming schedule does not cover (the options are then unchanged). */
 #define ORBX_PLAN_PYR_TILES 1
 #define ORBX_PLAN_PYR_STREAM 2
+#define ORBX_PLAN_FUSED 4
 int orbx_plan_set_options(orbx_plan* plan, int flags);
 
 /* mvImagePyramid[level] of frame `frame` of the last orbx_plan_extract on

@@ -16,6 +16,7 @@
 #include "orbx_internal.h"
 #include "orbx_sincos.h"
 #include "wave_ops.h"
+#include "fast_ops.h"
 
 #define ORBX_BRIEF_STORAGE static __constant__ const
 #include "brief_pattern.inc"
@@ -150,9 +151,6 @@ __device__ __forceinline__ void stage_rows_u32(uint8_t* __restrict__ lds, int lp
   }
 }
 
-typedef unsigned short us2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ us2 as_us2(uint32_t x) { return __builtin_bit_cast(us2, x); }
-__device__ __forceinline__ uint32_t as_u32(us2 x) { return __builtin_bit_cast(uint32_t, x); }
 
 // ---------------------------------------------------------------------------
 // k_pyramid: a chain of unique levels (PyrSeg) with OpenCV's INTER_LINEAR
@@ -395,32 +393,6 @@ __global__ __launch_bounds__(256) void k_pyr_area2(const uint8_t* __restrict__ f
 // (ORBextractor.cc:293-296,330-331).  Survivors are compacted in raster order
 // into the cell's slot list, packed (x-16)<<20 | (y-16)<<8 | score.
 // ---------------------------------------------------------------------------
-// FAST radius-3 circle (cv::makeOffsets, patternSize 16), as immediates
-__device__ constexpr int8_t c_circle_dx[16] = {0, 1, 2, 3, 3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1};
-__device__ constexpr int8_t c_circle_dy[16] = {3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1, 0, 1, 2, 3};
-
-__device__ __forceinline__ int min3i(int a, int b, int c) { return min(min(a, b), c); }
-__device__ __forceinline__ int max3i(int a, int b, int c) { return max(max(a, b), c); }
-
-__device__ __forceinline__ int fast_strength(const uint8_t* t, int tw) {
-  int I[16];
-#pragma unroll
-  for (int k = 0; k < 16; ++k) I[k] = t[c_circle_dy[k] * tw + c_circle_dx[k]];
-  const int v = t[0];
-  int mn3[16], mx3[16];
-#pragma unroll
-  for (int k = 0; k < 16; ++k) {
-    mn3[k] = min3i(I[k], I[(k + 1) & 15], I[(k + 2) & 15]);
-    mx3[k] = max3i(I[k], I[(k + 1) & 15], I[(k + 2) & 15]);
-  }
-  int Mb = 0, Md = 255;
-#pragma unroll
-  for (int k = 0; k < 16; ++k) {
-    Mb = max(Mb, min3i(mn3[k], mn3[(k + 3) & 15], mn3[(k + 6) & 15]));
-    Md = min(Md, max3i(mx3[k], mx3[(k + 3) & 15], mx3[(k + 6) & 15]));
-  }
-  return max3i(0, Mb - v, v - Md);
-}
 
 __device__ __forceinline__ int nms_keep(const uint8_t* amap, int bw, int bh, int bx, int by,
                                         int th) {
@@ -475,45 +447,6 @@ __device__ __forceinline__ bool nms_keep_tile(const uint8_t* amap, int tpitch, i
   return keep;
 }
 
-// 4 cyclically consecutive points of {0,2,..,14} all brighter (darker) than
-// v +- t: necessary for a 9-arc (any 9 contiguous circle points contain 4
-// consecutive even ones), i.e. for A > t.
-// Packed form: E_i = circle point 2i; P_i = (E_i, E_{i+4}) as 16-bit lanes,
-// so one packed min over four P's covers the windows starting at s and s+4:
-// s = 0/4: P0..P3; 1/5: P1,P2,P3,rot(P0); 2/6: P2,P3,rot(P0),rot(P1);
-// 3/7: P3,rot(P0),rot(P1),rot(P2) (rot swaps the halves).  Bright: some
-// window's min > v + t; dark: some window's max < v - t.
-__device__ __forceinline__ us2 rot16(us2 x) { return x.yx; }
-__device__ __forceinline__ bool fast_even_test_pk(const uint8_t* t, int tw, int th) {
-  us2 P0, P1, P2, P3;
-  P0.x = t[3 * tw];           // point 0  (0, 3)
-  P0.y = t[-3 * tw];          // point 8  (0, -3)
-  P1.x = t[2 * tw + 2];       // point 2  (2, 2)
-  P1.y = t[-2 * tw - 2];      // point 10 (-2, -2)
-  P2.x = t[3];                // point 4  (3, 0)
-  P2.y = t[-3];               // point 12 (-3, 0)
-  P3.x = t[-2 * tw + 2];      // point 6  (2, -2)
-  P3.y = t[2 * tw - 2];       // point 14 (-2, 2)
-  const unsigned short v = t[0];
-  const us2 s0 = rot16(P0), s1 = rot16(P1), s2 = rot16(P2);
-  const us2 m23 = __builtin_elementwise_min(P2, P3), m123 = __builtin_elementwise_min(P1, m23);
-  const us2 n01 = __builtin_elementwise_min(s0, s1);
-  const us2 B = __builtin_elementwise_max(
-      __builtin_elementwise_max(__builtin_elementwise_min(P0, m123), __builtin_elementwise_min(m123, s0)),
-      __builtin_elementwise_max(__builtin_elementwise_min(m23, n01),
-                                __builtin_elementwise_min(P3, __builtin_elementwise_min(n01, s2))));
-  const us2 x23 = __builtin_elementwise_max(P2, P3), x123 = __builtin_elementwise_max(P1, x23);
-  const us2 y01 = __builtin_elementwise_max(s0, s1);
-  const us2 D = __builtin_elementwise_min(
-      __builtin_elementwise_min(__builtin_elementwise_max(P0, x123), __builtin_elementwise_max(x123, s0)),
-      __builtin_elementwise_min(__builtin_elementwise_max(x23, y01),
-                                __builtin_elementwise_max(P3, __builtin_elementwise_max(y01, s2))));
-  const us2 hh = (us2)(unsigned short)(v + th);
-  const us2 vv = (us2)v, tt = (us2)(unsigned short)th;
-  const us2 db = __builtin_elementwise_sub_sat(B, hh);
-  const us2 dd = __builtin_elementwise_sub_sat(__builtin_elementwise_sub_sat(vv, D), tt);
-  return (as_u32(db) | as_u32(dd)) != 0u;
-}
 
 __device__ __forceinline__ bool fast_even_test(const uint8_t* t, int tw, int th) {
   const int v = t[0];
@@ -538,16 +471,8 @@ __device__ __forceinline__ int wave_excl_scan(int n, int lane, int* total) {
   return incl - n;
 }
 
-__device__ __forceinline__ void wave_sync_lds() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
 
 #define FS_NW (FS_NT / 64)
-struct GroupWords {
-  uint32_t w0, w1, w2, up, dn;
-};
 #ifndef FS_L1FLUSH
 #define FS_L1FLUSH 64 /* stage B runs once a wave's L1 holds this many entries */
 #endif
@@ -1133,9 +1058,9 @@ __device__ __forceinline__ int upper_bound_i(const int* a, int n, int v) {
       const uint32_t *__restrict__ ccount, int ncells_total, uint32_t *__restrict__ qkeys, \
       int32_t *__restrict__ qnode, size_t qk_stride, uint32_t *__restrict__ qout,          \
       size_t qout_stride, int *__restrict__ lcount, int nlevels, int smax, int maxcells,   \
-      int *__restrict__ err, uint32_t *__restrict__ qperm
+      int *__restrict__ err, uint32_t *__restrict__ qperm, const uint32_t *__restrict__ slots_hi
 #define QT_KERNEL_PASS \
-  lv, cells, slots, slot_stride, ccount, ncells_total, qkeys, qnode, qk_stride, qout, qout_stride, lcount, nlevels, smax, maxcells, err, qperm
+  lv, cells, slots, slot_stride, ccount, ncells_total, qkeys, qnode, qk_stride, qout, qout_stride, lcount, nlevels, smax, maxcells, err, qperm, slots_hi
 
 // QJ: keys per thread held in registers (256 QJ per level; more spill to the
 // global keys/node arrays).  Both instantiations are built for 8 waves per
@@ -1176,12 +1101,16 @@ __device__ __forceinline__ void qt_body(QT_KERNEL_ARGS) {
 
   // gather vToDistributeKeys (cell-major, raster within cell)
   const int nc = U.ncells;
-  for (int i = tid; i < nc; i += 256) cell_off[i] = (int)ccount[(size_t)f * ncells_total + U.cell_begin + i];
+  // a count with ORBX_CC_HI (k_pyrfast): the cell's keys are its iniThFAST
+  // set, in slots_hi
+  const uint32_t* fcc = ccount + (size_t)f * ncells_total + U.cell_begin;
+  for (int i = tid; i < nc; i += 256) cell_off[i] = (int)(fcc[i] & ~ORBX_CC_HI);
   __syncthreads();
   const int C = block_scan_excl(cell_off, nc, wtmp);
   if (tid == 0) cell_off[nc] = C;
   __syncthreads();
   const uint32_t* fslots = slots + (size_t)f * slot_stride;
+  const uint32_t* fslots_hi = slots_hi + (size_t)f * slot_stride;
   // keys k = tid + 256 j (j < QJ) and their node ids live in registers for
   // the whole distribution (every pass walks all keys twice: from global
   // memory that was a load-latency chain per pass); more keys than that
@@ -1196,13 +1125,13 @@ __device__ __forceinline__ void qt_body(QT_KERNEL_ARGS) {
     nr[j] = -1;
     if (k < C) {
       const int c = upper_bound_i(cell_off, nc, k) - 1;
-      kr[j] = fslots[cells[U.cell_begin + c].slot_off + (k - cell_off[c])];
+      kr[j] = ((fcc[c] & ORBX_CC_HI) ? fslots_hi : fslots)[cells[U.cell_begin + c].slot_off + (k - cell_off[c])];
       keys[k] = kr[j];
     }
   }
   for (int k = tid + 256 * QJ; k < C; k += 256) {
     const int c = upper_bound_i(cell_off, nc, k) - 1;
-    keys[k] = fslots[cells[U.cell_begin + c].slot_off + (k - cell_off[c])];
+    keys[k] = ((fcc[c] & ORBX_CC_HI) ? fslots_hi : fslots)[cells[U.cell_begin + c].slot_off + (k - cell_off[c])];
   }
   __syncthreads();  // cell_off is dead: its LDS becomes the node arrays
 #if defined(QT_PROBE_STOP) && QT_PROBE_STOP == 1  // profiling only: the gather alone

@@ -45,6 +45,9 @@ struct orbx_plan {
   /* row-streaming pyramid tables (k_pyr_stream) and the path choice */
   uint32_t *d_ps_tasks = nullptr, *d_ps_xlut = nullptr, *d_ps_ylut = nullptr;
   int32_t* d_ps_tick_end = nullptr;
+  /* fused pyramid + FAST tables (k_pyrfast) and its iniThFAST key lists */
+  uint32_t *d_pf_tasks = nullptr, *d_pf_xlut = nullptr, *d_pf_ylut = nullptr, *d_slots_hi = nullptr;
+  int32_t* d_pf_tick_end = nullptr;
   int options = 0; /* ORBX_PLAN_* (include/orbx.h) */
 };
 

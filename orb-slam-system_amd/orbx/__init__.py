@@ -42,7 +42,7 @@ assert KEYPOINT_DTYPE.itemsize == 28
 OK, ERR_ARG, ERR_CELL_ROI, ERR_LEVEL_SIZE, ERR_QUADTREE, ERR_CAPACITY, ERR_UNSUPPORTED, \
     ERR_HIP, ERR_NO_DEVICE = 0, -1, -2, -3, -4, -5, -6, -7, -8
 ORBM_PLAN_ZERO_TAIL, ORBM_PLAN_VALU = 1, 2  # orbm_plan_set_options flags (include/orbx.h)
-ORBX_PLAN_PYR_TILES, ORBX_PLAN_PYR_STREAM = 1, 2  # orbx_plan_set_options flags
+ORBX_PLAN_PYR_TILES, ORBX_PLAN_PYR_STREAM, ORBX_PLAN_FUSED = 1, 2, 4  # orbx_plan_set_options flags
 
 EXPORTED = [
     "orbx_abi_version", "orbx_status_string", "orbx_device_count", "orbx_tables",
@@ -569,8 +569,10 @@ class Plan:
 
     def set_options(self, pyramid="auto"):
         """pyramid: 'auto' (row-streaming for batches of >= 64 frames), 'tiles'
-        (k_pyramid) or 'stream' (k_pyr_stream for any batch); same results"""
-        flags = {"auto": 0, "tiles": ORBX_PLAN_PYR_TILES, "stream": ORBX_PLAN_PYR_STREAM}[pyramid]
+        (k_pyramid), 'stream' (k_pyr_stream for any batch) or 'fused' (pyramid
+        and cell FAST in one kernel, k_pyrfast); same results"""
+        flags = {"auto": 0, "tiles": ORBX_PLAN_PYR_TILES, "stream": ORBX_PLAN_PYR_STREAM,
+                 "fused": ORBX_PLAN_FUSED}[pyramid]
         _check(_lib.orbx_plan_set_options(self._h, flags), "orbx_plan_set_options")
 
     def level(self, frame, lvl, stream=None):

@@ -246,3 +246,25 @@ def test_stream_pyramid_schedule_matches_oracle(oracle, tmp_path, W, H, nf, L, s
         assert np.array_equal(raw[off:off + lv.size].reshape(lv.shape), lv), "level %d" % l
         off += lv.size
     assert off == raw.size
+
+
+FUSED_CASES = [(1920, 1080, 2000, 8, 1.2), (640, 480, 1000, 8, 1.2), (1241, 376, 2000, 8, 1.2),
+               (640, 480, 1000, 1, 1.2), (752, 480, 1200, 6, 1.5), (640, 480, 1000, 12, 1.1),
+               (642, 361, 1000, 8, 1.2), (644, 362, 1000, 8, 1.2), (600, 4400, 2000, 8, 1.2),
+               (1241, 376, 2000, 4, 1.7), (640, 480, 800, 3, 1.95), (640, 480, 1000, 8, 1.3)]
+
+
+@pytest.mark.parametrize("W,H,nf,L,sf", FUSED_CASES)
+def test_fused_pyramid_fast_schedule(tmp_path, W, H, nf, L, sf):
+    """k_pyrfast's tick schedule on the planner's tables (tests/cpp/pyrfast_emu.cpp):
+    every ring / strength-ring / bitmap read finds its row, written in an
+    earlier tick, no slot is written in a phase that reads it, every
+    detection row is tested and NMS'd once (after its neighbours) and every
+    next-level row resized once."""
+    exe = tmp_path / "pfe"
+    csrc = os.path.join(PKG, "csrc")
+    subprocess.check_call(["g++", "-O2", "-std=c++17", "-I", csrc,
+                           os.path.join(ROOT, "tests", "cpp", "pyrfast_emu.cpp"),
+                           os.path.join(csrc, "geometry.cpp"), "-o", str(exe)])
+    r = subprocess.run([str(exe), str(W), str(H), str(nf), str(L), repr(sf)], capture_output=True, text=True)
+    assert r.returncode == 0 and r.stdout.startswith("ok"), r.stdout + r.stderr

@@ -34,15 +34,16 @@ def _cmp_kps(a, b, what):
             raise AssertionError("%s: field %s differs at %d rows, first %d" % (what, f, len(bad), bad[0]))
 
 
+@pytest.mark.parametrize("mode", ["stream", "fused"])
 @pytest.mark.parametrize("w,h,nf,sc,L,guard,kind,idx", STREAM_CASES)
-def test_stream_pyramid_matches_oracle(gpu, oracle, w, h, nf, sc, L, guard, kind, idx):
+def test_stream_pyramid_matches_oracle(gpu, oracle, mode, w, h, nf, sc, L, guard, kind, idx):
     import torch
     B = 3
     prm = gpu.params(nf, sc, L, 20, 7, guard)
     plan = gpu.Plan(prm, w, h, B)
     frames = np.stack([synth.frame(w, h, idx + f, kind) for f in range(B)])
     tf = torch.from_numpy(frames).cuda()
-    plan.set_options("stream")
+    plan.set_options(mode)
     plan.extract(tf)
     plan.check()
     res = plan.results(B)
@@ -64,6 +65,36 @@ def test_stream_pyramid_matches_oracle(gpu, oracle, w, h, nf, sc, L, guard, kind
         for got, l in zip(levels[f], [l for l in range(1, L) if plan.geo.alias[l] == l]):
             assert np.array_equal(plan.level(f, l), got), "tiles vs stream, frame %d level %d" % (f, l)
         _cmp_kps(res2[f][0], res[f][0], "tiles vs stream frame %d" % f)
+
+
+FUSED_EXTRA = [
+    # (w, h, nfeatures, nlevels, iniThFAST, minThFAST, kind, frame_idx): a
+    # single level, and the threshold pairs of the GPU suite (the minThFAST
+    # retry, minThFAST above iniThFAST, equal ones)
+    (640, 480, 1000, 1, 20, 7, "rects", 120),
+    (640, 480, 1000, 8, 12, 5, "rects", 121),
+    (1241, 376, 2000, 8, 9, 15, "noise", 122),
+    (752, 480, 1200, 8, 7, 7, "pan", 123),
+    (1920, 1080, 2000, 8, 31, 10, "pan", 124),
+]
+
+
+@pytest.mark.parametrize("w,h,nf,L,ini,mn,kind,idx", FUSED_EXTRA)
+def test_fused_thresholds_match_oracle(gpu, oracle, w, h, nf, L, ini, mn, kind, idx):
+    """k_pyrfast's NMS at both thresholds and the per-cell choice between
+    them (iniThFAST keys in slots_hi, flagged counts) against the oracle."""
+    import torch
+    B = 2
+    plan = gpu.Plan(gpu.params(nf, 1.2, L, ini, mn, "empty"), w, h, B)
+    frames = np.stack([synth.frame(w, h, idx + f, kind) for f in range(B)])
+    plan.set_options("fused")
+    plan.extract(torch.from_numpy(frames).cuda())
+    plan.check()
+    res = plan.results(B)
+    for f in range(B):
+        rk, rd = oracle.Extractor(nf, 1.2, L, ini, mn, cell_guard="empty").extract(frames[f])
+        _cmp_kps(res[f][0], rk, "frame %d" % f)
+        assert np.array_equal(res[f][1], rd), "frame %d descriptors" % f
 
 
 def test_stream_pyramid_is_the_default_for_batches(gpu):
