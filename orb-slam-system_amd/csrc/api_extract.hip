@@ -362,7 +362,7 @@ static int extract_pass(orbx_plan* p, const uint8_t* frames, int n, size_t fstri
   }
   // K1 pyramid: row-streaming (one workgroup per frame) for batches, or the
   // tile chain (many small workgroups per frame) for single frames
-  p->timer.begin(ORBX_STAGE_RESIZE, s);
+  if (!fused) p->timer.begin(ORBX_STAGE_RESIZE, s);  // fused: all in the FAST stage's launch
   const bool stream = !fused && P.ps_ok && !(p->options & ORBX_PLAN_PYR_TILES) &&
                       (n >= 64 || (p->options & ORBX_PLAN_PYR_STREAM));
   if (stream) {
@@ -393,7 +393,7 @@ static int extract_pass(orbx_plan* p, const uint8_t* frames, int n, size_t fstri
                        reinterpret_cast<const int4*>(p->d_pyr_ys),
                        reinterpret_cast<const uint4*>(p->d_pyr_blob), p->d_pyr_bo, p->dbg);
   }
-  p->timer.end(ORBX_STAGE_RESIZE, s);
+  if (!fused) p->timer.end(ORBX_STAGE_RESIZE, s);
   if (p->ev_after_pyr && hipEventRecord(p->ev_after_pyr, s) != hipSuccess) return ORBX_ERR_HIP;
   // K2 FAST cells
   p->timer.begin(ORBX_STAGE_FAST, s);

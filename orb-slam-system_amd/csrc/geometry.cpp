@@ -652,7 +652,7 @@ bool plan_pyr_fast(Plan& P, int rows0, int rpt) {
   /* schedules */
   for (int p = 0; p < n; ++p) {
     PyrFastPass& Q = F.p[p];
-    Q.tick0 = (int)P.pf_tick_end.size();
+    Q.tick0 = (int)P.pf_tick_end.size() / 2;
     const int yd0 = Q.fast ? Q.y0 : 0, yd1 = Q.fast ? Q.y1 : 0;
     int da = yd0, dn = yd0, dr = 0;
     const int nh = Q.next ? Q.nh : 0;
@@ -719,34 +719,43 @@ bool plan_pyr_fast(Plan& P, int rows0, int rpt) {
         P.pf_ylut.push_back((uint32_t)(uint16_t)cf[0] | ((uint32_t)(uint16_t)cf[1] << 16));
       }
     }
-    /* tasks, largest first; the NMS task (one wave walks the rows in order)
-     * leads its tick */
+    /* tasks per tick, two lists (tick_end holds both ends): phase 1 the two
+     * NMS tasks (cell columns [0, ncv/2) and [ncv/2, ncv): one wave walks
+     * each half's rows in order; they lead, being the longest) and stage A;
+     * phase 2 the resize (it reads only ring rows of earlier ticks and writes
+     * HBM, so it runs beside stage C), each list largest first */
     for (const TickRec& t : tr) {
       std::vector<std::pair<int, uint64_t>> tk;
       auto add = [&](int type, int chunk, int nr, uint32_t y, int cost) {
         const uint32_t x = (uint32_t)type | ((uint32_t)p << 4) | ((uint32_t)chunk << 9) | ((uint32_t)nr << 16);
         tk.push_back({-cost, ((uint64_t)x << 32) | y});
       };
-      if (t.n1 - t.n0 > 255) return false; /* one NMS task per tick (one corner list) */
-      if (t.n1 > t.n0) add(ORBX_PF_NMS, 0, t.n1 - t.n0, (uint32_t)t.n0 | ((uint32_t)(t.n0 % Q.arows) << 22), 1 << 28);
+      auto flush = [&]() {
+        std::stable_sort(tk.begin(), tk.end(),
+                         [](const std::pair<int, uint64_t>& a, const std::pair<int, uint64_t>& b) { return a.first < b.first; });
+        for (auto& e : tk) {
+          P.pf_tasks.push_back((uint32_t)(e.second >> 32));
+          P.pf_tasks.push_back((uint32_t)e.second);
+        }
+        tk.clear();
+        P.pf_tick_end.push_back((int)(P.pf_tasks.size() / 2));
+      };
+      if (t.n1 - t.n0 > 255) return false; /* one NMS task per half and tick */
+      if (t.n1 > t.n0)
+        for (int half = 0; half < (Q.ncv > 1 ? 2 : 1); ++half)
+          add(ORBX_PF_NMS, half, t.n1 - t.n0, (uint32_t)t.n0 | ((uint32_t)(t.n0 % Q.arows) << 22), 1 << 28);
       for (int y0 = t.a0; y0 < t.a1; y0 += rpt) {
         const int nr = std::min(rpt, t.a1 - y0);
         for (int c = 0; c < Q.nchunk; ++c)
           add(ORBX_PF_FASTA, c, nr,
               (uint32_t)y0 | ((uint32_t)((y0 - 3) % Q.rrows) << 14) | ((uint32_t)(y0 % Q.arows) << 22), 3 * nr);
       }
+      flush();
       for (int y0 = t.r0; y0 < t.r1; y0 += rpt) {
         const int nr = std::min(rpt, t.r1 - y0);
         for (int c = 0; c < (Q.ng + 63) / 64; ++c) add(ORBX_PS_RESIZE, c, nr, (uint32_t)y0, nr);
       }
-      std::stable_sort(tk.begin(), tk.end(), [](const std::pair<int, uint64_t>& a, const std::pair<int, uint64_t>& b) {
-        return a.first < b.first;
-      });
-      for (auto& e : tk) {
-        P.pf_tasks.push_back((uint32_t)(e.second >> 32));
-        P.pf_tasks.push_back((uint32_t)e.second);
-      }
-      P.pf_tick_end.push_back((int)(P.pf_tasks.size() / 2));
+      flush();
     }
   }
   /* LDS layout */
@@ -765,7 +774,7 @@ bool plan_pyr_fast(Plan& P, int rows0, int rpt) {
   F.o_l1 = take(4LL * 15 * ORBX_PF_L1CAP);
   F.o_l2 = take(4LL * ORBX_PF_L2CAP);
   F.nms_cap = w_max;
-  F.o_nms = take(2LL * w_max);
+  F.o_nms = take(2LL * 2 * w_max); /* one corner list per NMS half */
   F.o_misc = take(64);
   F.lut_max_bytes = (int)lut_max;
   F.cells_max = cells_max;

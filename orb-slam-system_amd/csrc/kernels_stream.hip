@@ -425,12 +425,19 @@ __device__ __forceinline__ void pf_resize(const PyrFastPass& Q, const PfLds& L, 
   }
 }
 
-// NMS + emit of detection rows [y0, y0 + nr) in order (one wave)
+// NMS + emit of detection rows [y0, y0 + nr) in order (one wave), for the
+// cells of columns [jc0, jc1) (half 0: [0, ncv/2), half 1: [ncv/2, ncv); the
+// two halves run side by side on two waves)
 __device__ __forceinline__ void pf_nms(const PyrFast& F, const PyrFastPass& Q, const PfLds& L,
                                        uint32_t* __restrict__ fslots, uint32_t* __restrict__ fslots_hi,
-                                       uint32_t* __restrict__ fccount, int y0, int nr, int as, int lane) {
+                                       uint32_t* __restrict__ fccount, int y0, int nr, int as, int half,
+                                       int lane) {
   const int ini = F.ini_th, mn = F.min_th;
   const float rw = __builtin_amdgcn_rcpf((float)Q.wcell);
+  const int jc0 = half ? Q.ncv >> 1 : 0, jc1 = (half || Q.ncv == 1) ? Q.ncv : Q.ncv >> 1;
+  const int xa = Q.c0 + jc0 * Q.wcell, xb = jc1 == Q.ncv ? Q.c1 : Q.c0 + jc1 * Q.wcell;
+  const int wlo = xa >> 5, whi = (xb - 1) >> 5;  // bitmap words touching [xa, xb)
+  uint16_t* const cl = L.nms + half * F.nms_cap;
   int ci = (y0 - Q.y0) / Q.hcell;
   int zy0 = Q.y0 + ci * Q.hcell, zy1 = ci == Q.nrv - 1 ? Q.y1 : zy0 + Q.hcell;
   const unsigned long long below = (1ull << lane) - 1ull;
@@ -439,12 +446,18 @@ __device__ __forceinline__ void pf_nms(const PyrFast& F, const PyrFastPass& Q, c
     const int asm1 = as == 0 ? Q.arows - 1 : as - 1, asp1 = pf_wrap_inc(as, Q.arows);
     // the row's corners in raster order (bitmap words, cleared for the slot's next row)
     int nc = 0;
-    for (int w0 = 0; w0 < Q.bmw; w0 += 64) {
+    for (int w0 = wlo; w0 <= whi; w0 += 64) {
       const int wi = w0 + lane;
       uint32_t m = 0;
-      if (wi < Q.bmw) {
-        m = L.bmap[as * Q.bmw + wi];
-        L.bmap[as * Q.bmw + wi] = 0u;
+      if (wi <= whi) {
+        // this half's bits of the word; a word shared with the other half
+        // loses only this half's bits (atomic and), an own word is cleared
+        const int b0 = max(xa - 32 * wi, 0), b1 = min(xb - 32 * wi, 32);
+        const uint32_t own = (b1 >= 32 ? 0xFFFFFFFFu : ((1u << b1) - 1u)) & ~((1u << b0) - 1u);
+        uint32_t* wp = &L.bmap[as * Q.bmw + wi];
+        m = *wp & own;
+        if (own == 0xFFFFFFFFu) *wp = 0u;
+        else atomicAnd(wp, ~own);
       }
       const int cn = __popc(m);
       const int incl = wave_incl_scan(cn);
@@ -452,7 +465,7 @@ __device__ __forceinline__ void pf_nms(const PyrFast& F, const PyrFastPass& Q, c
       while (m) {
         const int b = __ffs((int)m) - 1;
         m &= m - 1u;
-        L.nms[off++] = (uint16_t)(32 * wi + b);
+        cl[off++] = (uint16_t)(32 * wi + b);
       }
       nc += lane_value(incl, 63);
     }
@@ -464,7 +477,7 @@ __device__ __forceinline__ void pf_nms(const PyrFast& F, const PyrFastPass& Q, c
     const int crow = ci * Q.ncv;
     for (int q0 = 0; q0 < nc; q0 += 64) {  // wave-uniform
       const bool act = q0 + lane < nc;
-      const int xx = act ? (int)L.nms[q0 + lane] : Q.c0;
+      const int xx = act ? (int)cl[q0 + lane] : xa;
       const int jc = min((int)(((float)(xx - Q.c0) + 0.5f) * rw), Q.ncv - 1);
       const int zx0 = Q.c0 + jc * Q.wcell, zx1 = jc == Q.ncv - 1 ? Q.c1 : zx0 + Q.wcell;
       const int a = A0[xx];
@@ -506,7 +519,7 @@ __device__ __forceinline__ void pf_nms(const PyrFast& F, const PyrFastPass& Q, c
       wave_sync_lds();
     }
     if (y == zy1 - 1) {  // the cell row is complete
-      for (int jc = lane; jc < Q.ncv; jc += 64) {
+      for (int jc = jc0 + lane; jc < jc1; jc += 64) {
         const int clo = L.cnt[jc], chi = L.cnt[F.ncv_max + jc];
         fccount[Q.cell_begin + crow + jc] = chi > 0 ? ((uint32_t)chi | ORBX_CC_HI) : (uint32_t)clo;
         L.cnt[jc] = 0;
@@ -605,10 +618,37 @@ __global__ __launch_bounds__(1024) void k_pyrfast(PF_KERNEL_ARGS) {
   uint32_t* fccount = ccount + (size_t)f * ncells_total;
   const int t_lo = min(F.ini_th, F.min_th);
   uint32_t* L1 = L.l1 + (wave > 0 ? wave - 1 : 0) * ORBX_PF_L1CAP;
-  int pending = -1;  // a task ticket drawn past its tick's end, kept for a later tick
+  int pending = -1;  // a task ticket drawn past its list's end, kept for a later list
   int T = 0;         // tick count over all passes (list parity)
   for (int p = 0; p < F.np; ++p) {
     const PyrFastPass& Q = F.p[p];
+    int n1 = 0;
+    // the tasks of one list (tick k, phase 1 or 2) by ticket, in list order
+    auto run_tasks = [&](int tend) {
+      for (;;) {
+        int t = pending;
+        if (t < 0) {
+          int v = 0;
+          if (lane == 0) v = atomicAdd(&L.misc[0], 1);
+          t = __builtin_amdgcn_readfirstlane(v);
+        }
+        if (t >= tend) {
+          pending = t;
+          break;
+        }
+        pending = -1;
+        const uint2 d = tasks[t];
+        const int type = (int)(d.x & 15);
+        if (type == ORBX_PF_FASTA) {
+          pf_fasta(Q, L, d.x, d.y, lane, L1, n1, t_lo, T & 1);
+        } else if (type == ORBX_PS_RESIZE) {
+          pf_resize(Q, L, fpyr, ylut, d.x, (int)d.y, lane);
+        } else {
+          pf_nms(F, Q, L, fslots, fslots_hi, fccount, (int)(d.y & 0x3FFFu), (int)((d.x >> 16) & 255),
+                 (int)((d.y >> 22) & 0xFFu), (int)((d.x >> 9) & 127), lane);
+        }
+      }
+    };
     // pass setup: the next level's column LUT, this level's cell slot offsets,
     // zero counts and corner bitmaps
     if (Q.next) {
@@ -625,37 +665,13 @@ __global__ __launch_bounds__(1024) void k_pyrfast(PF_KERNEL_ARGS) {
     const uint8_t* src = p == 0 ? frames + (size_t)f * fstride : fpyr + Q.soff;
     const uint32_t sp = p == 0 ? (uint32_t)rstride : (uint32_t)Q.spitch;
     const bool al16 = p > 0 || aligned16;
-    int n1 = 0;
     for (int k = 0; k < Q.nticks; ++k, ++T) {
       const int par = T & 1;
       // ---- phase 1
       if (wave == 0) {
         pf_load(Q, src, sp, L.ring, min(Q.h, Q.R * k), min(Q.h, Q.R * (k + 1)), lane, al16);
       } else {
-        const int tend = tick_end[Q.tick0 + k];
-        for (;;) {
-          int t = pending;
-          if (t < 0) {
-            int v = 0;
-            if (lane == 0) v = atomicAdd(&L.misc[0], 1);
-            t = __builtin_amdgcn_readfirstlane(v);
-          }
-          if (t >= tend) {
-            pending = t;
-            break;
-          }
-          pending = -1;
-          const uint2 d = tasks[t];
-          const int type = (int)(d.x & 15);
-          if (type == ORBX_PF_FASTA) {
-            pf_fasta(Q, L, d.x, d.y, lane, L1, n1, t_lo, par);
-          } else if (type == ORBX_PS_RESIZE) {
-            pf_resize(Q, L, fpyr, ylut, d.x, (int)d.y, lane);
-          } else {
-            pf_nms(F, Q, L, fslots, fslots_hi, fccount, (int)(d.y & 0x3FFFu), (int)((d.x >> 16) & 255),
-                   (int)((d.y >> 22) & 0xFFu), lane);
-          }
-        }
+        run_tasks(tick_end[2 * (Q.tick0 + k)]);
         // the wave's last even-test batch of the tick
         wave_sync_lds();
         if (n1 > 0) pf_stage_b(Q, L, lane < n1 ? L1[lane] : 0u, lane < n1, t_lo, lane, par);
@@ -678,6 +694,8 @@ __global__ __launch_bounds__(1024) void k_pyrfast(PF_KERNEL_ARGS) {
           const bool act = q + lane < n2;
           pf_stage_c(Q, L, act ? L.l2[q + lane] : 0u, act, t_lo);
         }
+        // then the next level's rows (ring rows of earlier ticks -> HBM)
+        run_tasks(tick_end[2 * (Q.tick0 + k) + 1]);
       }
       ps_barrier();
     }

@@ -196,7 +196,7 @@ struct PyrFastPass {
   int w, h;             /* source level size */
   int spitch;           /* HBM row pitch (0: the caller's row stride) */
   long long soff;       /* pyramid offset (-1: the caller's frame) */
-  int R, tick0, nticks; /* rows per tick, first tick, ticks */
+  int R, tick0, nticks; /* rows per tick, first tick (tick_end holds 2 entries a tick), ticks */
   int rrows, rpitch;    /* level ring rows / pitch (16-B multiple) */
   int arows;            /* strength ring rows (pitch rpitch) and corner-bitmap rows */
   int bmw;              /* corner bitmap words per row (ceil(w / 32)) */

@@ -76,11 +76,13 @@ int main(int argc, char** argv) {
       const int T = Q.tick0 + k;
       std::vector<W> ws;
       std::vector<int> tickA;  // detection rows stage-A'd this tick
-      const int t1 = P.pf_tick_end[T];
-      for (int t = t0; t < t1; ++t) {
+      const int t1 = P.pf_tick_end[2 * T], t2 = P.pf_tick_end[2 * T + 1];
+      for (int t = t0; t < t2; ++t) {
+        const int phase = t < t1 ? 1 : 2;
         const uint32_t x = P.pf_tasks[2 * t], yw = P.pf_tasks[2 * t + 1];
         const int type = x & 15, pp = (x >> 4) & 31, c = (x >> 9) & 127, nr = (x >> 16) & 255;
         if (pp != p) fail("task pass", t, pp, p);
+        if ((type == ORBX_PS_RESIZE) != (phase == 2)) fail("task in the wrong phase", t, type, phase);
         if (type == ORBX_PF_FASTA) {
           const int ya = yw & 0x3FFF, sl = (yw >> 14) & 0xFF, as = (yw >> 22) & 0xFF;
           if (nr > 8 || c >= Q.nchunk) fail("fasta task", t, nr, c);
@@ -109,8 +111,8 @@ int main(int argc, char** argv) {
             const int s0 = std::min(std::max(sy, 0), Q.h - 1), s1 = std::min(std::max(sy + 1, 0), Q.h - 1);
             const uint32_t e = P.pf_ylut[2 * (Q.yl + y)];
             if ((int)(e & 0xFF) != s0 % Q.rrows || (int)((e >> 8) & 0xFF) != s1 % Q.rrows) fail("row lut", y, 0, 0);
-            rd(ring, s0 % Q.rrows + 3, s0, k, 1, "resize source");
-            rd(ring, s1 % Q.rrows + 3, s1, k, 1, "resize source");
+            rd(ring, s0 % Q.rrows + 3, s0, k, 2, "resize source");
+            rd(ring, s1 % Q.rrows + 3, s1, k, 2, "resize source");
             if (c == 0) {
               if (stR[y]) fail("row resized twice", y, 0, 0);
               stR[y] = 1;
@@ -119,10 +121,11 @@ int main(int argc, char** argv) {
         } else if (type == ORBX_PF_NMS) {
           const int y0 = yw & 0x3FFF, as = (yw >> 22) & 0xFF;
           if (as != y0 % Q.arows) fail("nms slot", y0, as, 0);
+          if (c > 1 || (Q.ncv == 1 && c)) fail("nms half", c, Q.ncv, 0);
           for (int y = y0; y < y0 + nr; ++y) {
-            if (y < Q.y0 || y >= Q.y1 || stN[y]) fail("nms row", y, 0, k);
-            if (y > Q.y0 && !stN[y - 1]) fail("nms out of order", y, 0, k);
-            stN[y] = 1;
+            if (y < Q.y0 || y >= Q.y1 || (stN[y] >> c) & 1) fail("nms row", y, c, k);
+            if (y > Q.y0 && !((stN[y - 1] >> c) & 1)) fail("nms out of order", y, c, k);
+            stN[y] |= 1 << c;
             for (int d = -1; d <= 1; ++d) {
               const int yy = y + d;
               if (yy < Q.y0 || yy >= Q.y1) continue;
@@ -134,7 +137,7 @@ int main(int argc, char** argv) {
           fail("task type", t, type, 0);
         }
       }
-      t0 = t1;
+      t0 = t2;
       apply(ws, k, 1);
       // phase 2: stage C on this tick's rows (windows and strength rows), loader rows
       for (int y : tickA) {
@@ -155,13 +158,14 @@ int main(int argc, char** argv) {
       }
       apply(ws, k, 0);
     }
+    const int halves = Q.ncv > 1 ? 3 : 1;
     for (int y = Q.y0; Q.fast && y < Q.y1; ++y)
-      if (!stA[y] || !stN[y]) fail("detection row not processed", p, y, stA[y] * 2 + stN[y]);
+      if (!stA[y] || stN[y] != halves) fail("detection row not processed", p, y, stA[y] * 4 + stN[y]);
     for (int y = 0; Q.next && y < Q.nh; ++y)
       if (!stR[y]) fail("next-level row not resized", p, y, 0);
   }
   if (t0 != (int)(P.pf_tasks.size() / 2)) fail("tasks left", t0, 0, 0);
-  printf("ok passes %d ticks %zu tasks %zu lds %d\n", F.np, P.pf_tick_end.size(), P.pf_tasks.size() / 2,
+  printf("ok passes %d ticks %zu tasks %zu lds %d\n", F.np, P.pf_tick_end.size() / 2, P.pf_tasks.size() / 2,
          F.lds_bytes);
   return 0;
 }

@@ -5,7 +5,7 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 TAG=${1:-run}
-ARGS="--steps 3 --warmup 1 --workload ${WL:-c4} --batch ${BATCH:-0} --no-cpu-baseline --no-latency --serial"
+ARGS="--steps 3 --warmup 1 --workload ${WL:-c4} --batch ${BATCH:-0} --no-cpu-baseline --no-latency --serial --pyramid ${PYR:-auto}"
 export TMPDIR=/tmp
 OUT=$GRAFT_REPO_ROOT/gpurun_out/prof_$TAG
 mkdir -p $OUT
