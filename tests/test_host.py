@@ -268,3 +268,26 @@ def test_fused_pyramid_fast_schedule(tmp_path, W, H, nf, L, sf):
                            os.path.join(csrc, "geometry.cpp"), "-o", str(exe)])
     r = subprocess.run([str(exe), str(W), str(H), str(nf), str(L), repr(sf)], capture_output=True, text=True)
     assert r.returncode == 0 and r.stdout.startswith("ok"), r.stdout + r.stderr
+
+
+@pytest.mark.parametrize("W,H,nf,L,sf,ini,mn,kind", [
+    (1920, 1080, 2000, 8, 1.2, 20, 7, "pan"), (640, 480, 1000, 8, 1.2, 12, 5, "rects"),
+    (1241, 376, 2000, 8, 1.2, 9, 15, "noise"), (752, 480, 1200, 8, 1.2, 7, 7, "pan"),
+    (640, 480, 1000, 1, 1.2, 20, 7, "noise"), (640, 480, 1000, 8, 1.3, 20, 7, "noise")])
+def test_fused_fast_emulation_matches_oracle_candidates(tmp_path, W, H, nf, L, sf, ini, mn, kind):
+    """k_pyrfast's FAST half emulated on the planner's tables
+    (tests/cpp/pyrfast_fast_emu.cpp: bitmap corners, NMS per cell-column half,
+    raster emit into per-cell minThFAST / iniThFAST lists, the per-cell choice)
+    gives the oracle's vToDistributeKeys of every level key for key."""
+    exe = tmp_path / "pffe"
+    csrc = os.path.join(PKG, "csrc")
+    odir = os.path.join(ROOT, "oracle")
+    subprocess.check_call(["gcc", "-O2", "-std=c11", "-mfma", "-ffp-contract=off", "-c",
+                           os.path.join(odir, "orb_oracle.c"), "-o", str(tmp_path / "oo.o")])
+    subprocess.check_call(["g++", "-O2", "-std=c++17", "-I", csrc, "-I", odir,
+                           os.path.join(ROOT, "tests", "cpp", "pyrfast_fast_emu.cpp"),
+                           os.path.join(csrc, "geometry.cpp"), str(tmp_path / "oo.o"), "-lm", "-o", str(exe)])
+    (tmp_path / "in.raw").write_bytes(synth.frame(W, H, 7, kind).tobytes())
+    r = subprocess.run([str(exe), str(tmp_path / "in.raw"), str(W), str(H), str(nf), str(L), repr(sf),
+                        str(ini), str(mn)], capture_output=True, text=True)
+    assert r.returncode == 0 and r.stdout.startswith("ok"), r.stdout + r.stderr
