@@ -189,9 +189,9 @@ int orbx_plan_debug_counters(orbx_plan* plan, int* fast_overflow_strips);
  *   ORBX_PLAN_FUSED       pyramid and cell FAST in one kernel (k_pyrfast:
  *                         one workgroup per frame streams every level once
  *                         through LDS, FAST on the rows as they pass).
- * Automatic: k_pyr_stream for batches of >= 64 frames when the planner
- * could schedule it (no exact-2x level, rings within the LDS budget), else
- * k_pyramid.  Returns ORBX_ERR_ARG for unknown flags or both at once,
+ * Automatic (0): k_pyramid then k_fast_strips, the fastest measured (the
+ * streaming kernels take 1.2-2x / 2.6x its time at the bench workloads,
+ * DESIGN.md §4 round 4).  Returns ORBX_ERR_ARG for unknown flags or both at once,
  * ORBX_ERR_UNSUPPORTED for ORBX_PLAN_PYR_STREAM / ORBX_PLAN_FUSED on a plan
  * the streaming schedule does not cover (the options are then unchanged). */
 #define ORBX_PLAN_PYR_TILES 1

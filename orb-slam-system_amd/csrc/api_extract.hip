@@ -360,11 +360,12 @@ static int extract_pass(orbx_plan* p, const uint8_t* frames, int n, size_t fstri
     fast_launch(0, P.nstrips_l0, p->s_aux);
     if (hipEventRecord(p->ev_aux1, p->s_aux) != hipSuccess) return ORBX_ERR_HIP;
   }
-  // K1 pyramid: row-streaming (one workgroup per frame) for batches, or the
-  // tile chain (many small workgroups per frame) for single frames
+  // K1 pyramid: the tile chain (many small workgroups per frame), or on
+  // request the row-streaming kernel (one workgroup per frame)
   if (!fused) p->timer.begin(ORBX_STAGE_RESIZE, s);  // fused: all in the FAST stage's launch
-  const bool stream = !fused && P.ps_ok && !(p->options & ORBX_PLAN_PYR_TILES) &&
-                      (n >= 64 || (p->options & ORBX_PLAN_PYR_STREAM));
+  // (measured slower than the tile chain at every bench workload -- DESIGN
+  // §4 round 4 -- so only on request)
+  const bool stream = !fused && P.ps_ok && (p->options & ORBX_PLAN_PYR_STREAM);
   if (stream) {
     // waves per frame: 16 up to 256 frames (one workgroup per CU), fewer for
     // larger batches (several frames per CU)

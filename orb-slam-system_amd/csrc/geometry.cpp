@@ -989,8 +989,13 @@ int plan_geometry(const orbx_params& p, int width, int height, Plan& P) {
   P.geo.bytes_pyr_fast = bytes;
   /* row-streaming pyramid: the longest tick whose rings fit the LDS budget */
   static const int ticks[] = {8, 6, 4, 3, 2, 1};
+  int ps_rpt = 4, ps_r0max = 8;
+#ifdef ORBX_PROFILING
+  if (const char* e = getenv("ORBX_DEBUG_PS_RPT")) ps_rpt = std::max(1, atoi(e));
+  if (const char* e = getenv("ORBX_DEBUG_PS_R0")) ps_r0max = std::max(1, atoi(e));
+#endif
   for (int r0 : ticks)
-    if (plan_pyr_stream(P, r0, 4)) break;
+    if (r0 <= ps_r0max && plan_pyr_stream(P, r0, ps_rpt)) break;
   /* fused pyramid + FAST: the longest level-0 tick that fits */
   for (int r0 : ticks)
     if (plan_pyr_fast(P, r0, 4)) break;

@@ -67,6 +67,13 @@ __device__ __forceinline__ void ps_hpass(const uint8_t* row, int hsh, const uint
 
 #define PS_LOAD_U 8 /* loader: loads in flight per lane */
 
+#ifndef PS_PROBE  // profiling builds only (tools/variant.sh): 1 = the loader skips its loads
+#define PS_PROBE 0
+#endif
+#ifndef PF_PROBE  // profiling builds only: skip 1 NMS, 2 FASTA, 4 resize, 8 stage C, 16 loads
+#define PF_PROBE 0
+#endif
+
 template <int NT>
 __device__ __forceinline__ void ps_loader(const uint8_t* __restrict__ src, size_t rstride, const PyrStream& S,
                                           uint8_t* __restrict__ lds, int lane, int aligned16) {
@@ -75,7 +82,7 @@ __device__ __forceinline__ void ps_loader(const uint8_t* __restrict__ src, size_
   const int rp = S.rpitch[0], rr = S.rrows[0];
   const uint32_t rs = (uint32_t)rstride;
   for (int k = 0; k < S.nticks; ++k) {
-    const int a = min(H0, S.r0 * k), b = min(H0, S.r0 * (k + 1));
+    const int a = min(H0, S.r0 * k), b = PS_PROBE & 1 ? a : min(H0, S.r0 * (k + 1));
     if (aligned16) {
       const int nu = (W0 + 15) >> 4, total = (b - a) * nu;
       for (int i0 = 0; i0 < total; i0 += 64 * PS_LOAD_U) {
@@ -640,10 +647,10 @@ __global__ __launch_bounds__(1024) void k_pyrfast(PF_KERNEL_ARGS) {
         const uint2 d = tasks[t];
         const int type = (int)(d.x & 15);
         if (type == ORBX_PF_FASTA) {
-          pf_fasta(Q, L, d.x, d.y, lane, L1, n1, t_lo, T & 1);
+          if (!(PF_PROBE & 2)) pf_fasta(Q, L, d.x, d.y, lane, L1, n1, t_lo, T & 1);
         } else if (type == ORBX_PS_RESIZE) {
-          pf_resize(Q, L, fpyr, ylut, d.x, (int)d.y, lane);
-        } else {
+          if (!(PF_PROBE & 4)) pf_resize(Q, L, fpyr, ylut, d.x, (int)d.y, lane);
+        } else if (!(PF_PROBE & 1)) {
           pf_nms(F, Q, L, fslots, fslots_hi, fccount, (int)(d.y & 0x3FFFu), (int)((d.x >> 16) & 255),
                  (int)((d.y >> 22) & 0xFFu), (int)((d.x >> 9) & 127), lane);
         }
@@ -669,7 +676,8 @@ __global__ __launch_bounds__(1024) void k_pyrfast(PF_KERNEL_ARGS) {
       const int par = T & 1;
       // ---- phase 1
       if (wave == 0) {
-        pf_load(Q, src, sp, L.ring, min(Q.h, Q.R * k), min(Q.h, Q.R * (k + 1)), lane, al16);
+        pf_load(Q, src, sp, L.ring, min(Q.h, Q.R * k), (PF_PROBE & 16) ? min(Q.h, Q.R * k) : min(Q.h, Q.R * (k + 1)),
+                lane, al16);
       } else {
         run_tasks(tick_end[2 * (Q.tick0 + k)]);
         // the wave's last even-test batch of the tick
@@ -685,7 +693,7 @@ __global__ __launch_bounds__(1024) void k_pyrfast(PF_KERNEL_ARGS) {
           L.misc[3 + (par ^ 1)] = 0;
         }
       } else {
-        const int n2 = min(L.misc[1 + par], ORBX_PF_L2CAP);
+        const int n2 = (PF_PROBE & 8) ? 0 : min(L.misc[1 + par], ORBX_PF_L2CAP);
         for (;;) {
           int v = 0;
           if (lane == 0) v = atomicAdd(&L.misc[3 + par], 1);

@@ -568,9 +568,9 @@ class Plan:
         return {"fast_overflow_strips": v.value}
 
     def set_options(self, pyramid="auto"):
-        """pyramid: 'auto' (row-streaming for batches of >= 64 frames), 'tiles'
-        (k_pyramid), 'stream' (k_pyr_stream for any batch) or 'fused' (pyramid
-        and cell FAST in one kernel, k_pyrfast); same results"""
+        """pyramid: 'auto' (= the tile pyramid, fastest measured), 'tiles'
+        (k_pyramid), 'stream' (k_pyr_stream, one workgroup per frame) or
+        'fused' (pyramid and cell FAST in one kernel, k_pyrfast); same results"""
         flags = {"auto": 0, "tiles": ORBX_PLAN_PYR_TILES, "stream": ORBX_PLAN_PYR_STREAM,
                  "fused": ORBX_PLAN_FUSED}[pyramid]
         _check(_lib.orbx_plan_set_options(self._h, flags), "orbx_plan_set_options")

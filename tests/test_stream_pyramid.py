@@ -97,12 +97,14 @@ def test_fused_thresholds_match_oracle(gpu, oracle, w, h, nf, L, ini, mn, kind, 
         assert np.array_equal(res[f][1], rd), "frame %d descriptors" % f
 
 
-def test_stream_pyramid_is_the_default_for_batches(gpu):
-    """64 frames: the automatic choice (k_pyr_stream) equals the tile path."""
+def test_stream_pyramid_batch_of_64_matches_tiles(gpu):
+    """64 frames (several rounds of workgroups per CU at 640x480): the
+    streaming pyramid equals the tile path (the automatic choice)."""
     import torch
     B, W, H = 64, 640, 480
     plan = gpu.Plan(gpu.params(1000, 1.2, 8, 20, 7), W, H, B)
     tf = torch.from_numpy(synth.frames(W, H, 200, B, "pan")).cuda()
+    plan.set_options("stream")
     plan.extract(tf)
     plan.check()
     auto = plan.results(B)
