@@ -97,12 +97,12 @@ void launch_match(const MProblem* d_probs, int nprob, const MNodePair* d_nps, in
         // list2 gathered straight into +-1 bytes
         v4i_* gx2 = reinterpret_cast<v4i_*>(d_gx2);
         if (six_words) {
-          hipLaunchKernelGGL(k_match_expand2<6>, dim3((max_n2 * 6 + 255) / 256, nnp), dim3(256), 0, s,
+          hipLaunchKernelGGL(k_match_expand2<6>, dim3((max_n2 * ORBM_EXPAND_PER_POS(6) + 255) / 256, nnp), dim3(256), 0, s,
                              d_probs, d_nps, gx2);
           hipLaunchKernelGGL((k_match_cand_mfma<6, MC_RT>), dim3((max_n1 + 128 * MC_RT - 1) / (128 * MC_RT), nnp), dim3(256), 0, s,
                              d_probs, d_nps, gx2, d_cand, d_rowinfo, d_ev);
         } else {
-          hipLaunchKernelGGL(k_match_expand2<8>, dim3((max_n2 * 8 + 255) / 256, nnp), dim3(256), 0, s,
+          hipLaunchKernelGGL(k_match_expand2<8>, dim3((max_n2 * ORBM_EXPAND_PER_POS(8) + 255) / 256, nnp), dim3(256), 0, s,
                              d_probs, d_nps, gx2);
           hipLaunchKernelGGL((k_match_cand_mfma<8, MC_RT>), dim3((max_n1 + 128 * MC_RT - 1) / (128 * MC_RT), nnp), dim3(256), 0, s,
                              d_probs, d_nps, gx2, d_cand, d_rowinfo, d_ev);

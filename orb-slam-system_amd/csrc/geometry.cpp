@@ -867,6 +867,11 @@ int plan_geometry(const orbx_params& p, int width, int height, Plan& P) {
 
   /* FAST cell grid (ComputeKeyPointsOctTree :298-340) for unique levels */
   long long slots = 0;
+  /* k_fast_strips' column walk only pays on wide levels */
+  int cw_minw = ORBX_FS_COLWALK_MINW;
+#ifdef ORBX_PROFILING
+  if (const char* e = getenv("ORBX_DEBUG_CW_MINW")) cw_minw = atoi(e);
+#endif
   for (int l = 0; l < L; ++l) {
     LevelInfo& lv = P.levels[l];
     const int minB = ORBX_MINB, maxBX = lv.w - ORBX_EDGE + 3, maxBY = lv.h - ORBX_EDGE + 3;
@@ -925,6 +930,7 @@ int plan_geometry(const orbx_params& p, int width, int height, Plan& P) {
         StripInfo st;
         st.level = l; st.x = a.x; st.y = a.y; st.w = b.x + b.w - a.x; st.h = a.h;
         st.cell_begin = row_first + j0; st.ncells = j1 - j0; st.wcell = wCell;
+        st.colwalk = lv.w >= cw_minw;
         P.strips.push_back(st);
         P.strip_max_w = std::max(P.strip_max_w, st.w);
         P.strip_max_h = std::max(P.strip_max_h, st.h);

@@ -640,6 +640,7 @@ __device__ __forceinline__ void fs_strip_body(
       probe_sink |= clo | chi;
       return;
 #endif
+#ifndef FS_N1_VGPR
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const uint32_t x = (j & 1) ? chi : clo;
@@ -651,6 +652,25 @@ __device__ __forceinline__ void fs_strip_body(
         if (k) L1n[pos] = (uint16_t)(ebase + (uint32_t)j);
         n1 += __popcll(bal);
       }
+#else
+      // profiling variant: the list length in a VGPR (same value in every
+      // lane): slot = mbcnt(ballot) with n1 as its addend, n1 += v_bcnt of
+      // both ballot halves -- 7 VALU + 2 SALU per append instead of 5 + 7.
+      // Measured slower (c4 FAST 1.248 vs 1.202 ms, round 4): the CU-shared
+      // scalar unit is not what binds this kernel, VALU issue is
+      uint32_t n1v = (uint32_t)n1;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint32_t x = (j & 1) ? chi : clo;
+        const bool k = ((j & 2) ? (x >> 16) : (x & 0xFFFFu)) != 0;
+        const unsigned long long bal = __ballot(k);
+        const uint32_t blo = (uint32_t)bal, bhi = (uint32_t)(bal >> 32);
+        const int pos = (int)__builtin_amdgcn_mbcnt_hi(bhi, __builtin_amdgcn_mbcnt_lo(blo, n1v));
+        if (k) L1[pos] = (uint16_t)(ebase + (uint32_t)j);
+        asm("v_bcnt_u32_b32 %0, %1, %0\n\tv_bcnt_u32_b32 %0, %2, %0" : "+v"(n1v) : "s"(blo), "s"(bhi));
+      }
+      n1 = __builtin_amdgcn_readfirstlane((int)n1v);
+#endif
 #ifdef FS_PROBE_SALU  // profiling only: FS_PROBE_SALU extra scalar instructions per group
       {
         int sv = __builtin_amdgcn_readfirstlane(n1);
@@ -955,13 +975,15 @@ __device__ __forceinline__ void fs_kernel(
   const uint8_t* s0 = base + (size_t)st.y * pitch + xal;
   // column walk (fs_strip_body): dword-aligned rows, band rows <= 4 waves x
   // FS_CW_RMAX, and the band's dword columns plus both halo dwords within
-  // the 64 lanes (every strip of the bench workloads but wCell-32 levels)
+  // the 64 lanes (every strip of the bench workloads but wCell-32 levels),
+  // on levels the planner marks (st.colwalk: wide levels, where it measured
+  // faster; block staging on the narrow ones)
 #ifdef FS_NO_COLWALK  // profiling variant: block-wide staging for every strip
   const bool cw = false;
 #else
   const int cg0 = (lead + 3) >> 2, cg1 = (lead + st.w) >> 2;
   const int cgb = cg0 - (((lead + 3) & 3) != 3 ? 1 : 0);
-  const bool cw = FS_NW == 4 && aligned && st.h - 6 <= FS_NW * FS_CW_RMAX && cg1 - cgb <= 63;
+  const bool cw = FS_NW == 4 && st.colwalk && aligned && st.h - 6 <= FS_NW * FS_CW_RMAX && cg1 - cgb <= 63;
 #endif
   if (!cw) {
     if (aligned16) stage_region<v4u, 4, FS_NT>(tile, tpitch, s0, pitch, st.h, (tw + 15) >> 4, tid);

@@ -530,9 +530,13 @@ template __global__ void k_match_cand_rows<6>(const MProblem*, const MNodePair*,
 // sum_k -(+1 if a_k == b_k else -1) = 2 h - K (h = Hamming distance), so an
 // accumulator started at K ends at 2 h and the candidate key
 // (h << 16 | position) is (C << 15) + position.  k_match_expand2 writes the
-// gathered list2 as such bytes; k_match_cand_mfma computes 32 positions x
-// 32 rows per wave step (v_mfma_i32_32x32x32_i8, K = 32 bits per step) and
-// keeps the VALU for the top-T insertion only.
+// gathered list2 as such values; k_match_cand_mfma computes 32 positions x
+// 32 rows per wave step and keeps the VALU for the top-T insertion only.
+// Default (ORBM_FP4): the values are e2m1 nibbles (+-1.0 are exact) on the
+// MX-scaled v_mfma_scale_f32_32x32x64_f8f6f4 with x1.0 block scales, K = 64
+// bits per instruction in the cycles the i8 form spends on 32, and half the
+// operand bytes; every partial sum is an integer below 2^24, so the f32
+// accumulator is exact.  ORBM_FP4 0: +-1 bytes on v_mfma_i32_32x32x32_i8.
 // ---------------------------------------------------------------------------
 typedef int v4i_ __attribute__((ext_vector_type(4)));
 typedef int v16i_ __attribute__((ext_vector_type(16)));
@@ -549,24 +553,54 @@ __device__ __forceinline__ v4i_ pm1_bytes(uint32_t bits, bool pos) {
   return r;
 }
 
-// gx2[(g2 + j) * 2 * NK + 2 * s + h] = bits 16h .. 16h+15 of dword s of
-// the descriptor at list position j of the node pair (desc2[feat2[off2 +
-// j]]), as +-1 bytes (a' = 2a - 1): the list2 gather and the expansion in
-// one pass (the MFMA path needs no packed copy)
+// 8 bits -> 8 nibbles (bit t -> bit 4t)
+__device__ __forceinline__ uint32_t spread8_nib(uint32_t x) {
+  x &= 0xFFu;
+  x = (x | (x << 12)) & 0x000F000Fu;
+  x = (x | (x << 6)) & 0x03030303u;
+  return (x | (x << 3)) & 0x11111111u;
+}
+
+// 32 bits of K (16 from one dword, then 16 from the next) -> 32 e2m1
+// nibbles: +1.0 (0x2) / -1.0 (0xA) for bit set / clear (pos = true), or the
+// reverse; nibble t of the fragment is K element t
+__device__ __forceinline__ v4i_ pm1_nibs(uint32_t lo16, uint32_t hi16, bool pos) {
+  const uint32_t base = pos ? 0xAAAAAAAAu : 0x22222222u;  // ^ 8 flips 0xA <-> 0x2 per set bit
+  v4i_ r;
+  r[0] = (int)(base ^ (spread8_nib(lo16) << 3));
+  r[1] = (int)(base ^ (spread8_nib(lo16 >> 8) << 3));
+  r[2] = (int)(base ^ (spread8_nib(hi16) << 3));
+  r[3] = (int)(base ^ (spread8_nib(hi16 >> 8) << 3));
+  return r;
+}
+
+// i8 form (ORBM_FP4 0): gx2[(g2 + j) * 2 * NK + 2 * s + h] = bits 16h ..
+// 16h+15 of dword s of the descriptor at list position j of the node pair
+// (desc2[feat2[off2 + j]]), as +-1 bytes (a' = 2a - 1).  fp4 form:
+// gx2[(g2 + j) * NK + 2 * m + h] = bits 16h .. 16h+15 of dwords 2m and
+// 2m + 1 as +-1 nibbles (16 B per lane half and K step).  The list2 gather
+// and the expansion in one pass (the MFMA path needs no packed copy).
 template <int NK>
 __global__ __launch_bounds__(256) void k_match_expand2(const MProblem* __restrict__ probs,
                                                        const MNodePair* __restrict__ nps,
                                                        v4i_* __restrict__ gx2) {
   const MNodePair NP = nps[blockIdx.y];
-  const int i = blockIdx.x * 256 + threadIdx.x;  // (position, dword)
-  const int j = i / NK, s = i - j * NK;
+  constexpr int PER = ORBM_EXPAND_PER_POS(NK);
+  const int i = blockIdx.x * 256 + threadIdx.x;  // (position, K step)
+  const int j = i / PER, s = i - j * PER;
   if (j >= NP.n2) return;
   const MProblem& P = probs[NP.prob];
   const uint32_t idx2 = P.feat2[NP.off2 + j];
+  v4i_* o = gx2 + ((size_t)(NP.g2 + j) * PER + s) * 2;
+#if ORBM_FP4
+  const uint2 w = reinterpret_cast<const uint2*>(P.desc2 + (size_t)idx2 * 32)[s];
+  o[0] = pm1_nibs(w.x & 0xFFFFu, w.y & 0xFFFFu, true);
+  o[1] = pm1_nibs(w.x >> 16, w.y >> 16, true);
+#else
   const uint32_t w = reinterpret_cast<const uint32_t*>(P.desc2 + (size_t)idx2 * 32)[s];
-  v4i_* o = gx2 + ((size_t)(NP.g2 + j) * NK + s) * 2;
   o[0] = pm1_bytes(w & 0xFFFFu, true);
   o[1] = pm1_bytes(w >> 16, true);
+#endif
 }
 template __global__ void k_match_expand2<6>(const MProblem*, const MNodePair*, v4i_*);
 template __global__ void k_match_expand2<8>(const MProblem*, const MNodePair*, v4i_*);
@@ -575,17 +609,53 @@ template __global__ void k_match_expand2<8>(const MProblem*, const MNodePair*, v
 // insertions of the lane's 16 (row, position) values on the VALU
 // hoff = 4h + (K << 15): the lane half's position offset and the K bias;
 // value i of the tile is position t0 + (i & 3) + 8 (i >> 2) + 4h
-template <int NK>
-__device__ __forceinline__ void mfma_tile(const v4i_ (&af)[NK], const v4i_ (&bf)[NK], uint32_t t0,
-                                          int n2, uint32_t hoff, uint32_t (&L)[ORBM_T]) {
+typedef int v8i_ __attribute__((ext_vector_type(8)));
+typedef float v16f_ __attribute__((ext_vector_type(16)));
+
+// e2m1 operand in the f8f6f4 builtin's 8-dword slot (the backend keeps only
+// the 4 dwords the FP4 format reads)
+__device__ __forceinline__ v8i_ fp4_slot(const v4i_& x) { return v8i_{x[0], x[1], x[2], x[3], 0, 0, 0, 0}; }
+
+// NS K steps (NK dwords: NK i8 steps of 32 bits, or NK / 2 fp4 steps of 64)
+// fp4 form: the accumulator's start value 2^23 + K in every element (see
+// mfma_tile), held in registers for the whole tile loop
+template <int NS>
+__device__ __forceinline__ v16f_ fp4_acc_init() {
+  const float c0 = 8388608.0f + (float)(64 * NS);
+  v16f_ ci = {c0, c0, c0, c0, c0, c0, c0, c0, c0, c0, c0, c0, c0, c0, c0, c0};
+  asm volatile("" : "+v"(ci));  // a live tuple, not a per-tile re-splat
+  return ci;
+}
+
+template <int NS>
+__device__ __forceinline__ void mfma_tile(const v4i_ (&af)[NS], const v4i_ (&bf)[NS], uint32_t t0,
+                                          int n2, uint32_t hoff, uint32_t (&L)[ORBM_T],
+                                          const v16f_& ci) {
+  uint32_t k[16];
+#if ORBM_FP4
+  // x1.0 block scales (E8M0 127); the f32 accumulator starts at 2^23 + K
+  // (ci; hoff's K term is 0 here), so it ends at 2^23 + 2h: an exact integer
+  // in [2^23, 2^24), whose bit pattern is 0x4B000000 + 2h, and 0x4B000000 <<
+  // 15 vanishes mod 2^32, so key = bits << 15 + position as in the i8 form
+  v16f_ C = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(fp4_slot(af[0]), fp4_slot(bf[0]), ci, 4, 4,
+                                                            0, 0x7F, 0, 0x7F);
+#pragma unroll
+  for (int s = 1; s < NS; ++s)
+    C = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(fp4_slot(af[s]), fp4_slot(bf[s]), C, 4, 4, 0,
+                                                        0x7F, 0, 0x7F);
+#pragma unroll
+  for (int i = 0; i < 16; ++i)
+    k[i] = (__float_as_uint(C[i]) << 15) + hoff + (t0 + (uint32_t)((i & 3) + 8 * (i >> 2)));
+#else
+  (void)ci;
   // accumulate from 0 (an inline-constant C operand, no per-tile init):
   // C = 2h - K, and K << 15 is folded into the position offsets
   v16i_ C = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[0], bf[0], v16i_{}, 0, 0, 0);
 #pragma unroll
-  for (int s = 1; s < NK; ++s) C = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[s], bf[s], C, 0, 0, 0);
-  uint32_t k[16];
+  for (int s = 1; s < NS; ++s) C = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[s], bf[s], C, 0, 0, 0);
 #pragma unroll
   for (int i = 0; i < 16; ++i) k[i] = ((uint32_t)C[i] << 15) + hoff + (t0 + (uint32_t)((i & 3) + 8 * (i >> 2)));
+#endif
   if (t0 + 32 > (uint32_t)n2) {  // last tile: positions past the list
 #pragma unroll
     for (int i = 0; i < 16; ++i)
@@ -637,9 +707,10 @@ __global__ __launch_bounds__(256) void k_match_cand_mfma(
   const MProblem P = probs[NP.prob];
   const uint32_t* f2 = P.feat2 + NP.off2;
   const int n2 = NP.n2;
+  constexpr int NS = ORBM_EXPAND_PER_POS(NK);  // MFMA K steps per tile
   int a[RT], idx1[RT];
   bool act[RT], v1[RT];
-  v4i_ bf[RT][NK];
+  v4i_ bf[RT][NS];
   uint32_t L[RT][ORBM_T];
   const uint32_t sent = (uint32_t)P.dcap << 16;
 #pragma unroll
@@ -657,23 +728,34 @@ __global__ __launch_bounds__(256) void k_match_cand_mfma(
     }
     const uint32_t dw[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
 #pragma unroll
-    for (int s = 0; s < NK; ++s) bf[t][s] = pm1_bytes((dw[s] >> (16 * h)) & 0xFFFFu, false);
+    for (int s = 0; s < NS; ++s)
+#if ORBM_FP4
+      bf[t][s] = pm1_nibs((dw[2 * s] >> (16 * h)) & 0xFFFFu, (dw[2 * s + 1] >> (16 * h)) & 0xFFFFu, false);
+#else
+      bf[t][s] = pm1_bytes((dw[s] >> (16 * h)) & 0xFFFFu, false);
+#endif
 #pragma unroll
     for (int u = 0; u < ORBM_T; ++u) L[t][u] = sent;
   }
-  const uint32_t hoff = (uint32_t)(4 * h) + ((uint32_t)(32 * NK) << 15);
-  const v4i_* gx = gx2 + (size_t)NP.g2 * NK * 2 + h;
-  v4i_ af[NK], an[NK];
+  // the lane half's position offset (+ the i8 form's K bias, see mfma_tile)
+  const uint32_t hoff = (uint32_t)(4 * h) + (ORBM_FP4 ? 0u : ((uint32_t)(32 * NK) << 15));
+  const v4i_* gx = gx2 + (size_t)NP.g2 * NS * 2 + h;
+  v4i_ af[NS], an[NS];
+#if ORBM_FP4
+  const v16f_ ci = fp4_acc_init<NS>();
+#else
+  const v16f_ ci = {};
+#endif
 #pragma unroll
-  for (int s = 0; s < NK; ++s) af[s] = n2 > 0 ? gx[(size_t)min(c, n2 - 1) * NK * 2 + 2 * s] : v4i_{0, 0, 0, 0};
+  for (int s = 0; s < NS; ++s) af[s] = n2 > 0 ? gx[(size_t)min(c, n2 - 1) * NS * 2 + 2 * s] : v4i_{0, 0, 0, 0};
   for (int t0 = 0; t0 < n2; t0 += 32) {  // wave-uniform
     const int pn = min(t0 + 32 + c, n2 - 1);
 #pragma unroll
-    for (int s = 0; s < NK; ++s) an[s] = gx[(size_t)pn * NK * 2 + 2 * s];  // next tile (clamped)
+    for (int s = 0; s < NS; ++s) an[s] = gx[(size_t)pn * NS * 2 + 2 * s];  // next tile (clamped)
 #pragma unroll
-    for (int t = 0; t < RT; ++t) mfma_tile<NK>(af, bf[t], (uint32_t)t0, n2, hoff, L[t]);
+    for (int t = 0; t < RT; ++t) mfma_tile<NS>(af, bf[t], (uint32_t)t0, n2, hoff, L[t], ci);
 #pragma unroll
-    for (int s = 0; s < NK; ++s) af[s] = an[s];
+    for (int s = 0; s < NS; ++s) af[s] = an[s];
   }
   // merge the two halves' lists of each row (keys unique: position inside)
   if (h) {

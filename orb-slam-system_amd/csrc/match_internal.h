@@ -16,6 +16,15 @@
 #define ORBM_TH_LOW 50     /* ORBmatcher::TH_LOW (ORBmatcher.cc:14)       */
 #define ORBM_HISTO 30      /* ORBmatcher::HISTO_LENGTH (ORBmatcher.cc:15) */
 #define ORBM_MAX_N2 65536  /* list positions / idx2 bitmap bound          */
+/* k_match_cand_mfma operands: 1 = e2m1 +-1 nibbles on the MX-scaled
+ * v_mfma_scale_f32_32x32x64_f8f6f4 (64 bits of K per instruction, 16 B per
+ * 32 bits of a position), 0 = +-1 bytes on v_mfma_i32_32x32x32_i8 (32 bits
+ * per instruction, 32 B); kernels_match.hip */
+#ifndef ORBM_FP4
+#define ORBM_FP4 1
+#endif
+/* k_match_expand2 threads per list position: one per MFMA K step */
+#define ORBM_EXPAND_PER_POS(NK) (ORBM_FP4 ? (NK) / 2 : (NK))
 
 struct MProblem {
   const uint8_t* desc1;

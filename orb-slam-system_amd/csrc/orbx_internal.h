@@ -56,6 +56,9 @@ struct LevelInfo {
 #define ORBX_BLUR_TW 128
 #define ORBX_BLUR_TH 32
 #define ORBX_STRIP_MAXW 256 /* FAST strip: band width budget per workgroup */
+#ifndef ORBX_FS_COLWALK_MINW
+#define ORBX_FS_COLWALK_MINW 700 /* narrowest level whose strips take the column walk */
+#endif
 
 struct CellInfo {
   int level; /* unique level */
@@ -73,6 +76,7 @@ struct StripInfo {
   int cell_begin; /* first cell (index into the CellInfo table) */
   int ncells;
   int wcell;
+  int colwalk;    /* planner's choice of k_fast_strips' column walk (when it applies) */
 };
 
 /* per-level storage of the pyramid, passed by value to kernels that only
