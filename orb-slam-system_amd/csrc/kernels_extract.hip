@@ -277,6 +277,56 @@ __global__ __launch_bounds__(256) void k_pyramid(const uint8_t* __restrict__ fra
         const bool any_x = gx0 + 4 > X.z && gx0 < X.w;
         uint8_t* gdst = pyr + (size_t)f * pstride + S.off[s];
         const int gp = S.pitch[s];
+#ifdef PYR_RUNS
+        // row runs: thread slot r0 takes destination rows [r0 L, r0 L + L)
+        // in order, so a source row's horizontal pass (D & ~15 of the 4
+        // columns) is kept for the next destination row, whose first source
+        // row it is when the source advances by one (5 of 6 rows at scale
+        // 1.2); reused only when every active lane of the wave can (a
+        // wave-uniform branch), else recomputed
+        auto hpass = [&](int sy, uint32_t (&d)[4]) {
+          const uint32_t* Rw = reinterpret_cast<const uint32_t*>(cur + __mul24(sy, cpitch) + hbase);
+          const uint32_t lo = __builtin_amdgcn_alignbyte(Rw[1], Rw[0], hsh);
+          const uint32_t hi = __builtin_amdgcn_alignbyte(Rw[2], Rw[1], hsh);
+#pragma unroll
+          for (int k = 0; k < 4; ++k)
+            d[k] = __builtin_amdgcn_udot2(as_us2(__builtin_amdgcn_perm(hi, lo, hsel[k])), as_us2(hcoef[k]), 0u,
+                                          false) & 0xFFFFF0u;
+        };
+        int L = (nrows + R - 1) / R;
+#ifdef PYR_RUN5
+        L = (L + 4) / 5 * 5;  // runs in phase with scale 1.2's 5-row source pattern
+#endif
+        const int rend = min(r0 * L + L, nrows);
+        uint32_t hp[4] = {0, 0, 0, 0};
+        int psy = -1;
+        for (int r = r0 * L; r < rend; ++r) {
+          const uint2 e = yl[yo + r];
+          const int sy0 = (int)(e.x & 0xFFFF), sy1 = (int)(e.x >> 16);
+          uint32_t d0[4], d1[4];
+          if (__ballot(sy0 != psy) == 0ull) {  // wave-uniform
+#pragma unroll
+            for (int k = 0; k < 4; ++k) d0[k] = hp[k];
+          } else {
+            hpass(sy0, d0);
+          }
+          hpass(sy1, d1);
+          const uint64_t b0s = (uint64_t)((e.y & 0xFFFu) << 12), b1s = (uint64_t)(((e.y >> 16) & 0xFFFu) << 12);
+          uint32_t v[4];
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const uint32_t t0 = (uint32_t)((b0s * (uint64_t)d0[k]) >> 32);
+            const uint32_t t1 = (uint32_t)((b1s * (uint64_t)d1[k]) >> 32);
+            v[k] = (t0 + t1 + 2u) >> 2;
+            hp[k] = d1[k];
+          }
+          psy = sy1;
+          const uint32_t packed = __builtin_amdgcn_perm(v[1], v[0], 0x0C0C0400u) | __builtin_amdgcn_perm(v[3], v[2], 0x04000C0Cu);
+          *reinterpret_cast<uint32_t*>(nxt + r * dpitch + 4 * cg) = packed;
+          if (PYR_STORE_ON && any_x)
+            *reinterpret_cast<uint32_t*>(gdst + (uint32_t)((Y.x + r) * gp + gx0)) = packed;
+        }
+#else
         // PYR_U rows per iteration: every LDS read of the group is issued
         // before the first store (cur/nxt alias as far as the compiler knows)
         for (int rb = r0; rb < nrows; rb += PYR_U * R) {
@@ -327,6 +377,7 @@ __global__ __launch_bounds__(256) void k_pyramid(const uint8_t* __restrict__ fra
             }
           }
         }
+#endif
       }
     }
 #ifndef PYR_PROBE_NOSYNC  // profiling only: level passes without the block barrier (wrong pixels)
@@ -569,6 +620,14 @@ __device__ __forceinline__ void fs_strip_body(
   };
   {
     const uint32_t tt = (uint32_t)t_lo * 0x00010001u;
+    // stage A's v_perm selectors in SGPRs, set once (as literals the compiler
+    // re-materialised some into VGPRs every group: gfx9 VOP3 takes no literal)
+    uint32_t sel_v0, sel_v1, sel_a4lo, sel_a4hi, sel_a12hi;
+    asm volatile("s_mov_b32 %0, 0x0c020c00" : "=s"(sel_v0));
+    asm volatile("s_mov_b32 %0, 0x0c030c01" : "=s"(sel_v1));  // also a12 of the low half
+    asm volatile("s_mov_b32 %0, 0x0c050c03" : "=s"(sel_a4lo));
+    asm volatile("s_mov_b32 %0, 0x0c060c04" : "=s"(sel_a4hi));
+    asm volatile("s_mov_b32 %0, 0x0c040c02" : "=s"(sel_a12hi));
     // one 4-pixel group: tile byte offset off = r * tpitch + 4 g, list entry
     // ebase = r << 9 | 4 g; a lane with threshold 0xFF00 per 16-bit lane
     // (padding) finds no survivors; zf: zero the group's strength-map dword
@@ -596,15 +655,15 @@ __device__ __forceinline__ void fs_strip_body(
       const uint32_t w0 = q.w0, w1 = q.w1, w2 = q.w2, up = q.up, dn = q.dn;
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
-        const uint32_t sel = h ? 0x0c030c01u : 0x0c020c00u;
+        const uint32_t sel = h ? sel_v1 : sel_v0;
         const us2 v = as_us2(__builtin_amdgcn_perm(0u, w1, sel));
         const us2 a0 = as_us2(__builtin_amdgcn_perm(0u, dn, sel));
         const us2 a8 = as_us2(__builtin_amdgcn_perm(0u, up, sel));
         // (x+3, y) and (x-3, y) straight from the byte pairs {w2:w1} / {w1:w0}
         // (one v_perm each, no v_alignbyte): pixel i's point 4 is byte i+3 of
         // {w2:w1}, its point 12 byte i+1 of {w1:w0}
-        const us2 a4 = as_us2(__builtin_amdgcn_perm(w2, w1, h ? 0x0c060c04u : 0x0c050c03u));
-        const us2 a12 = as_us2(__builtin_amdgcn_perm(w1, w0, h ? 0x0c040c02u : 0x0c030c01u));
+        const us2 a4 = as_us2(__builtin_amdgcn_perm(w2, w1, h ? sel_a4hi : sel_a4lo));
+        const us2 a12 = as_us2(__builtin_amdgcn_perm(w1, w0, h ? sel_a12hi : sel_v1));
         const us2 t2 = as_us2(ttl);
         const us2 mb = __builtin_elementwise_min(__builtin_elementwise_max(a0, a8),
                                                  __builtin_elementwise_max(a4, a12));
@@ -612,7 +671,8 @@ __device__ __forceinline__ void fs_strip_body(
                                                  __builtin_elementwise_min(a4, a12));
         const us2 db = __builtin_elementwise_sub_sat(mb, v + t2);       // > 0 iff brighter arc
         const us2 dd = __builtin_elementwise_sub_sat(__builtin_elementwise_sub_sat(v, md), t2);
-        const uint32_t x = as_u32(db) | as_u32(dd);
+        uint32_t x = as_u32(db) | as_u32(dd);
+        asm("" : "+v"(x));  // one OR per half, shared by both pixels' tests
         if (h) chi = x; else clo = x;
       }
       if (zf) *reinterpret_cast<uint32_t*>(zp) = 0u;
@@ -644,7 +704,7 @@ __device__ __forceinline__ void fs_strip_body(
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const uint32_t x = (j & 1) ? chi : clo;
-        const bool k = ((j & 2) ? (x >> 16) : (x & 0xFFFFu)) != 0;
+        const bool k = (j & 2) ? x > 0xFFFFu : (uint16_t)x != 0;
         const unsigned long long bal = __ballot(k);
         const int pos = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
                                                        __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
@@ -728,9 +788,14 @@ __device__ __forceinline__ void fs_strip_body(
             q.up = V[k];
             q.w1 = V[k + 3];
             q.dn = V[k + 6];
-            q.w0 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)V[k + 3], 0x138, 0xf, 0xf, false);  // wave_shr:1
-            q.w2 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)V[k + 3], 0x130, 0xf, 0xf, false);  // wave_shl:1
-            gtest(q, zrow + k * tpitch, er + ((uint32_t)k << 9), tl, lact);
+            // bound_ctrl: the lane past the wave's edge reads 0 (a halo lane,
+            // its results are dropped) and no "old" operand is materialised
+            q.w0 = (uint32_t)__builtin_amdgcn_mov_dpp((int)V[k + 3], 0x138, 0xf, 0xf, true);  // wave_shr:1
+            q.w2 = (uint32_t)__builtin_amdgcn_mov_dpp((int)V[k + 3], 0x130, 0xf, 0xf, true);  // wave_shl:1
+            // zero-fill in every lane: halo lanes (and lanes repeating the
+            // right halo) zero dwords wholly outside [c0, c1), where no
+            // strength is ever written (gb >= 0 since c0 >= 3)
+            gtest(q, zrow + k * tpitch, er + ((uint32_t)k << 9), tl, true);
           }
         }
       }

@@ -690,7 +690,10 @@ __device__ __forceinline__ void mfma_tile(const v4i_ (&af)[NS], const v4i_ (&bf)
 #define MC_RT 2
 #endif
 template <int NK, int RT>
-__global__ __launch_bounds__(256) void k_match_cand_mfma(
+#ifndef MC_WPE
+#define MC_WPE 4 /* waves per SIMD the register budget is cut for */
+#endif
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MC_WPE))) void k_match_cand_mfma(
     const MProblem* __restrict__ probs, const MNodePair* __restrict__ nps,
     const v4i_* __restrict__ gx2, uint2* __restrict__ cand, int4* __restrict__ rowinfo,
     int2* __restrict__ ev) {
@@ -748,6 +751,7 @@ __global__ __launch_bounds__(256) void k_match_cand_mfma(
 #endif
 #pragma unroll
   for (int s = 0; s < NS; ++s) af[s] = n2 > 0 ? gx[(size_t)min(c, n2 - 1) * NS * 2 + 2 * s] : v4i_{0, 0, 0, 0};
+#ifdef MC_NO_PINGPONG  // profiling variant: one fragment set copied forward per tile
   for (int t0 = 0; t0 < n2; t0 += 32) {  // wave-uniform
     const int pn = min(t0 + 32 + c, n2 - 1);
 #pragma unroll
@@ -757,6 +761,23 @@ __global__ __launch_bounds__(256) void k_match_cand_mfma(
 #pragma unroll
     for (int s = 0; s < NS; ++s) af[s] = an[s];
   }
+#else
+  // two fragment sets in turn (tile t0 from af while an loads t0 + 32, then
+  // the reverse): no register copies per tile
+  for (int t0 = 0; t0 < n2; t0 += 64) {  // wave-uniform
+    const int pn = min(t0 + 32 + c, n2 - 1);
+#pragma unroll
+    for (int s = 0; s < NS; ++s) an[s] = gx[(size_t)pn * NS * 2 + 2 * s];
+#pragma unroll
+    for (int t = 0; t < RT; ++t) mfma_tile<NS>(af, bf[t], (uint32_t)t0, n2, hoff, L[t], ci);
+    if (t0 + 32 >= n2) break;  // wave-uniform
+    const int pf = min(t0 + 64 + c, n2 - 1);
+#pragma unroll
+    for (int s = 0; s < NS; ++s) af[s] = gx[(size_t)pf * NS * 2 + 2 * s];
+#pragma unroll
+    for (int t = 0; t < RT; ++t) mfma_tile<NS>(an, bf[t], (uint32_t)(t0 + 32), n2, hoff, L[t], ci);
+  }
+#endif
   // merge the two halves' lists of each row (keys unique: position inside)
   if (h) {
 #pragma unroll
