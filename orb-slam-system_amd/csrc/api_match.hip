@@ -22,9 +22,6 @@ __global__ void k_match_gather2(const MProblem*, const MNodePair*, uint4*, uint3
 typedef int v4i_ __attribute__((ext_vector_type(4)));
 template <int NK>
 __global__ void k_match_expand2(const MProblem*, const MNodePair*, v4i_*);
-#ifndef MC_RT
-#define MC_RT 2 /* row tiles of 32 per wave in k_match_cand_mfma */
-#endif
 template <int NK, int RT>
 __global__ void k_match_cand_mfma(const MProblem*, const MNodePair*, const v4i_*, uint2*, int4*,
                                   int2*);

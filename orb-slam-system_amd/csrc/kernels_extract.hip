@@ -277,56 +277,6 @@ __global__ __launch_bounds__(256) void k_pyramid(const uint8_t* __restrict__ fra
         const bool any_x = gx0 + 4 > X.z && gx0 < X.w;
         uint8_t* gdst = pyr + (size_t)f * pstride + S.off[s];
         const int gp = S.pitch[s];
-#ifdef PYR_RUNS
-        // row runs: thread slot r0 takes destination rows [r0 L, r0 L + L)
-        // in order, so a source row's horizontal pass (D & ~15 of the 4
-        // columns) is kept for the next destination row, whose first source
-        // row it is when the source advances by one (5 of 6 rows at scale
-        // 1.2); reused only when every active lane of the wave can (a
-        // wave-uniform branch), else recomputed
-        auto hpass = [&](int sy, uint32_t (&d)[4]) {
-          const uint32_t* Rw = reinterpret_cast<const uint32_t*>(cur + __mul24(sy, cpitch) + hbase);
-          const uint32_t lo = __builtin_amdgcn_alignbyte(Rw[1], Rw[0], hsh);
-          const uint32_t hi = __builtin_amdgcn_alignbyte(Rw[2], Rw[1], hsh);
-#pragma unroll
-          for (int k = 0; k < 4; ++k)
-            d[k] = __builtin_amdgcn_udot2(as_us2(__builtin_amdgcn_perm(hi, lo, hsel[k])), as_us2(hcoef[k]), 0u,
-                                          false) & 0xFFFFF0u;
-        };
-        int L = (nrows + R - 1) / R;
-#ifdef PYR_RUN5
-        L = (L + 4) / 5 * 5;  // runs in phase with scale 1.2's 5-row source pattern
-#endif
-        const int rend = min(r0 * L + L, nrows);
-        uint32_t hp[4] = {0, 0, 0, 0};
-        int psy = -1;
-        for (int r = r0 * L; r < rend; ++r) {
-          const uint2 e = yl[yo + r];
-          const int sy0 = (int)(e.x & 0xFFFF), sy1 = (int)(e.x >> 16);
-          uint32_t d0[4], d1[4];
-          if (__ballot(sy0 != psy) == 0ull) {  // wave-uniform
-#pragma unroll
-            for (int k = 0; k < 4; ++k) d0[k] = hp[k];
-          } else {
-            hpass(sy0, d0);
-          }
-          hpass(sy1, d1);
-          const uint64_t b0s = (uint64_t)((e.y & 0xFFFu) << 12), b1s = (uint64_t)(((e.y >> 16) & 0xFFFu) << 12);
-          uint32_t v[4];
-#pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            const uint32_t t0 = (uint32_t)((b0s * (uint64_t)d0[k]) >> 32);
-            const uint32_t t1 = (uint32_t)((b1s * (uint64_t)d1[k]) >> 32);
-            v[k] = (t0 + t1 + 2u) >> 2;
-            hp[k] = d1[k];
-          }
-          psy = sy1;
-          const uint32_t packed = __builtin_amdgcn_perm(v[1], v[0], 0x0C0C0400u) | __builtin_amdgcn_perm(v[3], v[2], 0x04000C0Cu);
-          *reinterpret_cast<uint32_t*>(nxt + r * dpitch + 4 * cg) = packed;
-          if (PYR_STORE_ON && any_x)
-            *reinterpret_cast<uint32_t*>(gdst + (uint32_t)((Y.x + r) * gp + gx0)) = packed;
-        }
-#else
         // PYR_U rows per iteration: every LDS read of the group is issued
         // before the first store (cur/nxt alias as far as the compiler knows)
         for (int rb = r0; rb < nrows; rb += PYR_U * R) {
@@ -377,7 +327,6 @@ __global__ __launch_bounds__(256) void k_pyramid(const uint8_t* __restrict__ fra
             }
           }
         }
-#endif
       }
     }
 #ifndef PYR_PROBE_NOSYNC  // profiling only: level passes without the block barrier (wrong pixels)

@@ -686,13 +686,7 @@ __device__ __forceinline__ void mfma_tile(const v4i_ (&af)[NS], const v4i_ (&bf)
 // gx2 (L1/L2: the waves of a workgroup and the node pair's other workgroups
 // read the same tiles), one tile ahead; each fragment feeds RT MFMA chains.
 // Validity arrays are not supported (k_match_cand_rows).
-#ifndef MC_RT
-#define MC_RT 2
-#endif
 template <int NK, int RT>
-#ifndef MC_WPE
-#define MC_WPE 4 /* waves per SIMD the register budget is cut for */
-#endif
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MC_WPE))) void k_match_cand_mfma(
     const MProblem* __restrict__ probs, const MNodePair* __restrict__ nps,
     const v4i_* __restrict__ gx2, uint2* __restrict__ cand, int4* __restrict__ rowinfo,

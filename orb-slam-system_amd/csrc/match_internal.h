@@ -23,6 +23,15 @@
 #ifndef ORBM_FP4
 #define ORBM_FP4 1
 #endif
+/* row tiles of 32 per wave in k_match_cand_mfma (round 4, fp4 operands:
+ * RT 1 at 95 VGPRs / 5 waves per SIMD beat RT 2 / 4 waves by 3 %, RT 4 lost
+ * 15 %) and the waves per SIMD its register budget is cut for */
+#ifndef MC_RT
+#define MC_RT 1
+#endif
+#ifndef MC_WPE
+#define MC_WPE 5
+#endif
 /* k_match_expand2 threads per list position: one per MFMA K step */
 #define ORBM_EXPAND_PER_POS(NK) (ORBM_FP4 ? (NK) / 2 : (NK))
 
