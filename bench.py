@@ -85,6 +85,9 @@ def parse():
                     help="pyramid kernel (orbx_plan_set_options; identical results)")
     ap.add_argument("--serial", action="store_true",
                     help="time only the serial step (no extraction/matching overlap across steps)")
+    ap.add_argument("--split", type=int, default=2,
+                    help="pipelined step: extract the batch as this many sub-batches, each on its own "
+                         "stream (same frames and work; the matcher waits for all of them)")
     ap.add_argument("--traffic", default="", help="PMC traffic summary (default profiles/traffic_<workload>.json)")
     a = ap.parse_args()
     wl = dict(WORKLOADS[a.workload])
@@ -627,6 +630,21 @@ def main_mono(args, wl):
     if match and not args.serial:
         sa = torch.cuda.Stream(device=dev)
         sb = torch.cuda.Stream(device=dev, priority=-1)
+        # --split S: S plans of B/S frames, sub-batch j extracted on stream
+        # sx[j] (j = 0 is sa, which also does the slot-0 copy and the boundary
+        # exchange), so one sub-batch's latency-bound kernels (quadtree, the
+        # launch tails) overlap another's
+        S = args.split
+        if S < 1:
+            raise SystemExit("bench.py: --split must be >= 1")
+        if B % S:
+            S = 1  # odd batches: one plan (the default 2 needs an even batch)
+        sub = B // S
+        subplans = [plan] if S == 1 else [orbx.Plan(prm, W, H, sub, device=local) for _ in range(S)]
+        for p_ in subplans:
+            p_.set_options(pyramid=args.pyramid)
+        sx = [sa] + [torch.cuda.Stream(device=dev) for _ in range(S - 1)]
+        ev_s = [torch.cuda.Event() for _ in range(S)]
         bufs = [(kps, desc, counts),
                 (torch.zeros_like(kps), torch.zeros_like(desc), torch.zeros_like(counts))]
         ev_x = [torch.cuda.Event(), torch.cuda.Event()]
@@ -649,7 +667,18 @@ def main_mono(args, wl):
                     k_i[0].copy_(k_j[B])
                     d_i[0].copy_(d_j[B])
                     c_i[0:1].copy_(c_j[B:B + 1])
-                plan.extract(frames, stream=sa, out=(k_i[1:], d_i[1:], c_i[1:]))
+            for j in range(1, S):
+                sx[j].wait_event(ev_m[i])
+            for j in range(S):
+                with torch.cuda.stream(sx[j]):
+                    lo, hi = 1 + j * sub, 1 + (j + 1) * sub
+                    subplans[j].extract(frames[j * sub:(j + 1) * sub], stream=sx[j],
+                                        out=(k_i[lo:hi], d_i[lo:hi], c_i[lo:hi]))
+                    if j:
+                        ev_s[j].record(sx[j])
+            with torch.cuda.stream(sa):
+                for j in range(1, S):
+                    sa.wait_event(ev_s[j])
                 if world > 1:
                     xch.ring_step(dist, rank, (k_i[B], d_i[B], c_i[B:B + 1]), (k_i[0], d_i[0], c_i[0:1]))
                 ev_x[i].record(sa)
@@ -703,7 +732,8 @@ def main_mono(args, wl):
         if world > 1:
             dist.barrier()
         el = finish_time(torch, dist, world, dev, time.perf_counter() - t0)
-        plan.check()
+        for p_ in subplans:
+            p_.check()
         # the frames are the same every step: the pipelined matches must equal
         # the serial loop's bit for bit
         same = bool(torch.equal(mp.match12[:B], ref12))
@@ -745,6 +775,9 @@ def main_mono(args, wl):
     if pipe is not None:
         out["step_mode"] = ("pipelined: step k+1's extraction overlaps step k's matching on a second, "
                             "high-priority stream (same work per step, matches equal the serial step's)")
+        if len(subplans) > 1:
+            out["step_mode"] += ("; extraction as %d sub-batches of %d frames on %d streams"
+                                 % (len(subplans), B // len(subplans), len(subplans)))
         out["serial"] = {"value": round(world * B * args.steps / el_serial, 2),
                          "ms_per_step": round(el_serial / args.steps * 1e3, 3),
                          "note": "stage times and roofline entries come from this serial timed loop "

@@ -1476,7 +1476,9 @@ __device__ __forceinline__ void brief_issue(const BriefKp& k, BriefRegs& R, int 
   const uint32_t c4 = (uint32_t)(ln % 12) * 4u, r0 = (uint32_t)(ln / 12);
   R.ht = c_htask.v[k.x - k.px0 - 21][lane];  // cc = 21..24
   if (k.inside) {
-    const uint8_t* b = k.img + (size_t)k.py0 * k.pitch + k.px0;  // wave-uniform
+    // wave-uniform; a level is < 4 GB: 32-bit scalar offset (a size_t
+    // product here was a quarter-rate v_mad_u64_u32 per keypoint)
+    const uint8_t* b = k.img + ((uint32_t)k.py0 * (uint32_t)k.pitch + (uint32_t)k.px0);
 #pragma unroll
     for (int u = 0; u < 9; ++u) {
       const uint32_t row = min(r0 + 5u * u, (uint32_t)(KP_ROWS - 1));
@@ -1551,6 +1553,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OB_WPE))) v
   const uint32_t* Q = qout + (size_t)f * qout_stride;
   const uint32_t* QP = qperm + (size_t)f * qout_stride;
   uint32_t(*P)[KP_PSTRIDE] = patch[wave];
+  orbx_keypoint* const kpsf = kps + (size_t)f * kcap;  // this frame's outputs
+  // IC_Angle weights, the lane's part (b0 = 24 for odd lanes, else 4)
+  const uint32_t Wlane = (uint32_t)((lane & 1) ? 24 + 19 : 4 + 19) * 0x01010101u + 0x03020100u;
+  uint8_t* const descf = desc + (size_t)f * kcap * 32;
   // sincos exception keys, entries lane and lane + 64 (brief_sincos)
   const uint32_t exk0 = ORBX_SINCOS_EXC[lane < ORBX_SINCOS_NEXC ? lane : 0][0];
   const uint32_t exk1 = lane + 64 < ORBX_SINCOS_NEXC ? ORBX_SINCOS_EXC[lane + 64][0] : 0xFFFFFFFFu;
@@ -1651,8 +1657,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OB_WPE))) v
     for (int k = 0; k < (OB_PROBE == 1 ? 0 : 3); ++k) {  // OB_PROBE 1: no horizontal pass (profiling only)
       const uint32_t e = (hte >> (8 * k)) & 0xFFu;
       if (e == 0xFFu) continue;
-      const int rp = (int)((e * 205u) >> 11), qi = (int)e - 10 * rp;  // e / 10 (exact for e < 256)
+      // e / 10 (exact for e < 256); 24-bit multiplies throughout this loop
+      // (v_mul_lo_u32 / v_mad_u64_u32 are quarter rate)
+      const int rp = (int)(__umul24(e, 205u) >> 11), qi = (int)e - 10 * rp;
       const int q = qlo + qi;
+      // the task's hblur column base (4 qi) * KP_HSTRIDE + rp as one
+      // full-rate 24-bit multiply-add (left to the compiler, the product
+      // was reassociated into a quarter-rate v_mul_lo_u32)
+      uint32_t hcol;
+      asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(hcol) : "v"(qi), "s"(4 * KP_HSTRIDE), "v"(rp));
       const int r0 = 2 * rp, r1 = min(2 * rp + 1, KP_ROWS - 1);
       const int d0 = max(q - 1, 0);  // q == 0: the weights of dword q-1 are 0 for the columns used
       const uint32_t a0 = P[r0][d0], a1 = P[r0][q], a2 = P[r0][q + 1];
@@ -1663,7 +1676,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OB_WPE))) v
         const uint32_t W0 = kb_w(m, 0), W1 = kb_w(m, 1), W2 = kb_w(m, 2);
         const uint32_t h0 = __builtin_amdgcn_udot4(a2, W2, __builtin_amdgcn_udot4(a1, W1, __builtin_amdgcn_udot4(a0, W0, 0u, false), false), false);
         const uint32_t h1 = __builtin_amdgcn_udot4(b2, W2, __builtin_amdgcn_udot4(b1, W1, __builtin_amdgcn_udot4(b0, W0, 0u, false), false), false);
-        (&hblur[wave][0][0])[__mul24(4 * qi + m, KP_HSTRIDE) + rp] = h0 | (h1 << 16);  // column 4 q + m - 4 qlo
+        (&hblur[wave][0][0])[hcol + m * KP_HSTRIDE] = h0 | (h1 << 16);  // column 4 q + m - 4 qlo
       }
     }
   }
@@ -1686,7 +1699,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OB_WPE))) v
     const int nhi = min(max(cc + um - b0 + 1, 0), 20), nlo = min(max(cc - um - b0, 0), 20);
     const uint32_t bits = ((1u << nhi) - 1u) & ~((1u << nlo) - 1u);
     const uint32_t* rowp = &P[cr + v][b0 >> 2];
-    const uint32_t W = (uint32_t)(b0 - cc + 19) * 0x01010101u + 0x03020100u;
+    // W = (b0 - cc + 19) * 0x01010101 + 0x03020100 (mod 2^32: byte j of W +
+    // 0x04040404 k is the weight u + 19 of column b0 + j + 4 k wherever the
+    // disk mask keeps it) as the lane's loop-invariant part minus the
+    // keypoint's scalar cc * 0x01010101: one VALU instead of a quarter-rate
+    // v_mul_lo_u32 (a byte splat of the difference is not equivalent: the
+    // carries of the whole-word form matter when b0 - cc + 19 < 0)
+    const uint32_t W = Wlane - (uint32_t)cc * 0x01010101u;
     uint32_t s = 0, m = 0;
 #pragma unroll
     for (int k = 0; k < 5; ++k) {
@@ -1698,7 +1717,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OB_WPE))) v
       s = __builtin_amdgcn_udot4(I, ones, s, false);
       m = __builtin_amdgcn_udot4(I, (W + 0x04040404u * k) & bmask, m, false);
     }
-    m10 = (int)m - 19 * (int)s;
+    m10 = (int)m - __mul24(19, (int)s);
     m01 = __mul24(v, (int)s);
   }
   // wave sums (uniform: scalar angle / sincos table) without LDS round trips
@@ -1732,7 +1751,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OB_WPE))) v
       const int row = (int)__builtin_rintf(__builtin_fmaf(fx, sn, ya));
       const int col = (int)__builtin_rintf(__builtin_fmaf(fx, cs, -yb));
       const int rt = cr + row - 3;  // first vertical tap (patch row)
-      const uint32_t* hc = &hblur[wave][hcc + col][rt >> 1];
+      const uint32_t* hc = &hblur[wave][0][0] + (__mul24(hcc + col, KP_HSTRIDE) + (rt >> 1));  // col may be < 0
       const uint32_t v0 = hc[0], v1 = hc[1], v2 = hc[2], v3 = hc[3];
       // row pairs (2k, 2k+1): taps rt..rt+6 start at the pair's low half
       // (rt even) or high half (rt odd)
@@ -1747,7 +1766,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OB_WPE))) v
   }
   if (lane < 4) {
     const uint64_t w = lane == 0 ? words[0] : lane == 1 ? words[1] : lane == 2 ? words[2] : words[3];
-    reinterpret_cast<uint64_t*>(desc + ((size_t)f * kcap + me.oi) * 32)[lane] = w;
+    reinterpret_cast<uint64_t*>(descf + (uint32_t)me.oi * 32u)[lane] = w;
   }
   if (lane == 0) {
     orbx_keypoint kp;
@@ -1762,7 +1781,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OB_WPE))) v
     kp.response = (float)score;
     kp.octave = l;
     kp.class_id = -1;
-    kps[(size_t)f * kcap + me.oi] = kp;
+    *reinterpret_cast<orbx_keypoint*>(reinterpret_cast<uint8_t*>(kpsf) + (uint32_t)me.oi * (uint32_t)sizeof(orbx_keypoint)) = kp;
   }
   }
 }
