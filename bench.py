@@ -88,6 +88,9 @@ def parse():
     ap.add_argument("--split", type=int, default=2,
                     help="pipelined step: extract the batch as this many sub-batches, each on its own "
                          "stream (same frames and work; the matcher waits for all of them)")
+    ap.add_argument("--match-whole", action="store_true",
+                    help="with --split: match the whole batch after every sub-batch is extracted "
+                         "(default: sub-batch j is matched as soon as it and its predecessor frame exist)")
     ap.add_argument("--traffic", default="", help="PMC traffic summary (default profiles/traffic_<workload>.json)")
     a = ap.parse_args()
     wl = dict(WORKLOADS[a.workload])
@@ -674,8 +677,7 @@ def main_mono(args, wl):
                     lo, hi = 1 + j * sub, 1 + (j + 1) * sub
                     subplans[j].extract(frames[j * sub:(j + 1) * sub], stream=sx[j],
                                         out=(k_i[lo:hi], d_i[lo:hi], c_i[lo:hi]))
-                    if j:
-                        ev_s[j].record(sx[j])
+                    ev_s[j].record(sx[j])
             with torch.cuda.stream(sa):
                 for j in range(1, S):
                     sa.wait_event(ev_s[j])
@@ -683,8 +685,21 @@ def main_mono(args, wl):
                     xch.ring_step(dist, rank, (k_i[B], d_i[B], c_i[B:B + 1]), (k_i[0], d_i[0], c_i[0:1]))
                 ev_x[i].record(sa)
             with torch.cuda.stream(sb):
-                sb.wait_event(ev_x[i])
-                mp.match(B, k_i[1:], d_i[1:], c_i[1:], k_i, d_i, c_i, args.nnratio, True, stream=sb)
+                if S == 1 or args.match_whole:
+                    sb.wait_event(ev_x[i])
+                    mp.match(B, k_i[1:], d_i[1:], c_i[1:], k_i, d_i, c_i, args.nnratio, True, stream=sb)
+                else:
+                    # sub-batch j's pairs (slot t vs t - 1, t in [lo, hi)) as soon as
+                    # sub-batch j and the frame before it exist: slot 0 comes from the
+                    # previous step (1 GPU) or the ring exchange (N GPUs)
+                    for j in range(S):
+                        lo, hi = 1 + j * sub, 1 + (j + 1) * sub
+                        sb.wait_event(ev_x[i] if (j == 0 and world > 1) else ev_s[j])
+                        if j:
+                            sb.wait_event(ev_s[j - 1])
+                        mp.match(sub, k_i[lo:hi], d_i[lo:hi], c_i[lo:hi], k_i[lo - 1:hi - 1],
+                                 d_i[lo - 1:hi - 1], c_i[lo - 1:hi - 1], args.nnratio, True, stream=sb,
+                                 out_offset=lo - 1)
                 ev_m[i].record(sb)
 
     for _ in range(args.warmup):
@@ -776,8 +791,10 @@ def main_mono(args, wl):
         out["step_mode"] = ("pipelined: step k+1's extraction overlaps step k's matching on a second, "
                             "high-priority stream (same work per step, matches equal the serial step's)")
         if len(subplans) > 1:
-            out["step_mode"] += ("; extraction as %d sub-batches of %d frames on %d streams"
-                                 % (len(subplans), B // len(subplans), len(subplans)))
+            out["step_mode"] += ("; extraction as %d sub-batches of %d frames on %d streams, %s"
+                                 % (len(subplans), B // len(subplans), len(subplans),
+                                    "the batch matched once all are extracted" if args.match_whole
+                                    else "each sub-batch matched as soon as it is extracted"))
         out["serial"] = {"value": round(world * B * args.steps / el_serial, 2),
                          "ms_per_step": round(el_serial / args.steps * 1e3, 3),
                          "note": "stage times and roofline entries come from this serial timed loop "

@@ -13,12 +13,12 @@
 #include "plan_internal.h"
 
 namespace orbx {
-__global__ void k_stereo_rows(const orbx_keypoint*, const int*, const StereoArgs, int*, uint16_t*,
+__global__ void k_stereo_rows(const orbx_keypoint*, const int*, const StereoArgs, int*, uint2*,
                               int*);
 __global__ void k_stereo_match(const orbx_keypoint*, const uint8_t*, const int*,
                                const orbx_keypoint*, const uint8_t*, const uint8_t*,
                                const uint8_t*, size_t, size_t, const uint8_t*, const uint8_t*,
-                               size_t, const StereoArgs, const int*, const uint16_t*, float*,
+                               size_t, const StereoArgs, const int*, const uint2*, float*,
                                float*, int*, int*);
 __global__ void k_stereo_filter(const int*, const StereoArgs, float*, float*, const int*, int*);
 }  // namespace orbx
@@ -32,7 +32,7 @@ struct orbs_plan {
   int W = 0, H = 0;
   StereoArgs args;
   int* d_rowoff = nullptr;
-  uint16_t* d_rows = nullptr;
+  uint2* d_rows = nullptr; /* CSR entries {iR | octave << 16, x} (kernels_stereo.hip) */
   int* d_sad = nullptr;
   int* d_err = nullptr;
   /* host drop-in (orbx_stereo_match) staging, batch 1 */
@@ -96,7 +96,7 @@ static int splan_create(const orbx_plan* g, int max_batch, orbs_plan** out) {
   const size_t B = (size_t)max_batch;
   const size_t K = (size_t)std::max(P.kcap, 1);
   if (hipMalloc((void**)&sp->d_rowoff, B * (A.nrows + 1) * sizeof(int)) != hipSuccess ||
-      hipMalloc((void**)&sp->d_rows, B * (size_t)std::max(A.rcap, 1) * sizeof(uint16_t)) != hipSuccess ||
+      hipMalloc((void**)&sp->d_rows, B * (size_t)std::max(A.rcap, 1) * sizeof(uint2)) != hipSuccess ||
       hipMalloc((void**)&sp->d_sad, B * K * sizeof(int)) != hipSuccess ||
       hipMalloc((void**)&sp->d_err, 16) != hipSuccess ||
       hipMemset(sp->d_err, 0, 16) != hipSuccess ||

@@ -71,15 +71,17 @@ __device__ __forceinline__ bool stereo_rows_of(const orbx_keypoint& k, const Ste
   return *minr >= 0 && *maxr < A.nrows;      // vRowIndices[yi] in range
 }
 
-// vRowIndices as CSR: rowoff[f][0..nrows], rows[f][...] = right keypoint
-// indices of each row.  The order inside a row does not matter: the search
-// takes the lexicographic minimum of (distance, iR), which is what the
-// reference's ascending-iR scan with a strict '<' selects.
+// vRowIndices as CSR: rowoff[f][0..nrows], rows[f][...] = the right
+// keypoints of each row as {iR | octave << 16, x} (the search's gates read
+// them from the entry: no dependent keypoint gather).  The order inside a row
+// does not matter: the search takes the lexicographic minimum of (distance,
+// iR), which is what the reference's ascending-iR scan with a strict '<'
+// selects.
 __global__ __launch_bounds__(SR_THREADS) void k_stereo_rows(const orbx_keypoint* __restrict__ kps_r,
                                                             const int* __restrict__ cnt_r,
                                                             const StereoArgs A,
                                                             int* __restrict__ rowoff,
-                                                            uint16_t* __restrict__ rows,
+                                                            uint2* __restrict__ rows,
                                                             int* __restrict__ err) {
   extern __shared__ int rc[];  // nrows
   __shared__ int wsum[SR_THREADS / 64 + 1];
@@ -108,11 +110,13 @@ __global__ __launch_bounds__(SR_THREADS) void k_stereo_rows(const orbx_keypoint*
     return;
   }
   __syncthreads();
-  uint16_t* R = rows + (size_t)f * A.rcap;
+  uint2* R = rows + (size_t)f * A.rcap;
   for (int iR = tid; iR < n; iR += SR_THREADS) {
+    const orbx_keypoint k = K[iR];
     int lo, hi;
-    if (!stereo_rows_of(K[iR], A, &lo, &hi)) continue;
-    for (int yi = lo; yi <= hi; ++yi) R[atomicAdd(&rc[yi], 1)] = (uint16_t)iR;
+    if (!stereo_rows_of(k, A, &lo, &hi)) continue;
+    const uint2 e = make_uint2((uint32_t)iR | ((uint32_t)k.octave << 16), __float_as_uint(k.x));
+    for (int yi = lo; yi <= hi; ++yi) R[atomicAdd(&rc[yi], 1)] = e;
   }
 }
 
@@ -139,7 +143,7 @@ __global__ __launch_bounds__(256) void k_stereo_match(
     const uint8_t* __restrict__ desc_r, const uint8_t* __restrict__ frames_l,
     const uint8_t* __restrict__ frames_r, size_t fstride, size_t rstride,
     const uint8_t* __restrict__ pyr_l, const uint8_t* __restrict__ pyr_r, size_t pstride,
-    const StereoArgs A, const int* __restrict__ rowoff, const uint16_t* __restrict__ rows,
+    const StereoArgs A, const int* __restrict__ rowoff, const uint2* __restrict__ rows,
     float* __restrict__ uright, float* __restrict__ depth, int* __restrict__ sad,
     int* __restrict__ err) {
   __shared__ int part[4][128];
@@ -147,16 +151,32 @@ __global__ __launch_bounds__(256) void k_stereo_match(
   const int f = blockIdx.y;
   const int nl = cnt_l[f];
   const orbx_keypoint* KL = kps_l + (size_t)f * A.kcap;
-  const orbx_keypoint* KR = kps_r + (size_t)f * A.kcap;
+  (void)kps_r;  // the right keypoints' gate fields come with the CSR entries
   const uint8_t* DL = desc_l + (size_t)f * A.kcap * 32;
   const uint8_t* DR = desc_r + (size_t)f * A.kcap * 32;
   const int* ro = rowoff + (size_t)f * (A.nrows + 1);
-  const uint16_t* R = rows + (size_t)f * A.rcap;
+  const uint2* R = rows + (size_t)f * A.rcap;
   const float minD = 0;                // :477
   const float maxD = A.mbf / A.mb;     // :476-478 (minZ = mb)
   const int thOrbDist = (100 + 50) / 2;  // :451 (TH_HIGH + TH_LOW) / 2
-  for (int iL = blockIdx.x * 4 + wave; iL < nl; iL += gridDim.x * 4) {
-    const orbx_keypoint kpL = KL[iL];
+  // the next left keypoint and its descriptor are loaded one keypoint ahead
+  const int stride = gridDim.x * 4;
+  int iL = blockIdx.x * 4 + wave;
+  orbx_keypoint kpN;
+  uint4 a0N, a1N;
+  if (iL < nl) {
+    kpN = KL[iL];
+    a0N = reinterpret_cast<const uint4*>(DL + (size_t)iL * 32)[0];
+    a1N = reinterpret_cast<const uint4*>(DL + (size_t)iL * 32)[1];
+  }
+  for (; iL < nl; iL += stride) {
+    const orbx_keypoint kpL = kpN;
+    const uint4 a0 = a0N, a1 = a1N;
+    if (iL + stride < nl) {  // wave-uniform
+      kpN = KL[iL + stride];
+      a0N = reinterpret_cast<const uint4*>(DL + (size_t)(iL + stride) * 32)[0];
+      a1N = reinterpret_cast<const uint4*>(DL + (size_t)(iL + stride) * 32)[1];
+    }
     float ur = -1.0f, dp = -1.0f;
     int sv = -1;
     bool bad = false;
@@ -169,28 +189,32 @@ __global__ __launch_bounds__(256) void k_stereo_match(
       const int cb = ro[row], ce = ro[row + 1];
       const float minU = uL - maxD, maxU = uL - minD;  // :497-498
       if (cb != ce && !(maxU < 0)) {
-        const uint4* dlp = reinterpret_cast<const uint4*>(DL + (size_t)iL * 32);
-        const uint4 a0 = dlp[0], a1 = dlp[1];
         uint32_t best = 0xFFFFFFFFu;
+        float ubest = 0.0f;  // x of this lane's best candidate
         for (int c = cb + lane; c < ce; c += 64) {  // :507-529
-          const int iR = R[c];
-          const orbx_keypoint& kpR = KR[iR];
-          const int oR = kpR.octave;
-          const float uR = kpR.x;
+          const uint2 e = R[c];
+          const int iR = (int)(e.x & 0xFFFFu), oR = (int)(e.x >> 16);
+          const float uR = __uint_as_float(e.y);
           if (oR >= levelL - 1 && oR <= levelL + 1 && uR >= minU && uR <= maxU) {
             const uint4* drp = reinterpret_cast<const uint4*>(DR + (size_t)iR * 32);
             const uint4 b0 = drp[0], b1 = drp[1];
             const int dist = __popc(a0.x ^ b0.x) + __popc(a0.y ^ b0.y) + __popc(a0.z ^ b0.z) +
                              __popc(a0.w ^ b0.w) + __popc(a1.x ^ b1.x) + __popc(a1.y ^ b1.y) +
                              __popc(a1.z ^ b1.z) + __popc(a1.w ^ b1.w);
-            if (dist < 100) best = min(best, ((uint32_t)dist << 16) | (uint32_t)iR);
+            const uint32_t key = ((uint32_t)dist << 16) | (uint32_t)iR;
+            if (dist < 100 && key < best) {
+              best = key;
+              ubest = uR;
+            }
           }
         }
+        const uint32_t mine = best;
         best = wave_min_u32(best);  // DPP, no LDS round trips
         const int bestDist = best == 0xFFFFFFFFu ? 100 : (int)(best >> 16);
         if (bestDist < thOrbDist) {  // :532
-          const int bestIdxR = (int)(best & 0xFFFFu);
-          const float uR0 = KR[bestIdxR].x;
+          // keys are unique (iR inside): the owner lane holds the winner's x
+          const int owner = __ffsll((unsigned long long)__ballot(mine == best)) - 1;
+          const float uR0 = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(ubest), owner));
           const float scaleFactor = A.inv_scale[levelL];
           const float scaleduL = roundf(kpL.x * scaleFactor);
           const float scaledvL = roundf(kpL.y * scaleFactor);
