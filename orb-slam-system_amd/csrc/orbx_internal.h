@@ -57,7 +57,7 @@ struct LevelInfo {
 #define ORBX_BLUR_TH 32
 #define ORBX_STRIP_MAXW 256 /* FAST strip: band width budget per workgroup */
 #ifndef ORBX_FS_COLWALK_MINW
-#define ORBX_FS_COLWALK_MINW 700 /* narrowest level whose strips take the column walk */
+#define ORBX_FS_COLWALK_MINW 400 /* narrowest level whose strips take the column walk */
 #endif
 
 struct CellInfo {
