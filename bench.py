@@ -85,9 +85,10 @@ def parse():
                     help="pyramid kernel (orbx_plan_set_options; identical results)")
     ap.add_argument("--serial", action="store_true",
                     help="time only the serial step (no extraction/matching overlap across steps)")
-    ap.add_argument("--split", type=int, default=2,
+    ap.add_argument("--split", type=int, default=None,
                     help="pipelined step: extract the batch as this many sub-batches, each on its own "
-                         "stream (same frames and work; the matcher waits for all of them)")
+                         "stream (same frames and work); default 2 for c1-c4 (measured +0.5-1.5 %%), "
+                         "1 for c5 (2 measured -12 %%)")
     ap.add_argument("--match-whole", action="store_true",
                     help="with --split: match the whole batch after every sub-batch is extracted "
                          "(default: sub-batch j is matched as soon as it and its predecessor frame exist)")
@@ -637,7 +638,7 @@ def main_mono(args, wl):
         # sx[j] (j = 0 is sa, which also does the slot-0 copy and the boundary
         # exchange), so one sub-batch's latency-bound kernels (quadtree, the
         # launch tails) overlap another's
-        S = args.split
+        S = 2 if args.split is None else args.split
         if S < 1:
             raise SystemExit("bench.py: --split must be >= 1")
         if B % S:
@@ -866,6 +867,26 @@ def main_c5(args, wl):
         ev_x = [torch.cuda.Event(), torch.cuda.Event()]
         ev_m = [torch.cuda.Event(), torch.cuda.Event()]
         it = [0]
+        # --split S (main_mono): sub-batch j's left + right extraction and its
+        # ComputeStereoMatches (own plans, own stereo plan) on stream sx[j];
+        # its SearchByBoW pairs start as soon as it and the frame before it exist
+        S = 1 if args.split is None else args.split
+        if S < 1:
+            raise SystemExit("bench.py: --split must be >= 1")
+        if B % S:
+            S = 1
+        sub = B // S
+        if S == 1:
+            subs = [(pl, pr, sp)]
+        else:
+            subs = []
+            for _ in range(S):
+                a_, b_ = orbx.Plan(prm, W, H, sub, device=local), orbx.Plan(prm, W, H, sub, device=local)
+                a_.set_options(pyramid=args.pyramid)
+                b_.set_options(pyramid=args.pyramid)
+                subs.append((a_, b_, orbx.StereoPlan(a_, device=local)))
+        sx = [sa] + [torch.cuda.Stream(device=dev) for _ in range(S - 1)]
+        ev_s = [torch.cuda.Event() for _ in range(S)]
 
         def pipe():
             if it[0] == 0:  # continue from the serial loop's state: buffer 0 = its last batch
@@ -883,15 +904,36 @@ def main_c5(args, wl):
                     k_i[0].copy_(k_j[B])
                     d_i[0].copy_(d_j[B])
                     c_i[0:1].copy_(c_j[B:B + 1])
-                pl.extract(fl, stream=sa, out=(k_i[1:], d_i[1:], c_i[1:]))
-                pr.extract(fr, stream=sa)
+            for j in range(1, S):
+                sx[j].wait_event(ev_m[i])
+            for j, (pl_j, pr_j, sp_j) in enumerate(subs):
+                lo, hi = 1 + j * sub, 1 + (j + 1) * sub
+                fl_j, fr_j = fl[j * sub:(j + 1) * sub], fr[j * sub:(j + 1) * sub]
+                with torch.cuda.stream(sx[j]):
+                    pl_j.extract(fl_j, stream=sx[j], out=(k_i[lo:hi], d_i[lo:hi], c_i[lo:hi]))
+                    pr_j.extract(fr_j, stream=sx[j])
+                    sp_j.match(pl_j, pr_j, fl_j, fr_j, mb, mbf, left_out=(k_i[lo:hi], d_i[lo:hi], c_i[lo:hi]),
+                               stream=sx[j])
+                    ev_s[j].record(sx[j])
+            with torch.cuda.stream(sa):
+                for j in range(1, S):
+                    sa.wait_event(ev_s[j])
                 if world > 1:
                     xch.ring_step(dist, rank, (k_i[B], d_i[B], c_i[B:B + 1]), (k_i[0], d_i[0], c_i[0:1]))
-                sp.match(pl, pr, fl, fr, mb, mbf, left_out=(k_i[1:], d_i[1:], c_i[1:]), stream=sa)
                 ev_x[i].record(sa)
             with torch.cuda.stream(sb):
-                sb.wait_event(ev_x[i])
-                mp.match(B, k_i[1:], d_i[1:], c_i[1:], k_i, d_i, c_i, args.nnratio, True, stream=sb)
+                if S == 1 or args.match_whole:
+                    sb.wait_event(ev_x[i])
+                    mp.match(B, k_i[1:], d_i[1:], c_i[1:], k_i, d_i, c_i, args.nnratio, True, stream=sb)
+                else:
+                    for j in range(S):
+                        lo, hi = 1 + j * sub, 1 + (j + 1) * sub
+                        sb.wait_event(ev_x[i] if (j == 0 and world > 1) else ev_s[j])
+                        if j:
+                            sb.wait_event(ev_s[j - 1])
+                        mp.match(sub, k_i[lo:hi], d_i[lo:hi], c_i[lo:hi], k_i[lo - 1:hi - 1],
+                                 d_i[lo - 1:hi - 1], c_i[lo - 1:hi - 1], args.nnratio, True, stream=sb,
+                                 out_offset=lo - 1)
                 ev_m[i].record(sb)
 
     for _ in range(args.warmup):
@@ -941,7 +983,8 @@ def main_c5(args, wl):
         if world > 1:
             dist.barrier()
         el = finish_time(torch, dist, world, dev, time.perf_counter() - t0)
-        sp.check()
+        for _, _, sp_j in subs:
+            sp_j.check()
         if not torch.equal(mp.match12[:B], ref12):
             raise SystemExit("bench.py: pipelined matches differ from the serial step")
     drec = dist_record(torch, dist, world, local)  # collective: every rank
@@ -983,6 +1026,11 @@ def main_c5(args, wl):
         out["step_mode"] = ("pipelined: step k+1's extraction + stereo matching overlap step k's "
                             "SearchByBoW on a second, high-priority stream (same work per step, "
                             "matches equal the serial step's)")
+        if len(subs) > 1:
+            out["step_mode"] += ("; extraction + stereo as %d sub-batches of %d pairs on %d streams, %s"
+                                 % (len(subs), sub, len(subs),
+                                    "the batch matched once all are extracted" if args.match_whole
+                                    else "each sub-batch matched as soon as it is extracted"))
         out["serial"] = {"value": round(world * B * args.steps / el_serial, 2),
                          "ms_per_step": round(el_serial / args.steps * 1e3, 3),
                          "note": "stage times and roofline entries come from this serial timed loop "
