@@ -632,8 +632,6 @@ def main_mono(args, wl):
     # resolver) fill the CUs the extraction leaves idle.  Same work per step.
     pipe = None
     if match and not args.serial:
-        sa = torch.cuda.Stream(device=dev)
-        sb = torch.cuda.Stream(device=dev, priority=-1)
         # --split S: S plans of B/S frames, sub-batch j extracted on stream
         # sx[j] (j = 0 is sa, which also does the slot-0 copy and the boundary
         # exchange), so one sub-batch's latency-bound kernels (quadtree, the
@@ -647,6 +645,12 @@ def main_mono(args, wl):
         subplans = [plan] if S == 1 else [orbx.Plan(prm, W, H, sub, device=local) for _ in range(S)]
         for p_ in subplans:
             p_.set_options(pyramid=args.pyramid)
+        # the pipeline's streams are created back to back, after every plan
+        # (each plan creates a stream of its own): HIP hands out its hardware
+        # queues (GPU_MAX_HW_QUEUES, 4 on the box) in creation order, and
+        # streams on one queue serialise
+        sa = torch.cuda.Stream(device=dev)
+        sb = torch.cuda.Stream(device=dev, priority=-1)
         sx = [sa] + [torch.cuda.Stream(device=dev) for _ in range(S - 1)]
         ev_s = [torch.cuda.Event() for _ in range(S)]
         bufs = [(kps, desc, counts),
@@ -860,8 +864,6 @@ def main_c5(args, wl):
     # on stream sb (reads only the double-buffered keypoints)
     pipe = None
     if not args.serial:
-        sa = torch.cuda.Stream(device=dev)
-        sb = torch.cuda.Stream(device=dev, priority=-1)
         bufs = [(kps, desc, counts),
                 (torch.zeros_like(kps), torch.zeros_like(desc), torch.zeros_like(counts))]
         ev_x = [torch.cuda.Event(), torch.cuda.Event()]
@@ -885,6 +887,8 @@ def main_c5(args, wl):
                 a_.set_options(pyramid=args.pyramid)
                 b_.set_options(pyramid=args.pyramid)
                 subs.append((a_, b_, orbx.StereoPlan(a_, device=local)))
+        sa = torch.cuda.Stream(device=dev)  # back to back, after every plan (main_mono)
+        sb = torch.cuda.Stream(device=dev, priority=-1)
         sx = [sa] + [torch.cuda.Stream(device=dev) for _ in range(S - 1)]
         ev_s = [torch.cuda.Event() for _ in range(S)]
 
