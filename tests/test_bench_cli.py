@@ -57,13 +57,15 @@ def test_bench_split_extraction_matches_serial():
     # --split 2: the pipelined step extracts the batch as two sub-batches on
     # two streams (two plans); bench.py aborts unless the matches equal the
     # serial loop's (one plan over the whole batch)
+    # (c5: left + right plans and a stereo plan per sub-batch)
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
-    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--workload", "c1", "--batch", "8",
-                        "--split", "2", "--steps", "3", "--warmup", "1", "--no-cpu-baseline", "--no-latency"],
-                       env=env, capture_output=True, text=True, timeout=300)
-    assert r.returncode == 0, r.stderr[-2000:]
-    d = json.loads(r.stdout.strip().splitlines()[-1])
-    assert d["value"] > 0 and "2 sub-batches" in d["step_mode"]
+    for wl in ("c1", "c5"):
+        r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--workload", wl, "--batch", "8",
+                            "--split", "2", "--steps", "3", "--warmup", "1", "--no-cpu-baseline", "--no-latency"],
+                           env=env, capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stderr[-2000:]
+        d = json.loads(r.stdout.strip().splitlines()[-1])
+        assert d["value"] > 0 and "2 sub-batches" in d["step_mode"]
 
 
 @pytest.mark.gpu
