@@ -37,6 +37,19 @@ __device__ __forceinline__ int hamming_u(const uint32_t d1[8], const uint32_t* b
          __popc(d1[6] ^ b1.z) + __popc(d1[7] ^ b1.w);
 }
 
+// a generic pointer known to point into global memory: loads through it are
+// global_load, which the wait counters order with the other vector memory
+// ops (a flat_load may return out of order, so a flat load pending on any
+// path makes the compiler wait for everything: vmcnt(0))
+typedef const uint32_t __attribute__((address_space(1)))* gu32_t;
+typedef const uint8_t __attribute__((address_space(1)))* gu8_t;
+__device__ __forceinline__ int hamming_g(const uint32_t d1[8], gu32_t b) {
+  int d = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) d += __popc(d1[k] ^ b[k]);  // two dwordx4 loads (32-B aligned rows)
+  return d;
+}
+
 // 256-bit Hamming distance as one accumulate chain: v_bcnt_u32_b32 adds its
 // second operand, so 8 xor + 8 bcnt (the compiler's add3 trees cost 3 more)
 __device__ __forceinline__ uint32_t bcnt_acc(uint32_t x, uint32_t acc) {
@@ -953,7 +966,7 @@ __global__ __launch_bounds__(64) void k_match_resolve_spec(
   if (unit >= nunits) return;
   const MNodePair NP = nps[unit];
   const MProblem P = probs[NP.prob];
-  const uint32_t* f2 = P.feat2 + NP.off2;
+  const gu32_t gf2 = (gu32_t)(P.feat2 + NP.off2);
   for (int w = lane; w < ((P.n2 + 31) >> 5); w += 64) bm[w] = 0u;
   for (int w = lane; w < P.n2; w += 64) claim[w] = 64;
   __builtin_amdgcn_wave_barrier();
@@ -975,14 +988,25 @@ __global__ __launch_bounds__(64) void k_match_resolve_spec(
 #endif
   auto chunk = [&](int4& inf_n, uint4 (&cv_n)[ORBM_T / 2], int base) {
     const int r = NP.row_base + base + lane;
+    // nothing of the row info stays live across the refill below, so the
+    // refill reuses the buffer's registers (with a buffer live across the
+    // fetch, the refill took other registers and the loop latch copied them
+    // back, waiting on every load in flight): the rounds need only the
+    // wave-uniform "list longer than the candidates" mask, and the rare
+    // rescan re-reads its row's idx1
     const int4 inf = inf_n;
     const bool feas = base + lane < NP.n1 && inf.x != 0 && inf.z < ORBM_TH_LOW;
+    const uint64_t longl = __ballot(inf.y > ORBM_T);
     uint2 c[ORBM_T];
 #pragma unroll
     for (int t = 0; t < ORBM_T / 2; ++t) {
       c[2 * t] = feas ? make_uint2(cv_n[t].x, cv_n[t].y) : make_uint2(0xFFFFFFFFu, 0u);
       c[2 * t + 1] = feas ? make_uint2(cv_n[t].z, cv_n[t].w) : make_uint2(0xFFFFFFFFu, 0u);
     }
+    // the selects happen here, not sunk past the refill (which would keep
+    // cv_n live across it)
+#pragma unroll
+    for (int t = 0; t < ORBM_T; ++t) asm volatile("" : "+v"(c[t].x), "+v"(c[t].y));
     // the buffer is consumed before it is refilled, so the refill can take the
     // same registers (otherwise the loop latch copies it, waiting on vmcnt)
     __builtin_amdgcn_sched_barrier(0);
@@ -1013,7 +1037,7 @@ __global__ __launch_bounds__(64) void k_match_resolve_spec(
           ++nun;
         }
       }
-      const bool hard = mine && nun < 2 && inf.y > ORBM_T;  // list exhausted: needs a rescan
+      const bool hard = mine && nun < 2 && ((longl >> lane) & 1ull);  // list exhausted: needs a rescan
       const bool acc = mine && !hard && k1 < ORBM_TH_LOW && (float)k1 < P.nnratio * (float)k2;
       if (acc) atomicMin(&claim[id1], lane);
       __builtin_amdgcn_wave_barrier();
@@ -1040,18 +1064,18 @@ __global__ __launch_bounds__(64) void k_match_resolve_spec(
 #ifdef RS_STATS
         st_hard++;
 #endif
-        const int idx1 = lane_value(inf.w, bnd);
-        const uint32_t* q1 = reinterpret_cast<const uint32_t*>(P.desc1 + (size_t)idx1 * 32);
+        const int idx1 = rowinfo[NP.row_base + base + bnd].w;
+        const gu32_t q1 = (gu32_t)(P.desc1 + (size_t)idx1 * 32);
         uint32_t d1[8];
 #pragma unroll
         for (int k = 0; k < 8; ++k) d1[k] = q1[k];
         uint32_t kb = 0xFFFFFFFFu;
         int d2 = INT_MAX;
         for (int jj = lane; jj < NP.n2; jj += 64) {
-          const int i2 = (int)f2[jj];
-          if (P.valid2 && !P.valid2[i2]) continue;
+          const int i2 = (int)gf2[jj];
+          if (P.valid2 && !((gu8_t)P.valid2)[i2]) continue;
           if ((bm[i2 >> 5] >> (i2 & 31)) & 1u) continue;
-          const int d = hamming_u(d1, reinterpret_cast<const uint32_t*>(P.desc2 + (size_t)i2 * 32));
+          const int d = hamming_g(d1, (gu32_t)(P.desc2 + (size_t)i2 * 32));
           best_merge(kb, d2, ((uint32_t)d << 16) | (uint32_t)jj, INT_MAX);
         }
 #pragma unroll
@@ -1061,7 +1085,7 @@ __global__ __launch_bounds__(64) void k_match_resolve_spec(
           best_merge(kb, d2, ok, od);
         }
         if (kb != 0xFFFFFFFFu) {
-          const int b1 = (int)(kb >> 16), bi = (int)f2[kb & 0xFFFFu];
+          const int b1 = (int)(kb >> 16), bi = (int)gf2[kb & 0xFFFFu];
           if (b1 < ORBM_TH_LOW && (float)b1 < P.nnratio * (float)d2 && lane == bnd) {
             atomicOr(&bm[bi >> 5], 1u << (bi & 31));
             ev[r] = make_int2(bi, 0);
@@ -1077,10 +1101,20 @@ __global__ __launch_bounds__(64) void k_match_resolve_spec(
   if (NP.n1 <= 0) return;
 #pragma unroll
   for (int b = 0; b < RS_NB; ++b) fetch(inf[b], cv[b], 64 * b);
-  for (int base = 0; base < NP.n1; base += 64 * RS_NB) {
+  // every buffer is refilled exactly once per iteration and the loop leaves
+  // through the breaks, so no buffer is a merge of old and refilled values
+  // at the latch (a merge there made the allocator copy the buffers back,
+  // waiting on every load in flight)
+  for (int base = 0;; base += 64 * RS_NB) {
+    bool done = false;
 #pragma unroll
-    for (int b = 0; b < RS_NB; ++b)
-      if (base + 64 * b < NP.n1) chunk(inf[b], cv[b], base + 64 * b);
+    for (int b = 0; b < RS_NB; ++b) {
+      if (!done) {
+        chunk(inf[b], cv[b], base + 64 * b);
+        done = base + 64 * (b + 1) >= NP.n1;
+      }
+    }
+    if (done) break;
   }
 #ifdef RS_STATS
   if (lane == 0 && unit < 4)
