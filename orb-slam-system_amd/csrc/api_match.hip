@@ -132,8 +132,9 @@ void launch_match(const MProblem* d_probs, int nprob, const MNodePair* d_nps, in
   const int units = sequential ? nprob : nnp;
   if (nrows > 0 && units > 0 && !sequential && max_bitmap_n2 <= 16384) {
     // speculative 64-row chunks; LDS = vbMatched2 bitmap + claim table
+    // (+ alignment to 8 B) + the chunk's candidate slots (64 lanes x ORBM_T)
     const int n2cap = std::max(max_bitmap_n2, 32);
-    const size_t lds = (size_t)((n2cap + 31) / 32) * 4 + (size_t)n2cap * 4;
+    const size_t lds = (size_t)((((n2cap + 31) / 32 + n2cap) + 1) & ~1) * 4 + (size_t)64 * ORBM_T * sizeof(uint2);
     hipLaunchKernelGGL(k_match_resolve_spec, dim3(units), dim3(64), lds, s, d_probs, d_nps, units,
                        d_cand, d_rowinfo, d_ev, n2cap);
   } else if (nrows > 0 && units > 0) {

@@ -961,6 +961,7 @@ __global__ __launch_bounds__(64) void k_match_resolve_spec(
   extern __shared__ uint32_t sm[];
   uint32_t* bm = sm;                                   // (n2cap + 31) / 32 words
   int* claim = reinterpret_cast<int*>(sm + ((n2cap + 31) >> 5));  // n2cap
+  uint2* cs = reinterpret_cast<uint2*>(sm + ((((n2cap + 31) >> 5) + n2cap + 1) & ~1));  // 64 * ORBM_T
   const int lane = threadIdx.x;
   const int unit = blockIdx.x;
   if (unit >= nunits) return;
@@ -1016,39 +1017,51 @@ __global__ __launch_bounds__(64) void k_match_resolve_spec(
 #ifdef RS_STATS
     st_feas += __popcll(pend); st_chunks++;
 #endif
+    // per chunk: the lane's valid-slot mask, and its candidate list in LDS
+    // (slot t of lane l at cs[64 t + l]) for the rounds' indexed reads
+    uint32_t V = 0;
+#pragma unroll
+    for (int t = 0; t < ORBM_T; ++t) {
+      V |= (c[t].x != 0xFFFFFFFFu ? 1u : 0u) << t;
+      cs[64 * t + lane] = c[t];
+    }
     while (pend) {
 #ifdef RS_STATS
       st_rounds++;
 #endif
       const bool mine = (pend >> lane) & 1ull;
-      // all bitmap words first (independent LDS reads, one wait), then the
-      // in-order scan in registers; empty slots read word 0 harmlessly
+      // all bitmap words first (independent LDS reads, one wait); empty
+      // slots read word 0 harmlessly.  The in-order scan for the first two
+      // unmatched candidates is a bit mask: U = valid & ~matched, first =
+      // lowest set bit, second = next one; their keys come from the lane's
+      // LDS slots (one read each) -- branch-free, where a per-slot scan
+      // chained 8 conditional steps through exec masks
       uint32_t bw[ORBM_T];
 #pragma unroll
       for (int t = 0; t < ORBM_T; ++t) bw[t] = bm[c[t].y >> 5];
-      int k1 = INT_MAX, k2 = INT_MAX, id1 = -1, nun = 0, plen = ORBM_T;
+      uint32_t B = 0;
 #pragma unroll
-      for (int t = 0; t < ORBM_T; ++t) {
-        const int i2 = (int)c[t].y;
-        const bool un = c[t].x != 0xFFFFFFFFu && !((bw[t] >> (i2 & 31)) & 1u);
-        if (un && nun < 2) {
-          if (nun == 0) { k1 = (int)(c[t].x >> 16); id1 = i2; }
-          else { k2 = (int)(c[t].x >> 16); plen = t + 1; }
-          ++nun;
-        }
-      }
-      const bool hard = mine && nun < 2 && ((longl >> lane) & 1ull);  // list exhausted: needs a rescan
+      for (int t = 0; t < ORBM_T; ++t) B |= ((bw[t] >> (c[t].y & 31u)) & 1u) << t;
+      const uint32_t U = V & ~B, U2 = U & (U - 1u);
+      const int fi = __ffs(U) - 1, si = __ffs(U2) - 1;  // -1: none
+      const uint2 e1 = cs[64 * max(fi, 0) + lane];
+      const uint32_t e2 = cs[64 * max(si, 0) + lane].x;
+      const int k1 = U ? (int)(e1.x >> 16) : INT_MAX;
+      const int id1 = (int)e1.y;  // used only when accepted (U != 0)
+      const int k2 = U2 ? (int)(e2 >> 16) : INT_MAX;
+      const int plen = U2 ? si + 1 : ORBM_T;  // slots the serial walk examined
+      const bool hard = mine && U2 == 0u && ((longl >> lane) & 1ull);  // list exhausted: needs a rescan
       const bool acc = mine && !hard && k1 < ORBM_TH_LOW && (float)k1 < P.nnratio * (float)k2;
       if (acc) atomicMin(&claim[id1], lane);
       __builtin_amdgcn_wave_barrier();
       int cl[ORBM_T];
 #pragma unroll
       for (int t = 0; t < ORBM_T; ++t) cl[t] = claim[c[t].y];
-      bool conf = false;
+      // slots claimed by an earlier lane (cl - lane < 0 for cl, lane in [0, 64])
+      uint32_t CL = 0;
 #pragma unroll
-      for (int t = 0; t < ORBM_T; ++t)
-        conf |= t < plen && c[t].x != 0xFFFFFFFFu && cl[t] < lane;
-      conf = conf && mine;
+      for (int t = 0; t < ORBM_T; ++t) CL |= ((uint32_t)(cl[t] - lane) >> 31) << t;
+      const bool conf = mine && (CL & V & ((1u << plen) - 1u)) != 0u;
       const uint64_t cm = __ballot(conf || hard);
       const int bnd = cm ? (__ffsll((unsigned long long)cm) - 1) : 64;
       __builtin_amdgcn_wave_barrier();
