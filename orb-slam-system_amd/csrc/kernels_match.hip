@@ -1152,29 +1152,58 @@ __global__ __launch_bounds__(256) void k_match_finalize(const MProblem* __restri
   const MProblem P = probs[p];
   const float factor = 1.0f / ORBM_HISTO;
   int* last = last_scratch + scratch_off[p];
+  // global views of the problem's arrays (generic pointers read from
+  // MProblem would compile to flat_load / flat_store)
+  typedef int __attribute__((address_space(1)))* gi32_t;
+  typedef const float __attribute__((address_space(1)))* gf32_t;
+  const gi32_t m12 = (gi32_t)P.match12;
   for (int i = tid; i < P.n1; i += 256) {
-    P.match12[i] = -1;
+    m12[i] = -1;
     last[i] = -1;
   }
   if (tid < ORBM_HISTO) hist[tid] = 0;
   if (tid == 0) { s_nev = 0; s_nfilt = 0; }
   __syncthreads();
+  // the problem's rows are one contiguous range: node pairs are laid out in
+  // order from np_begin (api_match.hip: the merge-join assigns row_base
+  // sequentially; a batched plan has one node pair per problem).  Each
+  // thread walks its rows FZ_U at a time: every load of a batch is issued
+  // before the first use (clamped rows, masked below), instead of three
+  // dependent round trips per row
+  const int rb = P.np_end > P.np_begin ? nps[P.np_begin].row_base : 0;
+  const int re = P.np_end > P.np_begin ? nps[P.np_end - 1].row_base + nps[P.np_end - 1].n1 : 0;
+  constexpr int FZ_U = 8;
   int nev = 0;
-  for (int j = P.np_begin; j < P.np_end; ++j) {
-    const MNodePair NP = nps[j];
-    for (int r = NP.row_base + tid; r < NP.row_base + NP.n1; r += 256) {
-      const int2 e = ev[r];
-      if (e.x < 0) continue;
-      const int idx1 = rowinfo[r].w;
+  for (int r0 = rb + tid; r0 < re; r0 += 256 * FZ_U) {
+    int2 e[FZ_U];
+    int i1[FZ_U];
+#pragma unroll
+    for (int u = 0; u < FZ_U; ++u) {
+      const int r = min(r0 + 256 * u, re - 1);
+      e[u] = ev[r];
+      i1[u] = rowinfo[r].w;
+    }
+    float rot[FZ_U];
+    if (P.check_ori) {
+#pragma unroll
+      for (int u = 0; u < FZ_U; ++u)
+        rot[u] = e[u].x >= 0 ? ((gf32_t)P.ang1)[(size_t)i1[u] * P.ang_stride] -
+                                   ((gf32_t)P.ang2)[(size_t)e[u].x * P.ang_stride]
+                             : 0.0f;
+    }
+#pragma unroll
+    for (int u = 0; u < FZ_U; ++u) {
+      const int r = r0 + 256 * u;
+      if (r >= re || e[u].x < 0) continue;
       int bin = 0;  // rotation histogram bin (ORBmatcher.cc:332-340)
       if (P.check_ori) {
-        float rot = P.ang1[(size_t)idx1 * P.ang_stride] - P.ang2[(size_t)e.x * P.ang_stride];
-        if (rot < 0.0f) rot += 360.0f;
-        bin = (int)roundf(rot * factor);
+        float ro = rot[u];
+        if (ro < 0.0f) ro += 360.0f;
+        bin = (int)roundf(ro * factor);
         if (bin == ORBM_HISTO) bin = 0;
         ev[r].y = bin;  // read back by this thread below
       }
-      atomicMax(&last[idx1], r);
+      atomicMax(&last[i1[u]], r);
       atomicAdd(&hist[bin], 1);
       ++nev;
     }
@@ -1199,25 +1228,42 @@ __global__ __launch_bounds__(256) void k_match_finalize(const MProblem* __restri
     ind[0] = ti[0]; ind[1] = ti[1]; ind[2] = ti[2];
   }
   __syncthreads();
-  for (int j = P.np_begin; j < P.np_end; ++j) {
-    const MNodePair NP = nps[j];
-    for (int r = NP.row_base + tid; r < NP.row_base + NP.n1; r += 256) {
-      const int2 e = ev[r];
-      if (e.x < 0) continue;
-      const int idx1 = rowinfo[r].w;
-      if (last[idx1] == r) P.match12[idx1] = e.x;
+  for (int r0 = rb + tid; r0 < re; r0 += 256 * FZ_U) {
+    int2 e[FZ_U];
+    int i1[FZ_U], l[FZ_U];
+#pragma unroll
+    for (int u = 0; u < FZ_U; ++u) {
+      const int r = min(r0 + 256 * u, re - 1);
+      e[u] = ev[r];
+      i1[u] = rowinfo[r].w;
+    }
+#pragma unroll
+    for (int u = 0; u < FZ_U; ++u) l[u] = last[i1[u]];
+#pragma unroll
+    for (int u = 0; u < FZ_U; ++u) {
+      const int r = r0 + 256 * u;
+      if (r < re && e[u].x >= 0 && l[u] == r) m12[i1[u]] = e[u].x;
     }
   }
   __syncthreads();
   int nf = 0;
   if (P.check_ori) {
-    for (int j = P.np_begin; j < P.np_end; ++j) {
-      const MNodePair NP = nps[j];
-      for (int r = NP.row_base + tid; r < NP.row_base + NP.n1; r += 256) {
-        const int2 e = ev[r];
-        if (e.x < 0) continue;
-        if (e.y == ind[0] || e.y == ind[1] || e.y == ind[2]) continue;
-        P.match12[rowinfo[r].w] = -2;  // set to nullptr by the rotation check (:359)
+    const int b0 = ind[0], b1 = ind[1], b2 = ind[2];
+    for (int r0 = rb + tid; r0 < re; r0 += 256 * FZ_U) {
+      int2 e[FZ_U];
+      int i1[FZ_U];
+#pragma unroll
+      for (int u = 0; u < FZ_U; ++u) {
+        const int r = min(r0 + 256 * u, re - 1);
+        e[u] = ev[r];
+        i1[u] = rowinfo[r].w;
+      }
+#pragma unroll
+      for (int u = 0; u < FZ_U; ++u) {
+        const int r = r0 + 256 * u;
+        if (r >= re || e[u].x < 0) continue;
+        if (e[u].y == b0 || e[u].y == b1 || e[u].y == b2) continue;
+        m12[i1[u]] = -2;  // set to nullptr by the rotation check (:359)
         ++nf;
       }
     }
