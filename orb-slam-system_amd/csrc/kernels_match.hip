@@ -1292,17 +1292,35 @@ __global__ __launch_bounds__(256) void k_match_select(
   __syncthreads();
   for (int i = tid; i < K; i += 256) atomicAdd(&hist[(int)kp[i].response & 255], 1);
   __syncthreads();
-  if (tid == 0) {
+  if (tid < 64) {
+    // the response cutoff R: the first bin, from 255 down, where the count
+    // of keypoints at or above it reaches topn (above = count strictly
+    // above).  Wave 0, 4 bins per lane in descending order, a lane scan,
+    // then the crossing lane walks its 4 bins (a single-thread walk over
+    // 256 bins was a chain of up to 256 LDS reads)
+    const int lane = tid;
     int R = -1, above = 0;
     if (K > topn) {
-      int cum = 0;
-      for (int v = 255; v >= 0; --v) {
-        if (cum + hist[v] >= topn) { R = v; above = cum; break; }
-        cum += hist[v];
+      int h[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) h[j] = hist[255 - 4 * lane - j];
+      const int sum = h[0] + h[1] + h[2] + h[3];
+      const int incl = wave_incl_scan(sum);
+      // exists: the bins hold all K > topn keypoints
+      const int L = __ffsll((unsigned long long)__ballot(incl >= topn)) - 1;
+      int cum = incl - sum;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if (R < 0 && cum + h[j] >= topn) { R = 255 - 4 * lane - j; above = cum; }
+        cum += h[j];
       }
+      R = lane_value(R, L);
+      above = lane_value(above, L);
     }
-    s_R = R;
-    s_above = above;
+    if (lane == 0) {
+      s_R = R;
+      s_above = above;
+    }
   }
   __syncthreads();
   const int R = s_R, needEq = topn - s_above;
