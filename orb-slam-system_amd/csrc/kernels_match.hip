@@ -1212,8 +1212,12 @@ __global__ __launch_bounds__(256) void k_match_finalize(const MProblem* __restri
   __syncthreads();
   if (tid == 0) {  // ComputeThreeMaxima (ORBmatcher.cc:469-502)
     int ti[3] = {-1, -1, -1}, tv[3] = {0, 0, 0};
+    int hv[ORBM_HISTO];  // every bin read up front (independent LDS reads)
+#pragma unroll
+    for (int i = 0; i < ORBM_HISTO; ++i) hv[i] = hist[i];
+#pragma unroll
     for (int i = 0; i < ORBM_HISTO; ++i) {
-      const int v = hist[i];
+      const int v = hv[i];
       for (int jj = 0; jj < 3; ++jj) {
         if (v > tv[jj]) {
           for (int k = 2; k > jj; --k) { tv[k] = tv[k - 1]; ti[k] = ti[k - 1]; }
@@ -1289,8 +1293,20 @@ __global__ __launch_bounds__(256) void k_match_select(
   const int K = side ? count_b[p] : count_a[p];
   uint32_t* out = sel + ((size_t)p * 2 + side) * topn;
   hist[tid] = 0;
+  // the first SEL_U blocks of 256 responses stay in registers for the
+  // selection pass below (all loads issued at once; no reload per block)
+  constexpr int SEL_U = 8;
+  int rr[SEL_U];
+#pragma unroll
+  for (int u = 0; u < SEL_U; ++u) {
+    const int i = tid + 256 * u;
+    rr[u] = i < K ? (int)kp[i].response : -2;
+  }
   __syncthreads();
-  for (int i = tid; i < K; i += 256) atomicAdd(&hist[(int)kp[i].response & 255], 1);
+#pragma unroll
+  for (int u = 0; u < SEL_U; ++u)
+    if (tid + 256 * u < K) atomicAdd(&hist[rr[u] & 255], 1);
+  for (int i = tid + 256 * SEL_U; i < K; i += 256) atomicAdd(&hist[(int)kp[i].response & 255], 1);
   __syncthreads();
   if (tid < 64) {
     // the response cutoff R: the first bin, from 255 down, where the count
@@ -1326,10 +1342,8 @@ __global__ __launch_bounds__(256) void k_match_select(
   const int R = s_R, needEq = topn - s_above;
   const int wave = tid >> 6, lane = tid & 63;
   int nsel = 0, neq = 0;
-  for (int base = 0; base < K; base += 256) {
+  auto block = [&](int base, int resp) {
     const int i = base + tid;
-    int resp = -2;
-    if (i < K) resp = (int)kp[i].response;
     const bool eq = (i < K) && resp == R;
     // rank among equal-response entries (ordered)
     const uint64_t meq = __ballot(eq);
@@ -1350,7 +1364,11 @@ __global__ __launch_bounds__(256) void k_match_select(
     nsel += wtot[0] + wtot[1] + wtot[2] + wtot[3];
     neq += eqtot;
     __syncthreads();
-  }
+  };
+#pragma unroll
+  for (int u = 0; u < SEL_U; ++u)
+    if (256 * u < K) block(256 * u, rr[u]);
+  for (int base = 256 * SEL_U; base < K; base += 256) block(base, base + tid < K ? (int)kp[base + tid].response : -2);
   if (tid == 0) {
     if (side == 0) { nps[p].n1 = nsel; probs[p].n1 = K; }
     else { nps[p].n2 = nsel; probs[p].n2 = K; }
