@@ -361,3 +361,23 @@ def test_search_by_bow_chunk_edges(gpu, oracle, n1, n2):
     m, nm = gpu.search_by_bow(kf1, kf2, 0.75, True)
     rm, rnm = oracle.search_by_bow(kf1, kf2, 0.75, True)
     assert nm == rnm and np.array_equal(m, rm)
+
+
+@pytest.mark.parametrize("n2", [16384, 16385])
+def test_search_by_bow_large_kf2(gpu, oracle, n2):
+    """KF2 at the speculative resolver's bound (16384 features: its bitmap,
+    claim table and per-lane candidate slots take their largest LDS layout)
+    and one past it (the bitmap-only resolver)."""
+    rng = np.random.default_rng(n2)
+    n1 = 400
+    d2 = rng.integers(0, 256, (n2, 32), dtype=np.uint8)
+    d1 = _correlated(rng, d2[rng.integers(0, n2, n1)], rng.integers(0, 40, n1))
+    one = lambda d: dict(desc=d, angle=rng.uniform(0, 360, len(d)).astype(np.float32), valid=None,
+                         node_id=np.array([9], np.uint32), off=np.array([0, len(d)], np.uint32),
+                         feat=np.arange(len(d), dtype=np.uint32))
+    kf1, kf2 = one(d1), one(d2)
+    for ratio in (0.75, 1.0):
+        m, nm = gpu.search_by_bow(kf1, kf2, ratio, True)
+        rm, rnm = oracle.search_by_bow(kf1, kf2, ratio, True)
+        assert nm == rnm and np.array_equal(m, rm), ratio
+        assert nm > 100  # the resolver commits at real density
