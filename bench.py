@@ -81,7 +81,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=40.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-latency", action="store_true")
-    ap.add_argument("--pyramid", choices=["auto", "tiles", "stream", "fused"], default="auto",
+    ap.add_argument("--pyramid", choices=["auto", "tiles"], default="auto",
                     help="pyramid kernel (orbx_plan_set_options; identical results)")
     ap.add_argument("--serial", action="store_true",
                     help="time only the serial step (no extraction/matching overlap across steps)")
@@ -193,9 +193,6 @@ def load_traffic(path):
 
 def roofline_entries(st, steps, by, geo, B, traffic):
     per_step = {k: st[k][0] / steps for k in st if st[k][1]}
-    if "resize" not in per_step and "fast_cells" in per_step and by.get("resize"):
-        # fused pyramid + FAST (k_pyrfast): one launch moves both stages' bytes
-        by = dict(by, fast_cells=by["fast_cells"] + by["resize"], resize=0)
     dom = max((k for k in per_step if k in by), key=per_step.get)
     launches = st[dom][1] / steps
     ach = by[dom] / (per_step[dom] * 1e-3) / 1e9

@@ -180,30 +180,23 @@ int orbx_plan_check(orbx_plan* plan, void* stream);
  * capacity so the scan runs on ordinary frames. */
 int orbx_plan_debug_counters(orbx_plan* plan, int* fast_overflow_strips);
 
-/* Kernel-path options of a plan (default 0 = automatic; persistent).  Every
- * path gives bit-identical results; they differ in speed only.
+/* Kernel-path options of a plan (default 0 = automatic; persistent).
  *   ORBX_PLAN_PYR_TILES   the pyramid by k_pyramid (2-D tiles of the level
- *                         chain, halo recompute) for every batch size;
- *   ORBX_PLAN_PYR_STREAM  the row-streaming pyramid (k_pyr_stream, one
- *                         workgroup per frame) for every batch size;
- *   ORBX_PLAN_FUSED       pyramid and cell FAST in one kernel (k_pyrfast:
- *                         one workgroup per frame streams every level once
- *                         through LDS, FAST on the rows as they pass).
- * Automatic (0): k_pyramid then k_fast_strips, the fastest measured (the
- * streaming kernels take 1.2-2x / 2.6x its time at the bench workloads,
- * DESIGN.md §4 round 4).  Returns ORBX_ERR_ARG for unknown flags or both at once,
- * ORBX_ERR_UNSUPPORTED for ORBX_PLAN_PYR_STREAM / ORBX_PLAN_FUSED on a plan
- * the streaming schedule does not cover (the options are then unchanged). */
+ *                         chain, halo recompute) for every batch size.
+ * Automatic (0) is the same path today.  The round-4 row-streaming pyramid
+ * and fused pyramid + FAST kernels (flags 2 and 4) measured 1.1x / 2.6x the
+ * tile path's time and were retired; their flags, like
+ * any other unknown bit, now return ORBX_ERR_ARG (options unchanged). */
 #define ORBX_PLAN_PYR_TILES 1
-#define ORBX_PLAN_PYR_STREAM 2
-#define ORBX_PLAN_FUSED 4
 int orbx_plan_set_options(orbx_plan* plan, int flags);
 
 /* mvImagePyramid[level] of frame `frame` of the last orbx_plan_extract on
  * this plan, copied to host rows of dst_stride bytes (synchronises `stream`,
  * which must be the stream of that extraction or ordered after it; NULL =
  * the default stream).  Level 0 (and levels aliasing it) are the caller's
- * frame and are not held by the plan: ORBX_ERR_ARG. */
+ * frame and are not held by the plan: ORBX_ERR_ARG.  With dst != NULL,
+ * `frame` must be below the frame count of the plan's last orbx_plan_extract
+ * (ORBX_ERR_ARG before any extraction); dst == NULL only reports the size. */
 int orbx_plan_level(orbx_plan* plan, int frame, int level, uint8_t* dst, size_t dst_stride,
                     int* width, int* height, void* stream);
 

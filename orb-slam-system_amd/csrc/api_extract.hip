@@ -26,23 +26,13 @@ __global__ void k_fast_strips_p288(const uint8_t*, size_t, size_t, const uint8_t
                               size_t, uint32_t*, int, int, int, int, int, int, int, int*, int, int);
 __global__ void k_quadtree(const LevelInfo*, const CellInfo*, const uint32_t*, size_t,
                            const uint32_t*, int, uint32_t*, int32_t*, size_t, uint32_t*, size_t,
-                           int*, int, int, int, int*, uint32_t*, const uint32_t*);
+                           int*, int, int, int, int*, uint32_t*);
 __global__ void k_quadtree_j6(const LevelInfo*, const CellInfo*, const uint32_t*, size_t,
                               const uint32_t*, int, uint32_t*, int32_t*, size_t, uint32_t*, size_t,
-                              int*, int, int, int, int*, uint32_t*, const uint32_t*);
-__global__ void k_pyrfast(const uint8_t*, size_t, size_t, uint8_t*, size_t, const PyrFast, const uint2*,
-                          const int*, const uint4*, const uint2*, const CellInfo*, uint32_t*, uint32_t*,
-                          size_t, uint32_t*, int, int);
+                              int*, int, int, int, int*, uint32_t*);
 __global__ void k_orient_brief(const uint8_t*, size_t, size_t, const uint8_t*, size_t,
                                const BriefArgs, const uint32_t*, size_t, const int*,
                                orbx_keypoint*, uint8_t*, int*, const uint32_t*, int);
-#define PS_DECL(name)                                                                                 \
-  __global__ void name(const uint8_t*, size_t, size_t, uint8_t*, size_t, const PyrStream, const uint2*, \
-                       const int*, const uint4*, const uint2*, int)
-PS_DECL(k_pyr_stream_1024);
-PS_DECL(k_pyr_stream_512);
-PS_DECL(k_pyr_stream_256);
-#undef PS_DECL
 __global__ void k_synth(uint8_t*, int, int, size_t, int, int);
 __global__ void k_selftest_sincos(const float*, int, float*);
 __global__ void k_selftest_sincos_range(uint32_t, int, float*);
@@ -140,9 +130,7 @@ static void plan_free(orbx_plan* p) {
   hipSetDevice(p->device);
   void* bufs[] = {p->d_lv, p->d_cells, p->d_strips, p->d_xofs, p->d_xofs1, p->d_yofs, p->d_alpha, p->d_beta,
                   p->d_pyr, p->d_blur, p->d_slots, p->d_ccount, p->d_qkeys, p->d_qout, p->d_qperm,
-                  p->d_qnode, p->d_lcount, p->d_err, p->d_pyr_xs, p->d_pyr_ys, p->d_pyr_bo, p->d_pyr_blob,
-                  p->d_ps_tasks, p->d_ps_xlut, p->d_ps_ylut, p->d_ps_tick_end, p->d_pf_tasks,
-                  p->d_pf_xlut, p->d_pf_ylut, p->d_slots_hi, p->d_pf_tick_end};
+                  p->d_qnode, p->d_lcount, p->d_err, p->d_pyr_xs, p->d_pyr_ys, p->d_pyr_bo, p->d_pyr_blob};
   for (void* b : bufs)
     if (b) hipFree(b);
   p->timer.release();
@@ -202,11 +190,7 @@ extern "C" int orbx_plan_create(const orbx_params* prm, int width, int height, i
       set_max_dynamic_lds((const void*)k_quadtree_j6, device) ||
       set_max_dynamic_lds((const void*)k_fast_strips, device) ||
       set_max_dynamic_lds((const void*)k_fast_strips_p288, device) ||
-      set_max_dynamic_lds((const void*)k_pyramid, device) ||
-      set_max_dynamic_lds((const void*)k_pyr_stream_1024, device) ||
-      set_max_dynamic_lds((const void*)k_pyr_stream_512, device) ||
-      set_max_dynamic_lds((const void*)k_pyr_stream_256, device) ||
-      set_max_dynamic_lds((const void*)k_pyrfast, device)) { plan_free(p); return ORBX_ERR_HIP; }
+      set_max_dynamic_lds((const void*)k_pyramid, device)) { plan_free(p); return ORBX_ERR_HIP; }
   if (p->overlap && (hipStreamCreateWithFlags(&p->s_aux, hipStreamNonBlocking) != hipSuccess ||
                      hipEventCreateWithFlags(&p->ev_aux0, hipEventDisableTiming) != hipSuccess ||
                      hipEventCreateWithFlags(&p->ev_aux1, hipEventDisableTiming) != hipSuccess)) {
@@ -267,11 +251,7 @@ extern "C" int orbx_plan_create(const orbx_params* prm, int width, int height, i
       upload(&p->d_xofs1, P.xofs1, us) || upload(&p->d_yofs, P.yofs, us) ||
       upload(&p->d_alpha, P.alpha, us) || upload(&p->d_beta, P.beta, us) ||
       upload(&p->d_pyr_xs, P.pyr_xs, us) || upload(&p->d_pyr_ys, P.pyr_ys, us) ||
-      upload(&p->d_pyr_bo, P.pyr_bo, us) || upload(&p->d_pyr_blob, P.pyr_blob, us) ||
-      upload(&p->d_ps_tasks, P.ps_tasks, us) || upload(&p->d_ps_xlut, P.ps_xlut, us) ||
-      upload(&p->d_ps_ylut, P.ps_ylut, us) || upload(&p->d_ps_tick_end, P.ps_tick_end, us) ||
-      upload(&p->d_pf_tasks, P.pf_tasks, us) || upload(&p->d_pf_xlut, P.pf_xlut, us) ||
-      upload(&p->d_pf_ylut, P.pf_ylut, us) || upload(&p->d_pf_tick_end, P.pf_tick_end, us)) {
+      upload(&p->d_pyr_bo, P.pyr_bo, us) || upload(&p->d_pyr_blob, P.pyr_blob, us)) {
     plan_free(p);
     return ORBX_ERR_HIP;
   }
@@ -283,7 +263,6 @@ extern "C" int orbx_plan_create(const orbx_params* prm, int width, int height, i
   const size_t B = (size_t)max_batch;
   if (dev_alloc((void**)&p->d_pyr, B * p->pyr_stride) ||
       dev_alloc((void**)&p->d_slots, B * p->slot_stride * 4) ||
-      (P.pf_ok && dev_alloc((void**)&p->d_slots_hi, B * p->slot_stride * 4)) ||
       dev_alloc((void**)&p->d_ccount, B * (size_t)(P.ncells ? P.ncells : 1) * 4) ||
       dev_alloc((void**)&p->d_qkeys, B * p->qk_stride * 4) ||
       dev_alloc((void**)&p->d_qnode, B * p->qk_stride * 4) ||
@@ -334,9 +313,6 @@ static int extract_pass(orbx_plan* p, const uint8_t* frames, int n, size_t fstri
   const int L = P.params.nlevels;
   uint8_t* const d_pyr = p->d_pyr + f0 * p->pyr_stride;
   uint32_t* const d_slots = p->d_slots + f0 * p->slot_stride;
-  uint32_t* const d_slots_hi = p->d_slots_hi ? p->d_slots_hi + f0 * p->slot_stride : nullptr;
-  // fused pyramid + FAST (k_pyrfast, one workgroup per frame) when asked for
-  const bool fused = P.pf_ok && (p->options & ORBX_PLAN_FUSED) != 0;
   uint32_t* const d_ccount = p->d_ccount + f0 * (size_t)P.ncells;
   uint32_t* const d_qkeys = p->d_qkeys + f0 * p->qk_stride;
   int32_t* const d_qnode = p->d_qnode + f0 * p->qk_stride;
@@ -351,7 +327,7 @@ static int extract_pass(orbx_plan* p, const uint8_t* frames, int n, size_t fstri
                        p->d_err + ORBX_ERRW_FAST_OVF, strip0, p->dbg);
   };
   const int nstrips = (int)P.strips.size();
-  const bool overlap = !fused && p->overlap && p->s_aux && P.nstrips_l0 > 0;
+  const bool overlap = p->overlap && p->s_aux && P.nstrips_l0 > 0;
   if (overlap) {
     // FAST on level 0 (which needs no pyramid) runs on the auxiliary stream
     // beside the pyramid kernel; the other levels' strips follow the pyramid
@@ -360,29 +336,11 @@ static int extract_pass(orbx_plan* p, const uint8_t* frames, int n, size_t fstri
     fast_launch(0, P.nstrips_l0, p->s_aux);
     if (hipEventRecord(p->ev_aux1, p->s_aux) != hipSuccess) return ORBX_ERR_HIP;
   }
-  // K1 pyramid: the tile chain (many small workgroups per frame), or on
-  // request the row-streaming kernel (one workgroup per frame)
-  if (!fused) p->timer.begin(ORBX_STAGE_RESIZE, s);  // fused: all in the FAST stage's launch
-  // (measured slower than the tile chain at every bench workload -- DESIGN
-  // §4 round 4 -- so only on request)
-  const bool stream = !fused && P.ps_ok && (p->options & ORBX_PLAN_PYR_STREAM);
-  if (stream) {
-    // waves per frame: 16 up to 256 frames (one workgroup per CU), fewer for
-    // larger batches (several frames per CU)
-    const int nt = n > 512 ? 256 : n > 256 ? 512 : 1024;
-    const int al16 = ((reinterpret_cast<uintptr_t>(frames) | fstride | rstride) & 15) == 0;
-    auto ps_launch = [&](auto kern) {
-      hipLaunchKernelGGL(kern, dim3((unsigned)n), dim3((unsigned)nt), P.ps.lds_bytes, s, frames, fstride,
-                         rstride, d_pyr, p->pyr_stride, P.ps, reinterpret_cast<const uint2*>(p->d_ps_tasks),
-                         p->d_ps_tick_end, reinterpret_cast<const uint4*>(p->d_ps_xlut),
-                         reinterpret_cast<const uint2*>(p->d_ps_ylut), al16);
-    };
-    if (nt == 1024) ps_launch(k_pyr_stream_1024);
-    else if (nt == 512) ps_launch(k_pyr_stream_512);
-    else ps_launch(k_pyr_stream_256);
-  }
+  // K1 pyramid: the tile chain (many small workgroups per frame; the
+  // row-streaming and fused kernels of round 4 measured slower and were
+  // retired)
+  p->timer.begin(ORBX_STAGE_RESIZE, s);
   for (const PyrSeg& g : P.segs) {
-    if (stream || fused) break;
     if (g.area) {
       hipLaunchKernelGGL(k_pyr_area2, dim3((unsigned)((g.w[1] + 1023) / 1024), (unsigned)g.h[1], (unsigned)n),
                          dim3(256), 0, s, frames, fstride, rstride, d_pyr, p->pyr_stride, g);
@@ -394,19 +352,13 @@ static int extract_pass(orbx_plan* p, const uint8_t* frames, int n, size_t fstri
                        reinterpret_cast<const int4*>(p->d_pyr_ys),
                        reinterpret_cast<const uint4*>(p->d_pyr_blob), p->d_pyr_bo, p->dbg);
   }
-  if (!fused) p->timer.end(ORBX_STAGE_RESIZE, s);
+  p->timer.end(ORBX_STAGE_RESIZE, s);
   if (p->ev_after_pyr && hipEventRecord(p->ev_after_pyr, s) != hipSuccess) return ORBX_ERR_HIP;
   // K2 FAST cells
   p->timer.begin(ORBX_STAGE_FAST, s);
   if (overlap) {
     fast_launch(P.nstrips_l0, nstrips - P.nstrips_l0, s);
     if (hipStreamWaitEvent(s, p->ev_aux1, 0) != hipSuccess) return ORBX_ERR_HIP;
-  } else if (fused) {
-    const int al16 = ((reinterpret_cast<uintptr_t>(frames) | fstride | rstride) & 15) == 0;
-    hipLaunchKernelGGL(k_pyrfast, dim3((unsigned)n), dim3(1024), P.pf.lds_bytes, s, frames, fstride, rstride, d_pyr,
-                       p->pyr_stride, P.pf, reinterpret_cast<const uint2*>(p->d_pf_tasks), p->d_pf_tick_end,
-                       reinterpret_cast<const uint4*>(p->d_pf_xlut), reinterpret_cast<const uint2*>(p->d_pf_ylut),
-                       p->d_cells, d_slots, d_slots_hi, p->slot_stride, d_ccount, P.ncells, al16);
   } else {
     fast_launch(0, nstrips, s);
   }
@@ -419,8 +371,7 @@ static int extract_pass(orbx_plan* p, const uint8_t* frames, int n, size_t fstri
                      dim3(256), p->qt_lds, s, p->d_lv, p->d_cells,
                      d_slots, p->slot_stride, d_ccount, P.ncells, d_qkeys, d_qnode,
                      p->qk_stride, d_qout, p->qout_stride, d_lcount, L, P.qt_smax,
-                     P.qt_max_cells, p->d_err, p->d_qperm + f0 * p->qout_stride,
-                     fused ? d_slots_hi : d_slots);
+                     P.qt_max_cells, p->d_err, p->d_qperm + f0 * p->qout_stride);
   p->timer.end(ORBX_STAGE_QUADTREE, s);
   // K4+K5+K6+K7 orientation, blur-at-sample descriptors, assembly
   p->timer.begin(ORBX_STAGE_BRIEF, s);
@@ -457,19 +408,24 @@ extern "C" int orbx_plan_extract(orbx_plan* p, const uint8_t* frames, int nframe
     return ORBX_ERR_ARG;
   const Plan& P = p->P;
   if (rstride < (size_t)P.W || fstride < rstride * (size_t)P.H) return ORBX_ERR_ARG;
-  /* the kernels form row offsets with 24-bit multiplies (__umul24) */
-  if (rstride >= ((size_t)1 << 24)) return ORBX_ERR_UNSUPPORTED;
+  /* the kernels form row offsets with 24-bit multiplies (__umul24) and the
+   * BRIEF patch base of level 0 (the caller's frame) as a 32-bit product of
+   * row and stride: every row offset of a frame must fit 32 bits */
+  if (rstride >= ((size_t)1 << 24) || rstride * (size_t)P.H >= ((size_t)1 << 32))
+    return ORBX_ERR_UNSUPPORTED;
   ORBX_TRY(hipSetDevice(p->device));
   hipStream_t s = (hipStream_t)stream; /* NULL = the default stream */
   // frames in passes of p->chunk: one pass's pyramid levels stay in the
   // Infinity Cache for its FAST and BRIEF reads
   const int ck = p->chunk > 0 ? p->chunk : nframes;
   const size_t kc = (size_t)P.kcap;
+  p->nextracted = 0;
   for (int c = 0; c < nframes; c += ck) {
     const int rc = extract_pass(p, frames + (size_t)c * fstride, std::min(ck, nframes - c), fstride, rstride,
                                 kps + (size_t)c * kc, desc + (size_t)c * kc * 32, counts + c, s, (size_t)c);
     if (rc) return rc;
   }
+  p->nextracted = nframes;
   return ORBX_OK;
 }
 
@@ -490,11 +446,7 @@ extern "C" int orbx_plan_check(orbx_plan* p, void* stream) {
 }
 
 extern "C" int orbx_plan_set_options(orbx_plan* p, int flags) {
-  if (!p || (flags & ~(ORBX_PLAN_PYR_TILES | ORBX_PLAN_PYR_STREAM | ORBX_PLAN_FUSED)) ||
-      (flags & (ORBX_PLAN_PYR_TILES | ORBX_PLAN_PYR_STREAM)) == (ORBX_PLAN_PYR_TILES | ORBX_PLAN_PYR_STREAM))
-    return ORBX_ERR_ARG;
-  if ((flags & ORBX_PLAN_PYR_STREAM) && !p->P.ps_ok) return ORBX_ERR_UNSUPPORTED;
-  if ((flags & ORBX_PLAN_FUSED) && !p->P.pf_ok) return ORBX_ERR_UNSUPPORTED;
+  if (!p || (flags & ~ORBX_PLAN_PYR_TILES)) return ORBX_ERR_ARG;
   p->options = flags;
   return ORBX_OK;
 }
@@ -507,6 +459,7 @@ extern "C" int orbx_plan_level(orbx_plan* p, int frame, int level, uint8_t* dst,
   if (height) *height = L.h;
   if (L.unique == 0) return ORBX_ERR_ARG;
   if (!dst) return ORBX_OK;
+  if (frame >= p->nextracted) return ORBX_ERR_ARG; /* frames the last extraction wrote */
   if (dst_stride < (size_t)L.w) return ORBX_ERR_ARG;
   ORBX_TRY(hipSetDevice(p->device));
   hipStream_t s = (hipStream_t)stream;

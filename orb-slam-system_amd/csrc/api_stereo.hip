@@ -181,7 +181,9 @@ extern "C" int orbs_plan_match(orbs_plan* sp, int nframes, const orbx_plan* left
       !d_desc_r || !d_count_r || !d_uright || !d_depth || !d_nmatches)
     return ORBX_ERR_ARG;
   if (row_stride < (size_t)sp->W || frame_stride < row_stride * (size_t)sp->H) return ORBX_ERR_ARG;
-  if (row_stride >= ((size_t)1 << 24)) return ORBX_ERR_UNSUPPORTED; /* 24-bit row offsets */
+  /* 24-bit row offsets, 32-bit offsets within a frame */
+  if (row_stride >= ((size_t)1 << 24) || row_stride * (size_t)sp->H >= ((size_t)1 << 32))
+    return ORBX_ERR_UNSUPPORTED;
   ORBX_TRY(hipSetDevice(sp->device));
   return splan_launch(sp, nframes, d_frames_l, d_frames_r, frame_stride, row_stride, left->d_pyr,
                       right->d_pyr, left->pyr_stride, d_kps_l, d_desc_l, d_count_l, d_kps_r,

@@ -1,5 +1,5 @@
-// fast_ops.h -- FAST-9/16 primitives shared by k_fast_strips
-// (kernels_extract.hip) and k_pyrfast (kernels_stream.hip): the strength
+// fast_ops.h -- FAST-9/16 primitives of k_fast_strips
+// (kernels_extract.hip): the strength
 // A(p) = max(0, max_arc min_k I_k - p, p - min_arc max_k I_k) over the 16 arcs
 // of 9 contiguous circle pixels (cv::FAST reports p at threshold t iff
 // A(p) > t and cornerScore<16> returns A - 1; ORBextractor.cc:330-331), the

@@ -381,411 +381,6 @@ static int plan_pyramid(Plan& P) {
   return ORBX_OK;
 }
 
-/* ---- row-streaming pyramid (k_pyr_stream) ------------------------------
- * Same arithmetic and coefficient packing as k_pyramid's blobs (origin =
- * column 0 of the full-width source row).  The schedule: level-0 rows
- * [r0 k, r0 (k+1)) arrive in tick k; level j produces, in tick k, every row
- * whose two source rows were produced before tick k.  A level's ring holds
- * the rows live in any tick: the ones written in it and the ones its
- * successor reads in it, so a slot is never rewritten while a later tick
- * still reads it (rows read at tick k are >= that tick's lowest read row). */
-bool plan_pyr_stream(Plan& P, int r0, int rpt) {
-  P.ps_ok = false;
-  P.ps_tasks.clear();
-  P.ps_tick_end.clear();
-  P.ps_xlut.clear();
-  P.ps_ylut.clear();
-  if (r0 < 1 || rpt < 1 || rpt > 255) return false;
-  std::vector<int> ch;
-  for (int l = 0; l < (int)P.levels.size(); ++l)
-    if (P.levels[l].unique == l) ch.push_back(l);
-  const int n = (int)ch.size();
-  if (n < 2 || n > ORBX_PS_MAXL) return false;
-  for (int j = 1; j < n; ++j)
-    if (P.area2[ch[j]] || P.levels[ch[j]].src_level != ch[j - 1]) return false;
-  PyrStream S;
-  memset(&S, 0, sizeof(S));
-  S.nl = n;
-  S.r0 = r0;
-  for (int j = 0; j < n; ++j) {
-    const LevelInfo& lv = P.levels[ch[j]];
-    S.lev[j] = ch[j];
-    S.w[j] = lv.w;
-    S.h[j] = lv.h;
-    S.ng[j] = (lv.w + 3) >> 2;
-    if (j > 0) {
-      S.gpitch[j] = lv.pitch;
-      S.goff[j] = lv.pyr_off;
-      if (lv.h > 8191 || (S.ng[j] + 63) / 64 > 127) return false; /* task word fields */
-    }
-  }
-  /* column LUT: uint2 per column, 4 per group (build_blobs layout, origin 0) */
-  for (int j = 1; j < n; ++j) {
-    const LevelInfo& lv = P.levels[ch[j]];
-    S.xl[j] = (int)(P.ps_xlut.size() / 2);
-    for (int g = 0; g < S.ng[j]; ++g) {
-      int glo = 0;
-      for (int k = 0; k < 4; ++k) {
-        const int d = std::min(4 * g + k, lv.w - 1);
-        const int lo = P.xofs[lv.lut_x + d], hi = P.xofs1[lv.lut_x + d];
-        const int16_t* cf = &P.alpha[2 * (lv.lut_x + d)];
-        if (cf[0] < 0 || cf[0] > 4095 || cf[1] < 0 || cf[1] > 4095) return false;
-        if (k == 0) glo = lo;
-        if (hi - glo > 7 || lo < glo) return false;
-        if (k == 0)
-          P.ps_xlut.push_back((uint32_t)lo | ((uint32_t)(hi - lo) << 16));
-        else
-          P.ps_xlut.push_back((uint32_t)(lo - glo) | 0x0C00u | ((uint32_t)(hi - glo) << 16) | 0x0C000000u);
-        P.ps_xlut.push_back((uint32_t)(uint16_t)cf[0] | ((uint32_t)(uint16_t)cf[1] << 16));
-      }
-    }
-  }
-  /* source rows of destination row y of chain level j (clamped as cv::resize) */
-  auto src_rows = [&](int j, int y, int& s0, int& s1) {
-    const int sy = P.yofs[P.levels[ch[j]].lut_y + y];
-    s0 = std::min(std::max(sy, 0), S.h[j - 1] - 1);
-    s1 = std::min(std::max(sy + 1, 0), S.h[j - 1] - 1);
-  };
-  /* schedule */
-  std::vector<int> nxt(n, 0), span(n, 0);
-  struct Tick { std::vector<int> a, b; };
-  std::vector<Tick> ticks;
-  for (int k = 0;; ++k) {
-    bool done = true;
-    for (int j = 0; j < n; ++j) done = done && nxt[j] >= S.h[j];
-    if (done) break;
-    if (k > 4 * S.h[0] + 64) return false; /* no progress: cannot happen for a chain */
-    Tick t;
-    t.a = nxt;
-    t.b = nxt;
-    t.b[0] = std::min(S.h[0], r0 * (k + 1));
-    t.a[0] = std::min(S.h[0], r0 * k);
-    std::vector<int> readlo(n, 1 << 30);
-    for (int j = 1; j < n; ++j) {
-      int y = nxt[j];
-      while (y < S.h[j]) {
-        int s0, s1;
-        src_rows(j, y, s0, s1);
-        if (std::max(s0, s1) >= nxt[j - 1]) break; /* produced before this tick? */
-        readlo[j - 1] = std::min(readlo[j - 1], s0);
-        ++y;
-      }
-      t.b[j] = y;
-    }
-    for (int j = 0; j < n; ++j) {
-      const int lo = std::min(readlo[j], t.a[j]);
-      span[j] = std::max(span[j], t.b[j] - lo);
-    }
-    nxt = t.b;
-    ticks.push_back(t);
-  }
-  S.nticks = (int)ticks.size();
-  /* LDS: column LUT, then one ring per chain level, 16 B slack (the
-   * horizontal pass reads up to 12 bytes past a row), then the ticket */
-  long long off = ((long long)P.ps_xlut.size() * 4 + 15) & ~15LL;
-  S.lut_lds = 0;
-  S.lut_bytes = (int)off;
-  for (int j = 0; j < n; ++j) {
-    S.rrows[j] = std::max(span[j], 1);
-    if (S.rrows[j] > 255) return false;
-    S.rpitch[j] = (S.w[j] + 15) & ~15;
-    S.roff[j] = (int)off;
-    off += (long long)S.rrows[j] * S.rpitch[j];
-  }
-  off += 16 + 16;
-  if (off > ORBX_PS_LDS_MAX) return false;
-  S.lds_bytes = (int)off;
-  /* row LUT: ring slots of both source rows and of the destination row,
-   * coefficient pair; the kernel's vertical step needs b0, b1 < 4096 */
-  for (int j = 1; j < n; ++j) {
-    const LevelInfo& lv = P.levels[ch[j]];
-    S.yl[j] = (int)(P.ps_ylut.size() / 2);
-    for (int y = 0; y < S.h[j]; ++y) {
-      int s0, s1;
-      src_rows(j, y, s0, s1);
-      const int16_t* cf = &P.beta[2 * (lv.lut_y + y)];
-      if (cf[0] < 0 || cf[0] > 4095 || cf[1] < 0 || cf[1] > 4095) return false;
-      P.ps_ylut.push_back((uint32_t)(s0 % S.rrows[j - 1]) | ((uint32_t)(s1 % S.rrows[j - 1]) << 8) |
-                          ((uint32_t)(y % S.rrows[j]) << 16));
-      P.ps_ylut.push_back((uint32_t)(uint16_t)cf[0] | ((uint32_t)(uint16_t)cf[1] << 16));
-    }
-  }
-  /* tasks: per tick, every (level, 64-group chunk, run of <= rpt rows) of the
-   * rows produced in it, largest runs first (the ticket hands them out in
-   * this order, so the tick's tail is made of small tasks) */
-  for (const Tick& t : ticks) {
-    std::vector<std::pair<int, uint64_t>> tk;
-    for (int j = 1; j < n; ++j) {
-      const int nch = (S.ng[j] + 63) / 64;
-      for (int y0 = t.a[j]; y0 < t.b[j]; y0 += rpt) {
-        const int nr = std::min(rpt, t.b[j] - y0);
-        for (int c = 0; c < nch; ++c) {
-          const uint32_t x = ORBX_PS_RESIZE | ((uint32_t)j << 4) | ((uint32_t)c << 9) | ((uint32_t)nr << 16);
-          tk.push_back({-nr * 64 * 1024 + j, ((uint64_t)x << 32) | (uint32_t)y0});
-        }
-      }
-    }
-    std::stable_sort(tk.begin(), tk.end(), [](const std::pair<int, uint64_t>& a, const std::pair<int, uint64_t>& b) {
-      return a.first < b.first;
-    });
-    for (auto& e : tk) {
-      P.ps_tasks.push_back((uint32_t)(e.second >> 32));
-      P.ps_tasks.push_back((uint32_t)e.second);
-    }
-    P.ps_tick_end.push_back((int)(P.ps_tasks.size() / 2));
-  }
-  P.ps = S;
-  P.ps_ok = true;
-  return true;
-}
-
-/* ---- fused pyramid + FAST (k_pyrfast) ----------------------------------
- * Per pass (source level), tick k: the ring holds source rows [0, R k)
- * (those of earlier ticks); stage A / B run on detection rows whose 7-row
- * window is in it, stage C (phase 2) on the same rows, the next level's rows
- * whose two source rows are in it are resized, and NMS + emit run on the
- * detection rows whose strength rows y-1..y+1 were finished in earlier
- * ticks.  Ring sizes are the largest live spans (rows read or written in one
- * tick), as for plan_pyr_stream. */
-bool plan_pyr_fast(Plan& P, int rows0, int rpt) {
-  P.pf_ok = false;
-  P.pf_tasks.clear();
-  P.pf_tick_end.clear();
-  P.pf_xlut.clear();
-  P.pf_ylut.clear();
-  if (rows0 < 1 || rpt < 1 || rpt > 8) return false;
-  std::vector<int> ch;
-  for (int l = 0; l < (int)P.levels.size(); ++l)
-    if (P.levels[l].unique == l) ch.push_back(l);
-  const int n = (int)ch.size();
-  if (n < 1 || n > ORBX_PF_MAXP) return false;
-  for (int j = 1; j < n; ++j)
-    if (P.area2[ch[j]] || P.levels[ch[j]].src_level != ch[j - 1]) return false;
-  PyrFast F;
-  memset(&F, 0, sizeof(F));
-  F.np = n;
-  F.key_xs = P.levels[0].key_xs;
-  F.ini_th = P.ini_th;
-  F.min_th = P.min_th;
-  const int W0 = P.levels[0].w;
-  long long ring_max = 0, aring_max = 0, bmap_max = 0, lut_max = 0;
-  int cells_max = 1, ncv_max = 1, w_max = 0;
-  for (int p = 0; p < n; ++p) {
-    PyrFastPass& Q = F.p[p];
-    const LevelInfo& lv = P.levels[ch[p]];
-    Q.lev = ch[p];
-    Q.w = lv.w;
-    Q.h = lv.h;
-    Q.spitch = p == 0 ? 0 : lv.pitch;
-    Q.soff = p == 0 ? -1 : lv.pyr_off;
-    if (lv.h > 16383 || lv.w > 8191) return false; /* task / entry fields */
-    Q.R = std::max(4, (int)(((long long)rows0 * W0 + lv.w / 2) / lv.w));
-    Q.rpitch = (lv.w + 15) & ~15;
-    Q.bmw = (lv.w + 31) >> 5;
-    w_max = std::max(w_max, lv.w);
-    /* FAST cells of this level: row-major, the same count of valid cells per
-     * row, zones [x+3, x+w-3) x [y+3, y+h-3) tiling one rectangle */
-    Q.fast = 0;
-    if (lv.ncells > 0) {
-      const CellInfo* c = &P.cells[lv.cell_begin];
-      int ncv = 0;
-      while (ncv < lv.ncells && c[ncv].y == c[0].y) ++ncv;
-      if (lv.ncells % ncv) return false;
-      const int nrv = lv.ncells / ncv;
-      Q.ncv = ncv;
-      Q.nrv = nrv;
-      Q.wcell = P.geo.wcell[ch[p]];
-      Q.hcell = P.geo.hcell[ch[p]];
-      Q.cell_begin = lv.cell_begin;
-      Q.c0 = c[0].x + 3;
-      Q.y0 = c[0].y + 3;
-      Q.c1 = c[ncv - 1].x + c[ncv - 1].w - 3;
-      Q.y1 = c[(nrv - 1) * ncv].y + c[(nrv - 1) * ncv].h - 3;
-      for (int i = 0; i < nrv; ++i)
-        for (int jc = 0; jc < ncv; ++jc) {
-          const CellInfo& e = c[i * ncv + jc];
-          const int zx0 = Q.c0 + jc * Q.wcell, zx1 = jc == ncv - 1 ? Q.c1 : zx0 + Q.wcell;
-          const int zy0 = Q.y0 + i * Q.hcell, zy1 = i == nrv - 1 ? Q.y1 : zy0 + Q.hcell;
-          if (e.x + 3 != zx0 || e.x + e.w - 3 != zx1 || e.y + 3 != zy0 || e.y + e.h - 3 != zy1 || zx1 <= zx0 ||
-              zy1 <= zy0 || zx1 - zx0 > 64)
-            return false;
-        }
-      if (Q.c0 < 4 || Q.y0 < 3 || Q.c1 + 3 > lv.w || Q.y1 + 3 > lv.h) return false;
-      Q.fast = 1;
-      Q.gs = Q.c0 >> 2;
-      const int ngd = ((Q.c1 - 1) >> 2) - Q.gs + 1;
-      Q.nchunk = (ngd + 61) / 62;
-      if (Q.nchunk > 127) return false;
-      cells_max = std::max(cells_max, lv.ncells);
-      ncv_max = std::max(ncv_max, ncv);
-    }
-    Q.next = p + 1 < n;
-    if (Q.next) {
-      const LevelInfo& nv = P.levels[ch[p + 1]];
-      Q.nw = nv.w;
-      Q.nh = nv.h;
-      Q.ng = (nv.w + 3) >> 2;
-      Q.npitch = nv.pitch;
-      Q.noff = nv.pyr_off;
-      if ((Q.ng + 63) / 64 > 127 || nv.h > 16383) return false;
-      /* column LUT (build_blobs layout, origin 0) */
-      Q.xl = (int)(P.pf_xlut.size() / 2);
-      for (int g = 0; g < Q.ng; ++g) {
-        int glo = 0;
-        for (int k = 0; k < 4; ++k) {
-          const int d = std::min(4 * g + k, nv.w - 1);
-          const int lo = P.xofs[nv.lut_x + d], hi = P.xofs1[nv.lut_x + d];
-          const int16_t* cf = &P.alpha[2 * (nv.lut_x + d)];
-          if (cf[0] < 0 || cf[0] > 4095 || cf[1] < 0 || cf[1] > 4095) return false;
-          if (k == 0) glo = lo;
-          if (hi - glo > 7 || lo < glo) return false;
-          if (k == 0)
-            P.pf_xlut.push_back((uint32_t)lo | ((uint32_t)(hi - lo) << 16));
-          else
-            P.pf_xlut.push_back((uint32_t)(lo - glo) | 0x0C00u | ((uint32_t)(hi - glo) << 16) | 0x0C000000u);
-          P.pf_xlut.push_back((uint32_t)(uint16_t)cf[0] | ((uint32_t)(uint16_t)cf[1] << 16));
-        }
-      }
-      lut_max = std::max(lut_max, (long long)Q.ng * 32);
-    }
-  }
-  /* schedules */
-  for (int p = 0; p < n; ++p) {
-    PyrFastPass& Q = F.p[p];
-    Q.tick0 = (int)P.pf_tick_end.size() / 2;
-    const int yd0 = Q.fast ? Q.y0 : 0, yd1 = Q.fast ? Q.y1 : 0;
-    int da = yd0, dn = yd0, dr = 0;
-    const int nh = Q.next ? Q.nh : 0;
-    const LevelInfo* nv = Q.next ? &P.levels[F.p[p + 1].lev] : nullptr;
-    auto src_rows = [&](int y, int& s0, int& s1) {
-      const int sy = P.yofs[nv->lut_y + y];
-      s0 = std::min(std::max(sy, 0), Q.h - 1);
-      s1 = std::min(std::max(sy + 1, 0), Q.h - 1);
-    };
-    int rspan = 1, aspan = 1;
-    struct TickRec { int a0, a1, n0, n1, r0, r1; };
-    std::vector<TickRec> tr;
-    for (int k = 0;; ++k) {
-      if (da >= yd1 && dn >= yd1 && dr >= nh) break;
-      if (k > 4 * Q.h + 64) return false;
-      const int av = std::min(Q.h, Q.R * k), av1 = std::min(Q.h, Q.R * (k + 1));
-      TickRec t;
-      t.a0 = da;
-      t.a1 = std::max(da, std::min(yd1, av - 3));
-      const int aend = da; /* strength rows finished before this tick: [yd0, aend) */
-      t.n0 = dn;
-      t.n1 = aend >= yd1 ? yd1 : std::max(dn, aend - 1);
-      t.r0 = dr;
-      int y = dr, rlo = 1 << 30;
-      while (y < nh) {
-        int s0, s1;
-        src_rows(y, s0, s1);
-        if (std::max(s0, s1) >= av) break;
-        rlo = std::min(rlo, s0);
-        ++y;
-      }
-      t.r1 = y;
-      int lo = av;
-      if (t.a1 > t.a0) lo = std::min(lo, t.a0 - 3);
-      if (t.r1 > t.r0) lo = std::min(lo, rlo);
-      rspan = std::max(rspan, av1 - lo);
-      if (t.a1 > t.a0 || t.n1 > t.n0) {
-        int alo = 1 << 30, ahi = -1;
-        if (t.a1 > t.a0) { alo = std::min(alo, t.a0); ahi = std::max(ahi, t.a1 - 1); }
-        if (t.n1 > t.n0) { alo = std::min(alo, std::max(yd0, t.n0 - 1)); ahi = std::max(ahi, std::min(yd1 - 1, t.n1)); }
-        aspan = std::max(aspan, ahi - alo + 1);
-      }
-      da = t.a1;
-      dn = t.n1;
-      dr = t.r1;
-      tr.push_back(t);
-    }
-    Q.nticks = (int)tr.size();
-    Q.rrows = rspan;
-    Q.arows = aspan;
-    if (Q.rrows > 255 || Q.arows > 255) return false;
-    ring_max = std::max(ring_max, (long long)(Q.rrows + 6) * Q.rpitch); /* + 3 guard rows each side */
-    aring_max = std::max(aring_max, (long long)Q.arows * Q.rpitch);
-    bmap_max = std::max(bmap_max, (long long)Q.arows * Q.bmw * 4);
-    /* row LUT of the next level: this pass's ring slots of both source rows */
-    if (Q.next) {
-      Q.yl = (int)(P.pf_ylut.size() / 2);
-      for (int yy = 0; yy < nh; ++yy) {
-        int s0, s1;
-        src_rows(yy, s0, s1);
-        const int16_t* cf = &P.beta[2 * (nv->lut_y + yy)];
-        if (cf[0] < 0 || cf[0] > 4095 || cf[1] < 0 || cf[1] > 4095) return false;
-        P.pf_ylut.push_back((uint32_t)(s0 % Q.rrows) | ((uint32_t)(s1 % Q.rrows) << 8));
-        P.pf_ylut.push_back((uint32_t)(uint16_t)cf[0] | ((uint32_t)(uint16_t)cf[1] << 16));
-      }
-    }
-    /* tasks per tick, two lists (tick_end holds both ends): phase 1 the two
-     * NMS tasks (cell columns [0, ncv/2) and [ncv/2, ncv): one wave walks
-     * each half's rows in order; they lead, being the longest) and stage A;
-     * phase 2 the resize (it reads only ring rows of earlier ticks and writes
-     * HBM, so it runs beside stage C), each list largest first */
-    for (const TickRec& t : tr) {
-      std::vector<std::pair<int, uint64_t>> tk;
-      auto add = [&](int type, int chunk, int nr, uint32_t y, int cost) {
-        const uint32_t x = (uint32_t)type | ((uint32_t)p << 4) | ((uint32_t)chunk << 9) | ((uint32_t)nr << 16);
-        tk.push_back({-cost, ((uint64_t)x << 32) | y});
-      };
-      auto flush = [&]() {
-        std::stable_sort(tk.begin(), tk.end(),
-                         [](const std::pair<int, uint64_t>& a, const std::pair<int, uint64_t>& b) { return a.first < b.first; });
-        for (auto& e : tk) {
-          P.pf_tasks.push_back((uint32_t)(e.second >> 32));
-          P.pf_tasks.push_back((uint32_t)e.second);
-        }
-        tk.clear();
-        P.pf_tick_end.push_back((int)(P.pf_tasks.size() / 2));
-      };
-      if (t.n1 - t.n0 > 255) return false; /* one NMS task per half and tick */
-      if (t.n1 > t.n0)
-        for (int half = 0; half < (Q.ncv > 1 ? 2 : 1); ++half)
-          add(ORBX_PF_NMS, half, t.n1 - t.n0, (uint32_t)t.n0 | ((uint32_t)(t.n0 % Q.arows) << 22), 1 << 28);
-      for (int y0 = t.a0; y0 < t.a1; y0 += rpt) {
-        const int nr = std::min(rpt, t.a1 - y0);
-        for (int c = 0; c < Q.nchunk; ++c)
-          add(ORBX_PF_FASTA, c, nr,
-              (uint32_t)y0 | ((uint32_t)((y0 - 3) % Q.rrows) << 14) | ((uint32_t)(y0 % Q.arows) << 22), 3 * nr);
-      }
-      flush();
-      for (int y0 = t.r0; y0 < t.r1; y0 += rpt) {
-        const int nr = std::min(rpt, t.r1 - y0);
-        for (int c = 0; c < (Q.ng + 63) / 64; ++c) add(ORBX_PS_RESIZE, c, nr, (uint32_t)y0, nr);
-      }
-      flush();
-    }
-  }
-  /* LDS layout */
-  long long off = 0;
-  auto take = [&](long long bytes) {
-    const long long o = off;
-    off += (bytes + 15) & ~15LL;
-    return (int)o;
-  };
-  F.o_ring = take(ring_max + 16);
-  F.o_aring = take(aring_max + 16);
-  F.o_bmap = take(bmap_max);
-  F.o_lut = take(lut_max);
-  F.o_cell = take(4LL * cells_max);
-  F.o_cnt = take(8LL * ncv_max);
-  F.o_l1 = take(4LL * 15 * ORBX_PF_L1CAP);
-  F.o_l2 = take(4LL * ORBX_PF_L2CAP);
-  F.nms_cap = w_max;
-  F.o_nms = take(2LL * 2 * w_max); /* one corner list per NMS half */
-  F.o_misc = take(64);
-  F.lut_max_bytes = (int)lut_max;
-  F.cells_max = cells_max;
-  F.ncv_max = ncv_max;
-  F.lds_bytes = (int)off;
-  if (off > ORBX_PF_LDS_MAX) return false;
-  P.pf = F;
-  P.pf_ok = true;
-  return true;
-}
-
 int plan_geometry(const orbx_params& p, int width, int height, Plan& P) {
   int rc = compute_tables(p, P.tables);
   if (rc) return rc;
@@ -993,18 +588,6 @@ int plan_geometry(const orbx_params& p, int width, int height, Plan& P) {
   }
   P.geo.pixels = px;
   P.geo.bytes_pyr_fast = bytes;
-  /* row-streaming pyramid: the longest tick whose rings fit the LDS budget */
-  static const int ticks[] = {8, 6, 4, 3, 2, 1};
-  int ps_rpt = 4, ps_r0max = 8;
-#ifdef ORBX_PROFILING
-  if (const char* e = getenv("ORBX_DEBUG_PS_RPT")) ps_rpt = std::max(1, atoi(e));
-  if (const char* e = getenv("ORBX_DEBUG_PS_R0")) ps_r0max = std::max(1, atoi(e));
-#endif
-  for (int r0 : ticks)
-    if (r0 <= ps_r0max && plan_pyr_stream(P, r0, ps_rpt)) break;
-  /* fused pyramid + FAST: the longest level-0 tick that fits */
-  for (int r0 : ticks)
-    if (plan_pyr_fast(P, r0, 4)) break;
   return ORBX_OK;
 }
 

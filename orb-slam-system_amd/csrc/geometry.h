@@ -46,21 +46,6 @@ struct Plan {
   std::vector<int32_t> pyr_ys;
   std::vector<uint32_t> pyr_blob; /* LUT blobs (pairs of u32 = uint2 entries) */
   std::vector<int32_t> pyr_bo;    /* blob start offsets (uint2 units), per segment ntx+1, nty+1 */
-  /* row-streaming pyramid (k_pyr_stream; orbx_internal.h); ps_ok = false when
-   * the chain has an exact-2x level or does not fit the LDS budget */
-  bool ps_ok = false;
-  PyrStream ps;
-  std::vector<uint32_t> ps_tasks;    /* uint2 {x, y} per task, ticks in order */
-  std::vector<int32_t> ps_tick_end;  /* cumulative task count after each tick */
-  std::vector<uint32_t> ps_xlut;     /* uint2 per column, 4 per group, groups of every level */
-  std::vector<uint32_t> ps_ylut;     /* uint2 per destination row: ring slots | coefficients */
-  /* fused pyramid + FAST (k_pyrfast; orbx_internal.h PyrFast) */
-  bool pf_ok = false;
-  PyrFast pf;
-  std::vector<uint32_t> pf_tasks;    /* uint2 {x, y} per task, ticks of all passes in order */
-  std::vector<int32_t> pf_tick_end;  /* cumulative task count after each tick */
-  std::vector<uint32_t> pf_xlut;     /* column LUTs (uint2 per column, 4 per group) */
-  std::vector<uint32_t> pf_ylut;     /* row LUTs: source ring slots | coefficients */
   long long pyr_bytes = 0, blur_bytes = 0, nslots = 0, qk_elems = 0;
   int ncells = 0, kcap = 0;
   int qt_smax = 0;     /* max DistributeOctTree splittable list length */
@@ -70,16 +55,6 @@ struct Plan {
 
 /* returns ORBX_OK or an ORBX_ERR_* code */
 int plan_geometry(const orbx_params& p, int width, int height, Plan& plan);
-
-/* k_pyr_stream schedule for rows_per_tick level-0 rows per tick and at most
- * rows_per_task destination rows per task (plan_geometry calls it with the
- * largest tick that fits ORBX_PS_LDS_MAX); false when not applicable */
-bool plan_pyr_stream(Plan& P, int rows_per_tick, int rows_per_task);
-
-/* k_pyrfast schedule: pass p uses ticks of about rows0 * w0 / w_p source
- * rows (at least 4), stage-A / resize tasks of at most rows_per_task rows;
- * false when not applicable (exact-2x level, LDS budget, cell geometry) */
-bool plan_pyr_fast(Plan& P, int rows0, int rows_per_task);
 
 }  // namespace orbx
 

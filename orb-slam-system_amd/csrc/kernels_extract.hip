@@ -1094,9 +1094,9 @@ __device__ __forceinline__ int upper_bound_i(const int* a, int n, int v) {
       const uint32_t *__restrict__ ccount, int ncells_total, uint32_t *__restrict__ qkeys, \
       int32_t *__restrict__ qnode, size_t qk_stride, uint32_t *__restrict__ qout,          \
       size_t qout_stride, int *__restrict__ lcount, int nlevels, int smax, int maxcells,   \
-      int *__restrict__ err, uint32_t *__restrict__ qperm, const uint32_t *__restrict__ slots_hi
+      int *__restrict__ err, uint32_t *__restrict__ qperm
 #define QT_KERNEL_PASS \
-  lv, cells, slots, slot_stride, ccount, ncells_total, qkeys, qnode, qk_stride, qout, qout_stride, lcount, nlevels, smax, maxcells, err, qperm, slots_hi
+  lv, cells, slots, slot_stride, ccount, ncells_total, qkeys, qnode, qk_stride, qout, qout_stride, lcount, nlevels, smax, maxcells, err, qperm
 
 // QJ: keys per thread held in registers (256 QJ per level; more spill to the
 // global keys/node arrays).  Both instantiations are built for 8 waves per
@@ -1137,16 +1137,13 @@ __device__ __forceinline__ void qt_body(QT_KERNEL_ARGS) {
 
   // gather vToDistributeKeys (cell-major, raster within cell)
   const int nc = U.ncells;
-  // a count with ORBX_CC_HI (k_pyrfast): the cell's keys are its iniThFAST
-  // set, in slots_hi
   const uint32_t* fcc = ccount + (size_t)f * ncells_total + U.cell_begin;
-  for (int i = tid; i < nc; i += 256) cell_off[i] = (int)(fcc[i] & ~ORBX_CC_HI);
+  for (int i = tid; i < nc; i += 256) cell_off[i] = (int)fcc[i];
   __syncthreads();
   const int C = block_scan_excl(cell_off, nc, wtmp);
   if (tid == 0) cell_off[nc] = C;
   __syncthreads();
   const uint32_t* fslots = slots + (size_t)f * slot_stride;
-  const uint32_t* fslots_hi = slots_hi + (size_t)f * slot_stride;
   // keys k = tid + 256 j (j < QJ) and their node ids live in registers for
   // the whole distribution (every pass walks all keys twice: from global
   // memory that was a load-latency chain per pass); more keys than that
@@ -1161,13 +1158,13 @@ __device__ __forceinline__ void qt_body(QT_KERNEL_ARGS) {
     nr[j] = -1;
     if (k < C) {
       const int c = upper_bound_i(cell_off, nc, k) - 1;
-      kr[j] = ((fcc[c] & ORBX_CC_HI) ? fslots_hi : fslots)[cells[U.cell_begin + c].slot_off + (k - cell_off[c])];
+      kr[j] = fslots[cells[U.cell_begin + c].slot_off + (k - cell_off[c])];
       keys[k] = kr[j];
     }
   }
   for (int k = tid + 256 * QJ; k < C; k += 256) {
     const int c = upper_bound_i(cell_off, nc, k) - 1;
-    keys[k] = ((fcc[c] & ORBX_CC_HI) ? fslots_hi : fslots)[cells[U.cell_begin + c].slot_off + (k - cell_off[c])];
+    keys[k] = fslots[cells[U.cell_begin + c].slot_off + (k - cell_off[c])];
   }
   __syncthreads();  // cell_off is dead: its LDS becomes the node arrays
 #if defined(QT_PROBE_STOP) && QT_PROBE_STOP == 1  // profiling only: the gather alone
@@ -1476,8 +1473,10 @@ __device__ __forceinline__ void brief_issue(const BriefKp& k, BriefRegs& R, int 
   const uint32_t c4 = (uint32_t)(ln % 12) * 4u, r0 = (uint32_t)(ln / 12);
   R.ht = c_htask.v[k.x - k.px0 - 21][lane];  // cc = 21..24
   if (k.inside) {
-    // wave-uniform; a level is < 4 GB: 32-bit scalar offset (a size_t
-    // product here was a quarter-rate v_mad_u64_u32 per keypoint)
+    // wave-uniform; every row offset of a level fits 32 bits (levels >= 2
+    // are orbx's own buffers; for level 0, the caller's frame,
+    // orbx_plan_extract rejects rstride * H >= 2^32): 32-bit scalar offset
+    // (a size_t product here was a quarter-rate v_mad_u64_u32 per keypoint)
     const uint8_t* b = k.img + ((uint32_t)k.py0 * (uint32_t)k.pitch + (uint32_t)k.px0);
 #pragma unroll
     for (int u = 0; u < 9; ++u) {
@@ -1495,7 +1494,7 @@ __device__ __forceinline__ void brief_issue(const BriefKp& k, BriefRegs& R, int 
     for (int u = 0; u < 9; ++u) {
       const int r = min((int)r0 + 5 * u, KP_ROWS - 1);
       const int gy = reflect101(min(max(k.py0 + r, -3), k.UH + 2), k.UH);
-      const uint32_t ro = __umul24((uint32_t)gy, (uint32_t)k.pitch);
+      const uint32_t ro = __umul24((uint32_t)gy, (uint32_t)k.pitch);  // < 2^32: same API check
       if (cin) {
         R.r[u] = ld32u(k.img + (ro + (uint32_t)cx));
       } else {

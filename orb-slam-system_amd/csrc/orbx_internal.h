@@ -147,83 +147,6 @@ struct PyrSeg {
   long long off[ORBX_MAX_LEVELS]; /* pyr offset; -1 = the caller's frame (level 0) */
 };
 
-/* row-streaming pyramid (k_pyr_stream): one workgroup per frame walks the
- * frame top to bottom in ticks.  Tick k: the loader wave brings level-0 rows
- * [r0 k, r0 (k+1)) into their LDS ring; the worker waves take the tick's
- * tasks (a level, a chunk of 64 four-pixel groups, a run of destination
- * rows) by an LDS ticket and compute those rows from source rows that earlier
- * ticks left in the source level's ring; one barrier per tick.  Every level
- * row is computed once (no halo recompute) and written to HBM once; source
- * rows' horizontal passes are reused across consecutive destination rows of
- * a task.  Chain index j: 0 = level 0 (the caller's frame), j >= 1 the
- * unique levels in order. */
-#define ORBX_PS_MAXL 16
-#define ORBX_PS_LDS_MAX (150 * 1024)
-struct PyrStream {
-  int nl;         /* chain length incl. level 0 */
-  int nticks;     /* barriers = ticks */
-  int r0;         /* level-0 rows per tick */
-  int lut_lds;    /* LDS byte offset of the column LUT (uint2 entries, 4 per group) */
-  int lut_bytes;  /* its size (16-B multiple) */
-  int lds_bytes;  /* total dynamic LDS, the ticket word included */
-  int w[ORBX_PS_MAXL], h[ORBX_PS_MAXL], ng[ORBX_PS_MAXL]; /* ng = four-pixel groups per row */
-  int rrows[ORBX_PS_MAXL];  /* ring rows (row y lives in slot y % rrows) */
-  int rpitch[ORBX_PS_MAXL]; /* ring row pitch, 16-B multiple */
-  int roff[ORBX_PS_MAXL];   /* ring LDS byte offset */
-  int gpitch[ORBX_PS_MAXL]; /* HBM row pitch (j >= 1) */
-  long long goff[ORBX_PS_MAXL]; /* offset in the frame's pyramid buffer (j >= 1) */
-  int xl[ORBX_PS_MAXL];     /* first LUT entry (uint2) of level j's groups (j >= 1) */
-  int yl[ORBX_PS_MAXL];     /* first row-LUT entry of level j (j >= 1) */
-  int lev[ORBX_PS_MAXL];    /* level index of chain entry j */
-};
-/* task word x: type (bits 0-3) | chain level (4-8) | chunk (9-15) | rows (16-23); y = first row */
-#define ORBX_PS_RESIZE 1
-
-/* fused pyramid + FAST (k_pyrfast): one workgroup per frame makes one pass
- * per unique level (chain order).  Pass p streams its source level (the
- * caller's frame, or the level pass p-1 wrote) top to bottom through an LDS
- * ring in ticks of R rows; each tick's tasks run FAST's cardinal / even tests
- * (stage A in a column walk over ring rows, stage B on the per-wave survivor
- * lists), resize rows of the next level (to HBM) and NMS + emit of finished
- * detection rows; the full FAST strength of the tick's even-test survivors
- * (stage C, one shared list) runs in a second phase.  Two barriers per tick.
- * Output: the per-cell keys of the k_fast_strips layout, except that a cell
- * whose keys come from iniThFAST has ccount | ORBX_CC_HI and its keys in the
- * slots_hi array (k_quadtree reads either). */
-#define ORBX_PF_MAXP 16
-#define ORBX_PF_LDS_MAX (156 * 1024)
-#define ORBX_CC_HI 0x80000000u
-#define ORBX_PF_L1CAP 320  /* per-wave cardinal survivors: < 64 carried + <= 4 * 62 new per row */
-#define ORBX_PF_L2CAP 2048 /* shared even-test survivors per tick (overflow: stage C at once) */
-struct PyrFastPass {
-  int lev;              /* level index of the source level */
-  int w, h;             /* source level size */
-  int spitch;           /* HBM row pitch (0: the caller's row stride) */
-  long long soff;       /* pyramid offset (-1: the caller's frame) */
-  int R, tick0, nticks; /* rows per tick, first tick (tick_end holds 2 entries a tick), ticks */
-  int rrows, rpitch;    /* level ring rows / pitch (16-B multiple) */
-  int arows;            /* strength ring rows (pitch rpitch) and corner-bitmap rows */
-  int bmw;              /* corner bitmap words per row (ceil(w / 32)) */
-  int fast;             /* 0: no FAST cell on this level */
-  int c0, c1, y0, y1;   /* detection columns / rows */
-  int ncv, nrv, wcell, hcell, cell_begin;
-  int gs, nchunk;       /* first group (c0 >> 2); stage-A chunks of 62 groups */
-  int next;             /* 1: this pass resizes the next unique level */
-  int nw, nh, ng, npitch; /* next level: size, groups, HBM pitch */
-  long long noff;       /* next level's pyramid offset */
-  int xl, yl;           /* next level's column LUT (uint2 entries) / row LUT offsets in the globals */
-};
-struct PyrFast {
-  int np;
-  int lds_bytes;
-  int key_xs, ini_th, min_th;
-  /* LDS byte offsets */
-  int o_ring, o_aring, o_bmap, o_lut, o_cell, o_cnt, o_l1, o_l2, o_misc, o_nms;
-  int lut_max_bytes, cells_max, ncv_max, nms_cap;
-  PyrFastPass p[ORBX_PF_MAXP];
-};
-#define ORBX_PF_FASTA 2
-#define ORBX_PF_NMS 3
 
 #if defined(__HIPCC__)
 #define ORBX_HDI __host__ __device__ inline

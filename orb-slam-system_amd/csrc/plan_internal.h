@@ -42,13 +42,8 @@ struct orbx_plan {
   int overlap = 0; /* FAST on level 0 beside the pyramid on s_aux */
   hipStream_t s_aux = nullptr;
   hipEvent_t ev_aux0 = nullptr, ev_aux1 = nullptr;
-  /* row-streaming pyramid tables (k_pyr_stream) and the path choice */
-  uint32_t *d_ps_tasks = nullptr, *d_ps_xlut = nullptr, *d_ps_ylut = nullptr;
-  int32_t* d_ps_tick_end = nullptr;
-  /* fused pyramid + FAST tables (k_pyrfast) and its iniThFAST key lists */
-  uint32_t *d_pf_tasks = nullptr, *d_pf_xlut = nullptr, *d_pf_ylut = nullptr, *d_slots_hi = nullptr;
-  int32_t* d_pf_tick_end = nullptr;
   int options = 0; /* ORBX_PLAN_* (include/orbx.h) */
+  int nextracted = 0; /* frames of the last orbx_plan_extract (orbx_plan_level bound) */
 };
 
 struct orbx_extractor {

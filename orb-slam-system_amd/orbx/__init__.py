@@ -42,7 +42,7 @@ assert KEYPOINT_DTYPE.itemsize == 28
 OK, ERR_ARG, ERR_CELL_ROI, ERR_LEVEL_SIZE, ERR_QUADTREE, ERR_CAPACITY, ERR_UNSUPPORTED, \
     ERR_HIP, ERR_NO_DEVICE = 0, -1, -2, -3, -4, -5, -6, -7, -8
 ORBM_PLAN_ZERO_TAIL, ORBM_PLAN_VALU = 1, 2  # orbm_plan_set_options flags (include/orbx.h)
-ORBX_PLAN_PYR_TILES, ORBX_PLAN_PYR_STREAM, ORBX_PLAN_FUSED = 1, 2, 4  # orbx_plan_set_options flags
+ORBX_PLAN_PYR_TILES = 1  # orbx_plan_set_options flag
 
 EXPORTED = [
     "orbx_abi_version", "orbx_status_string", "orbx_device_count", "orbx_tables",
@@ -568,11 +568,9 @@ class Plan:
         return {"fast_overflow_strips": v.value}
 
     def set_options(self, pyramid="auto"):
-        """pyramid: 'auto' (= the tile pyramid, fastest measured), 'tiles'
-        (k_pyramid), 'stream' (k_pyr_stream, one workgroup per frame) or
-        'fused' (pyramid and cell FAST in one kernel, k_pyrfast); same results"""
-        flags = {"auto": 0, "tiles": ORBX_PLAN_PYR_TILES, "stream": ORBX_PLAN_PYR_STREAM,
-                 "fused": ORBX_PLAN_FUSED}[pyramid]
+        """pyramid: 'auto' or 'tiles' (k_pyramid, the one pyramid path since
+        the round-4 streaming kernels were retired)"""
+        flags = {"auto": 0, "tiles": ORBX_PLAN_PYR_TILES}[pyramid]
         _check(_lib.orbx_plan_set_options(self._h, flags), "orbx_plan_set_options")
 
     def level(self, frame, lvl, stream=None):

@@ -166,6 +166,45 @@ def test_batched_plan_matches_single(gpu, oracle):
         assert np.array_equal(res[f][1], rd)
 
 
+def test_plan_argument_checks(gpu, oracle):
+    """C-ABI argument checks of the batched plan:
+    * orbx_plan_set_options accepts 0 / ORBX_PLAN_PYR_TILES only; the retired
+      streaming / fused flags (2, 4) and every combination are ORBX_ERR_ARG;
+    * orbx_plan_level copies only frames the last extraction wrote
+      (ORBX_ERR_ARG before any extraction and past its frame count; the size
+      query with dst = NULL stays valid);
+    * a row stride whose frame span reaches 2^32 bytes (the kernels' 32-bit
+      in-frame offsets) is ORBX_ERR_UNSUPPORTED, refused before any launch."""
+    import ctypes
+    import torch
+    lib = gpu._lib
+    W, H, B = 640, 480, 3
+    plan = gpu.Plan(gpu.params(1000, 1.2, 8, 20, 7), W, H, B)
+    for flags in (2, 4, 3, 5, 6, 7, 8, -1):
+        assert lib.orbx_plan_set_options(plan._h, flags) == gpu.ERR_ARG, flags
+    assert lib.orbx_plan_set_options(plan._h, gpu.ORBX_PLAN_PYR_TILES) == gpu.OK
+    assert lib.orbx_plan_set_options(plan._h, 0) == gpu.OK
+    buf = np.zeros((H, W), np.uint8)
+    w, h = ctypes.c_int(0), ctypes.c_int(0)
+    assert lib.orbx_plan_level(plan._h, 0, 2, None, 0, ctypes.byref(w), ctypes.byref(h), None) == gpu.OK
+    assert (w.value, h.value) == (533, 400)
+    assert lib.orbx_plan_level(plan._h, 0, 2, buf.ctypes.data, W, None, None, None) == gpu.ERR_ARG
+    frames = torch.from_numpy(synth.frames(W, H, 70, 2, "rects")).cuda()
+    plan.extract(frames)
+    plan.check()
+    ref = oracle.Extractor(1000, 1.2, 8, 20, 7)
+    ref.extract(synth.frame(W, H, 71))
+    assert np.array_equal(plan.level(1, 2), ref.level(2))
+    assert lib.orbx_plan_level(plan._h, 2, 2, buf.ctypes.data, W, None, None, None) == gpu.ERR_ARG
+    # frame span: rows of (2^24 - 16) bytes, 480 of them > 2^32
+    rs = (1 << 24) - 16
+    rc = lib.orbx_plan_extract(plan._h, frames.data_ptr(), 1, rs * H, rs, plan.kps.data_ptr(),
+                               plan.desc.data_ptr(), plan.counts.data_ptr(), None)
+    assert rc == gpu.ERR_UNSUPPORTED
+    # a refused call leaves the last extraction's levels in place
+    assert np.array_equal(plan.level(1, 2), ref.level(2))
+
+
 @pytest.mark.parametrize("W,H,nf,guard,ccap", [(640, 480, 1000, "strict", 0),
                                                 (640, 480, 1000, "strict", 24),
                                                 (1920, 1080, 2000, "empty", 48),

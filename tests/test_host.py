@@ -188,106 +188,3 @@ def test_fused_pyramid_tiling_matches_oracle(oracle, tmp_path, W, H, nf, L, sf):
     assert off == raw.size
 
 
-# k_pyr_stream: (W, H, nfeatures, nlevels, scale, r0, rows per task); r0 = 0 is
-# the planner's own choice (the largest tick that fits the LDS budget)
-STREAM_CASES = [(1920, 1080, 2000, 8, 1.2, 0, 4), (640, 480, 1000, 8, 1.2, 0, 4),
-                (1241, 376, 2000, 8, 1.2, 0, 4), (1920, 1080, 2000, 8, 1.2, 1, 1),
-                (1920, 1080, 2000, 8, 1.2, 3, 2), (642, 361, 1000, 8, 1.2, 2, 3),
-                (752, 480, 1200, 4, 1.5, 0, 4), (640, 480, 500, 14, 1.1, 0, 4),
-                (1000, 700, 500, 3, 1.9, 0, 4), (1241, 376, 2000, 4, 1.7, 5, 4),
-                (600, 4400, 2000, 8, 1.2, 0, 4), (644, 362, 1000, 8, 1.2, 0, 4),
-                (640, 480, 800, 3, 1.95, 0, 4), (640, 480, 1000, 8, 1.3, 0, 4)]
-
-
-@pytest.mark.parametrize("W,H,nf,L,sf", [(4096, 400, 2000, 8, 1.2), (1280, 600, 1000, 6, 2.0),
-                                         (320, 240, 500, 2, 1.2)])
-def test_stream_pyramid_not_planned(tmp_path, W, H, nf, L, sf):
-    """No streaming schedule where it cannot apply: rings + column LUT past
-    the LDS budget (4096 wide), an exact-2x level (INTER_AREA path), no
-    resized level at all; those plans keep k_pyramid."""
-    exe = tmp_path / "pse"
-    csrc = os.path.join(PKG, "csrc")
-    subprocess.check_call(["g++", "-O2", "-std=c++17", "-I", csrc,
-                           os.path.join(ROOT, "tests", "cpp", "pyr_stream_emu.cpp"),
-                           os.path.join(csrc, "geometry.cpp"), "-o", str(exe)])
-    (tmp_path / "in.raw").write_bytes(synth.frame(W, H, 5, "noise").tobytes())
-    r = subprocess.run([str(exe), str(tmp_path / "in.raw"), str(W), str(H), str(nf), str(L), repr(sf),
-                        str(tmp_path / "o.bin")], capture_output=True, text=True)
-    assert r.returncode == 4 and "no stream plan" in r.stdout
-
-
-@pytest.mark.parametrize("W,H,nf,L,sf,r0,rpt", STREAM_CASES)
-def test_stream_pyramid_schedule_matches_oracle(oracle, tmp_path, W, H, nf, L, sf, r0, rpt):
-    """Host emulation of k_pyr_stream's ticks on the planner's tables: every
-    ring read finds the row it expects, written in an earlier tick; no slot is
-    written in a tick that reads it; every level row is computed once; the
-    levels equal the oracle's pyramid."""
-    exe = tmp_path / "pse"
-    csrc = os.path.join(PKG, "csrc")
-    subprocess.check_call(["g++", "-O2", "-std=c++17", "-I", csrc,
-                           os.path.join(ROOT, "tests", "cpp", "pyr_stream_emu.cpp"),
-                           os.path.join(csrc, "geometry.cpp"), "-o", str(exe)])
-    img = synth.frame(W, H, 5, "noise")
-    (tmp_path / "in.raw").write_bytes(img.tobytes())
-    out = tmp_path / "out.bin"
-    args = [str(exe), str(tmp_path / "in.raw"), str(W), str(H), str(nf), str(L), repr(sf), str(out)]
-    if r0:
-        args += [str(r0), str(rpt)]
-    r = subprocess.run(args, capture_output=True, text=True)
-    assert r.returncode == 0, r.stdout + r.stderr
-    raw = np.frombuffer(out.read_bytes(), np.uint8)
-    ref = oracle.Extractor(nf, sf, L, 20, 7, cell_guard="empty")
-    ref.extract(img)
-    off = 0
-    for l in range(1, L):
-        lv = ref.level(l)
-        if lv.shape == ref.level(l - 1).shape:
-            continue
-        assert np.array_equal(raw[off:off + lv.size].reshape(lv.shape), lv), "level %d" % l
-        off += lv.size
-    assert off == raw.size
-
-
-FUSED_CASES = [(1920, 1080, 2000, 8, 1.2), (640, 480, 1000, 8, 1.2), (1241, 376, 2000, 8, 1.2),
-               (640, 480, 1000, 1, 1.2), (752, 480, 1200, 6, 1.5), (640, 480, 1000, 12, 1.1),
-               (642, 361, 1000, 8, 1.2), (644, 362, 1000, 8, 1.2), (600, 4400, 2000, 8, 1.2),
-               (1241, 376, 2000, 4, 1.7), (640, 480, 800, 3, 1.95), (640, 480, 1000, 8, 1.3)]
-
-
-@pytest.mark.parametrize("W,H,nf,L,sf", FUSED_CASES)
-def test_fused_pyramid_fast_schedule(tmp_path, W, H, nf, L, sf):
-    """k_pyrfast's tick schedule on the planner's tables (tests/cpp/pyrfast_emu.cpp):
-    every ring / strength-ring / bitmap read finds its row, written in an
-    earlier tick, no slot is written in a phase that reads it, every
-    detection row is tested and NMS'd once (after its neighbours) and every
-    next-level row resized once."""
-    exe = tmp_path / "pfe"
-    csrc = os.path.join(PKG, "csrc")
-    subprocess.check_call(["g++", "-O2", "-std=c++17", "-I", csrc,
-                           os.path.join(ROOT, "tests", "cpp", "pyrfast_emu.cpp"),
-                           os.path.join(csrc, "geometry.cpp"), "-o", str(exe)])
-    r = subprocess.run([str(exe), str(W), str(H), str(nf), str(L), repr(sf)], capture_output=True, text=True)
-    assert r.returncode == 0 and r.stdout.startswith("ok"), r.stdout + r.stderr
-
-
-@pytest.mark.parametrize("W,H,nf,L,sf,ini,mn,kind", [
-    (1920, 1080, 2000, 8, 1.2, 20, 7, "pan"), (640, 480, 1000, 8, 1.2, 12, 5, "rects"),
-    (1241, 376, 2000, 8, 1.2, 9, 15, "noise"), (752, 480, 1200, 8, 1.2, 7, 7, "pan"),
-    (640, 480, 1000, 1, 1.2, 20, 7, "noise"), (640, 480, 1000, 8, 1.3, 20, 7, "noise")])
-def test_fused_fast_emulation_matches_oracle_candidates(tmp_path, W, H, nf, L, sf, ini, mn, kind):
-    """k_pyrfast's FAST half emulated on the planner's tables
-    (tests/cpp/pyrfast_fast_emu.cpp: bitmap corners, NMS per cell-column half,
-    raster emit into per-cell minThFAST / iniThFAST lists, the per-cell choice)
-    gives the oracle's vToDistributeKeys of every level key for key."""
-    exe = tmp_path / "pffe"
-    csrc = os.path.join(PKG, "csrc")
-    odir = os.path.join(ROOT, "oracle")
-    subprocess.check_call(["gcc", "-O2", "-std=c11", "-mfma", "-ffp-contract=off", "-c",
-                           os.path.join(odir, "orb_oracle.c"), "-o", str(tmp_path / "oo.o")])
-    subprocess.check_call(["g++", "-O2", "-std=c++17", "-I", csrc, "-I", odir,
-                           os.path.join(ROOT, "tests", "cpp", "pyrfast_fast_emu.cpp"),
-                           os.path.join(csrc, "geometry.cpp"), str(tmp_path / "oo.o"), "-lm", "-o", str(exe)])
-    (tmp_path / "in.raw").write_bytes(synth.frame(W, H, 7, kind).tobytes())
-    r = subprocess.run([str(exe), str(tmp_path / "in.raw"), str(W), str(H), str(nf), str(L), repr(sf),
-                        str(ini), str(mn)], capture_output=True, text=True)
-    assert r.returncode == 0 and r.stdout.startswith("ok"), r.stdout + r.stderr

@@ -6,6 +6,7 @@ appear with the same name, return type and parameter types.  Reads the
 reference headers as text; skipped where /root/reference is absent."""
 import os
 import re
+import subprocess
 
 import pytest
 
@@ -90,3 +91,82 @@ def test_descriptor_distance_signature_matches_reference():
     assert rd["DescriptorDistance"] <= md["DescriptorDistance"]
     assert rd["ORBmatcher"] <= md["ORBmatcher"]
     assert re.search(r"static int DescriptorDistance", mine)
+
+
+# ORBmatcher::SearchByBoW, both overloads (include/ORBmatcher.h:44-45).  The
+# compat header offers them as templates over the caller's KeyFrame / Frame /
+# MapPoint classes; this test instantiates both with stand-in classes named
+# and shaped as the reference's (the members the matcher reads: KeyFrame.h
+# GetMapPointMatches / mvKeysUn / mFeatVec / mDescriptors, Frame.h N /
+# mvKeys / mFeatVec / mDescriptors, MapPoint.h isBad) by binding each to a
+# member-function pointer whose parameter list is the reference's own: a
+# parameter that drifts (const, reference vs pointer, element type) fails to
+# deduce and the compile fails.  The lists come from the reference header
+# text where it is present, else from the copy below (checked against it
+# when both exist).
+_BOW_DECLS = ["int SearchByBoW(KeyFrame *pKF, Frame &F, std::vector<MapPoint*> &vpMapPointMatches);",
+              "int SearchByBoW(KeyFrame *pKF1, KeyFrame* pKF2, std::vector<MapPoint*> &vpMatches12);"]
+
+_BOW_STANDINS = r"""
+#include <map>
+#include <vector>
+#include "orbslam2_compat.hpp"
+namespace ORB_SLAM2 {
+class MapPoint { public: bool isBad() { return false; } };
+class KeyFrame {
+ public:
+  std::vector<cv::KeyPoint> mvKeysUn;
+  std::map<unsigned int, std::vector<unsigned int>> mFeatVec;  // DBoW2::FeatureVector
+  cv::Mat mDescriptors;
+  std::vector<MapPoint*> GetMapPointMatches() { return std::vector<MapPoint*>(); }
+};
+class Frame {
+ public:
+  int N = 0;
+  std::vector<cv::KeyPoint> mvKeys;
+  std::map<unsigned int, std::vector<unsigned int>> mFeatVec;
+  cv::Mat mDescriptors;
+};
+}  // namespace ORB_SLAM2
+using namespace ORB_SLAM2;
+"""
+
+
+def _bow_param_lists(decls):
+    out = []
+    for d in decls:
+        m = re.search(r"SearchByBoW\s*\(([^()]*)\)", d)
+        out.append(_params(m.group(1)))
+    return out
+
+
+def _bow_probe(tmp_path, lists):
+    src = _BOW_STANDINS
+    for i, ps in enumerate(lists):
+        src += "int (ORBmatcher::*bow%d)(%s) = &ORBmatcher::SearchByBoW;\n" % (i, ", ".join(ps))
+    p = tmp_path / "bow_sig.cpp"
+    p.write_text(src)
+    return subprocess.run(["g++", "-std=c++17", "-fsyntax-only", "-I", os.path.dirname(COMPAT),
+                           "-I", os.path.join(ROOT, "include"), str(p)], capture_output=True, text=True)
+
+
+def test_search_by_bow_overloads_bind_reference_signatures(tmp_path):
+    decls = _BOW_DECLS
+    if os.path.exists(os.path.join(REF, "ORBmatcher.h")):
+        ref = _strip(open(os.path.join(REF, "ORBmatcher.h")).read())
+        found = re.findall(r"int SearchByBoW\s*\([^()]*\)\s*;", ref)
+        assert _bow_param_lists(found) == _bow_param_lists(_BOW_DECLS), found
+        decls = found
+    lists = _bow_param_lists(decls)
+    assert [len(x) for x in lists] == [3, 3]
+    r = _bow_probe(tmp_path, lists)
+    assert r.returncode == 0, r.stderr
+
+
+def test_search_by_bow_probe_rejects_drifted_signature(tmp_path):
+    """The probe is sharp: a parameter list that differs from the reference's
+    (here the match vector by const reference) does not bind."""
+    lists = _bow_param_lists(_BOW_DECLS)
+    drift = [lists[0], (lists[1][0], lists[1][1], "const std::vector<MapPoint*>&")]
+    r = _bow_probe(tmp_path, drift)
+    assert r.returncode != 0

@@ -24,10 +24,6 @@ STAGE_OF = {
     "k_orient_brief": "orient_brief",
     "k_match_select": "match_select",
     "k_pyr_area2": "resize",
-    "k_pyr_stream_1024": "resize",
-    "k_pyr_stream_512": "resize",
-    "k_pyr_stream_256": "resize",
-    "k_pyrfast": "fast_cells",
     "k_match_setup": "match_select",
     "k_match_cand_rows": "match_candidates",
     "k_match_candidates": "match_candidates",
