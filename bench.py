@@ -81,6 +81,9 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=40.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-latency", action="store_true")
+    ap.add_argument("--brief", choices=["auto", "patch", "level"], default="auto",
+                    help="BRIEF blur form (orbx_plan_set_options; identical results): per-keypoint "
+                         "patch blur, every level blurred once, or the planner's choice")
     ap.add_argument("--pyramid", choices=["auto", "tiles"], default="auto",
                     help="pyramid kernel (orbx_plan_set_options; identical results)")
     ap.add_argument("--serial", action="store_true",
@@ -161,18 +164,28 @@ def level_pixels(geo):
     return P, uniq, alias
 
 
-def stage_bytes(geo, nframes, kps_total, npairs, topn):
-    """Algorithmic bytes per step of each stage."""
+def stage_bytes(geo, nframes, kps_total, npairs, topn, level_blur=False):
+    """Algorithmic bytes per step of each stage.
+    level_blur: the plan blurred every level once (k_blur, stage 'blur')."""
     P, uniq, alias = level_pixels(geo)
     resize = sum(P[l] + P[alias[l - 1]] for l in uniq if l > 0)
     fast = sum(P[l] for l in uniq)
-    # per keypoint: the 43x43 source patch the IC disk (r=15) and the blurred
-    # BRIEF samples (|offset| <= 13*sqrt(2), +3 blur taps) cover, + 28 B
-    # keypoint + 32 B descriptor out
-    brief = (43 * 43 + 60) * kps_total
+    if level_blur:
+        # per keypoint: the unblurred 31x31 IC disk square and the blurred
+        # 37x37 sample square (|offset| <= 18) it reads, + 28 B keypoint + 32 B
+        # descriptor out; the blur pass reads and writes every unique level
+        brief = (31 * 31 + 37 * 37 + 60) * kps_total
+    else:
+        # per keypoint: the 43x43 source patch the IC disk (r=15) and the blurred
+        # BRIEF samples (|offset| <= 13*sqrt(2), +3 blur taps) cover, + 28 B
+        # keypoint + 32 B descriptor out
+        brief = (43 * 43 + 60) * kps_total
     match = npairs * (2 * topn * 32 + topn * 8)
-    return {"resize": resize * nframes, "fast_cells": fast * nframes,
-            "orient_brief": brief, "match_candidates": match}
+    out = {"resize": resize * nframes, "fast_cells": fast * nframes,
+           "orient_brief": brief, "match_candidates": match}
+    if level_blur:
+        out["blur"] = 2 * fast * nframes
+    return out
 
 
 def min_pyr_fast_bytes(geo, nframes):
@@ -595,7 +608,7 @@ def main_mono(args, wl):
     B, W, H = args.batch, wl["W"], wl["H"]
     prm = orbx.params(wl["nfeatures"], 1.2, wl["nlevels"], 20, 7, wl["guard"])
     plan = orbx.Plan(prm, W, H, B, device=local)
-    plan.set_options(pyramid=args.pyramid)
+    plan.set_options(pyramid=args.pyramid, brief=args.brief)
     kcap = plan.kcap
     match = wl["match"]
     mp = orbx.MatchPlan(B, kcap, wl["topn"], device=local, zero_tail=True) if match else None
@@ -641,7 +654,7 @@ def main_mono(args, wl):
         sub = B // S
         subplans = [plan] if S == 1 else [orbx.Plan(prm, W, H, sub, device=local) for _ in range(S)]
         for p_ in subplans:
-            p_.set_options(pyramid=args.pyramid)
+            p_.set_options(pyramid=args.pyramid, brief=args.brief)
         # the pipeline's streams are created back to back, after every plan
         # (each plan creates a stream of its own): HIP hands out its hardware
         # queues (GPU_MAX_HW_QUEUES, 4 on the box) in creation order, and
@@ -762,7 +775,7 @@ def main_mono(args, wl):
             dist.destroy_process_group()
         return
     geo = plan.geo
-    by = stage_bytes(geo, B, kps_total, B, wl["topn"])
+    by = stage_bytes(geo, B, kps_total, B, wl["topn"], level_blur=st.get("blur", (0, 0))[1] > 0)
     traffic = load_traffic(args.traffic)
     per_step, roof, pf = roofline_entries(st, args.steps, by, geo, B, traffic)
     unit = "frames/s"
@@ -824,8 +837,8 @@ def main_c5(args, wl):
     prm = orbx.params(wl["nfeatures"], 1.2, wl["nlevels"], 20, 7)
     pl = orbx.Plan(prm, W, H, B, device=local)
     pr = orbx.Plan(prm, W, H, B, device=local)
-    pl.set_options(pyramid=args.pyramid)
-    pr.set_options(pyramid=args.pyramid)
+    pl.set_options(pyramid=args.pyramid, brief=args.brief)
+    pr.set_options(pyramid=args.pyramid, brief=args.brief)
     sp = orbx.StereoPlan(pl, device=local)
     kcap = pl.kcap
     mp = orbx.MatchPlan(B, kcap, wl["topn"], device=local, zero_tail=True)
@@ -881,8 +894,8 @@ def main_c5(args, wl):
             subs = []
             for _ in range(S):
                 a_, b_ = orbx.Plan(prm, W, H, sub, device=local), orbx.Plan(prm, W, H, sub, device=local)
-                a_.set_options(pyramid=args.pyramid)
-                b_.set_options(pyramid=args.pyramid)
+                a_.set_options(pyramid=args.pyramid, brief=args.brief)
+                b_.set_options(pyramid=args.pyramid, brief=args.brief)
                 subs.append((a_, b_, orbx.StereoPlan(a_, device=local)))
         sa = torch.cuda.Stream(device=dev)  # back to back, after every plan (main_mono)
         sb = torch.cuda.Stream(device=dev, priority=-1)
@@ -993,7 +1006,7 @@ def main_c5(args, wl):
         if world > 1:
             dist.destroy_process_group()
         return
-    by = stage_bytes(pl.geo, 2 * B, kps_total, B, wl["topn"])
+    by = stage_bytes(pl.geo, 2 * B, kps_total, B, wl["topn"], level_blur=st.get("blur", (0, 0))[1] > 0)
     traffic = load_traffic(args.traffic)
     per_step, roof, pf = roofline_entries(st, args.steps, by, pl.geo, 2 * B, traffic)
     out = {

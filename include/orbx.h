@@ -180,14 +180,23 @@ int orbx_plan_check(orbx_plan* plan, void* stream);
  * capacity so the scan runs on ordinary frames. */
 int orbx_plan_debug_counters(orbx_plan* plan, int* fast_overflow_strips);
 
-/* Kernel-path options of a plan (default 0 = automatic; persistent).
- *   ORBX_PLAN_PYR_TILES   the pyramid by k_pyramid (2-D tiles of the level
- *                         chain, halo recompute) for every batch size.
- * Automatic (0) is the same path today.  The round-4 row-streaming pyramid
- * and fused pyramid + FAST kernels (flags 2 and 4) measured 1.1x / 2.6x the
- * tile path's time and were retired; their flags, like
- * any other unknown bit, now return ORBX_ERR_ARG (options unchanged). */
+/* Kernel-path options of a plan (default 0 = automatic; persistent).  Every
+ * path gives bit-identical results; they differ in speed only.
+ *   ORBX_PLAN_PYR_TILES    the pyramid by k_pyramid (2-D tiles of the level
+ *                          chain, halo recompute) -- the one pyramid path;
+ *   ORBX_PLAN_BRIEF_PATCH  descriptors blur each keypoint's 43 x 48 patch
+ *                          (k_orient_brief);
+ *   ORBX_PLAN_BRIEF_LEVEL  every unique level is blurred once (k_blur) and
+ *                          the descriptors sample it (k_orient_brief_lb).
+ * Automatic (0): the tile pyramid, and the level blur when nfeatures x 43 x
+ * 48 exceeds ORBX_LB_RATIO x the unique level pixels.
+ * The round-4 row-streaming pyramid and fused pyramid + FAST kernels (flags
+ * 2 and 4) measured 1.1x / 2.6x the tile path's time and were retired; their
+ * flags, like any other unknown bit or both BRIEF flags at once, return
+ * ORBX_ERR_ARG (options unchanged). */
 #define ORBX_PLAN_PYR_TILES 1
+#define ORBX_PLAN_BRIEF_PATCH 8
+#define ORBX_PLAN_BRIEF_LEVEL 16
 int orbx_plan_set_options(orbx_plan* plan, int flags);
 
 /* mvImagePyramid[level] of frame `frame` of the last orbx_plan_extract on
@@ -248,6 +257,21 @@ typedef struct {
  * Synchronous. */
 int orbm_search_by_bow(const orbx_bow_frame* kf1, const orbx_bow_frame* kf2, float nnratio,
                        int check_ori, int device, int32_t* match12, int* nmatches);
+
+/* SearchByBoW(KeyFrame*, Frame&, vector<MapPoint*>&) in upstream ORB-SLAM2's
+ * form (SURVEY.md §5 switch bow_kf_frame=full; this reference ships only the
+ * stub of src/ORBmatcher.cc:88-119, which the compat header keeps as the
+ * default).  kf: the KeyFrame (valid[i] = its MapPoint i is non-null and not
+ * bad, angles of mvKeysUn); frame: the Frame (mvKeys angles; its valid is
+ * ignored: every Frame feature is a candidate).  Per KF row in node order:
+ * best / second over the node's unclaimed Frame features, accepted when
+ * best <= TH_LOW (50) and best < nnratio * second; the rotation check as the
+ * KF-KF form.  match_f[frame->n] = the KF feature whose MapPoint the Frame
+ * feature received (vpMapPointMatches[i] = vpMapPointsKF[match_f[i]]), -1 for
+ * none (vpMapPointMatches starts as F.N nulls).  Synchronous.
+ * ORBX_ERR_UNSUPPORTED for nnratio <= 50/256 (no second-best could pass). */
+int orbm_search_by_bow_kf_frame(const orbx_bow_frame* kf, const orbx_bow_frame* frame, float nnratio,
+                                int check_ori, int device, int32_t* match_f, int* nmatches);
 
 /* ORBmatcher::DescriptorDistance (src/ORBmatcher.cc:896-908), batched on the
  * device: dist[i] = Hamming(a + 32*ia[i], b + 32*ib[i]); host pointers. */

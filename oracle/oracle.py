@@ -56,6 +56,7 @@ def lib():
         L.oo_brief_descriptor.argtypes = [P, i, i, i, f, P]
         L.oo_descriptor_distance.argtypes = [P, P]
         L.oo_search_by_bow.argtypes = [i, P, P, P, i, P, P, P, i, P, P, P, i, P, P, P, f, i, P]
+        L.oo_search_by_bow_kf_frame.argtypes = [i, P, P, P, i, P, P, P, i, P, P, i, P, P, P, f, i, P]
         L.oo_vocab_from_records.restype = P
         L.oo_vocab_from_records.argtypes = [i, i, i, i, i, P, P, P, P]
         L.oo_vocab_destroy.argtypes = [P]
@@ -216,6 +217,25 @@ def search_by_bow(kf1, kf2, nnratio=0.6, check_ori=True):
                                 len(d2), _p(d2), _p(a2), _p(v2), len(n2), _p(n2), _p(o2), _p(f2),
                                 float(nnratio), 1 if check_ori else 0, _p(m))
     return m, nm
+
+
+def search_by_bow_kf_frame(kf, fr, nnratio=0.6, check_ori=True):
+    """Upstream ORB-SLAM2's SearchByBoW(KeyFrame*, Frame&) (the reference
+    ships a stub, src/ORBmatcher.cc:88-119): kf / fr as search_by_bow's
+    dicts (fr's valid is not used).  Returns (match_f int32[F.N]: KF index
+    whose MapPoint Frame feature j received, -1 = none; nmatches)."""
+    d1 = np.ascontiguousarray(kf["desc"], np.uint8)
+    a1 = np.ascontiguousarray(kf["angle"], np.float32)
+    v1 = None if kf.get("valid") is None else np.ascontiguousarray(kf["valid"], np.uint8)
+    n1, o1, f1 = (np.ascontiguousarray(kf[k], np.uint32) for k in ("node_id", "off", "feat"))
+    d2 = np.ascontiguousarray(fr["desc"], np.uint8)
+    a2 = np.ascontiguousarray(fr["angle"], np.float32)
+    n2, o2, f2 = (np.ascontiguousarray(fr[k], np.uint32) for k in ("node_id", "off", "feat"))
+    m = np.full(max(len(d2), 1), -1, np.int32)
+    nm = lib().oo_search_by_bow_kf_frame(len(d1), _p(d1), _p(a1), _p(v1), len(n1), _p(n1), _p(o1), _p(f1),
+                                         len(d2), _p(d2), _p(a2), len(n2), _p(n2), _p(o2), _p(f2),
+                                         float(nnratio), 1 if check_ori else 0, _p(m))
+    return m[:len(d2)].copy(), nm
 
 
 def compute_stereo_matches(kl, dl, kr, dr, scale, inv_scale, lpyr, rpyr, mb, mbf):

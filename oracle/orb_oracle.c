@@ -952,6 +952,97 @@ int oo_search_by_bow(int n1, const uint8_t* desc1, const float* angle1, const ui
   return nmatches;
 }
 
+/* SearchByBoW(KeyFrame* pKF, Frame& F, vector<MapPoint*>& vpMapPointMatches)
+ * in upstream ORB-SLAM2's form (raulmur/ORB_SLAM2 src/ORBmatcher.cc,
+ * SearchByBoW(KeyFrame*, Frame&, ...)); this reference keeps only the stub
+ * (src/ORBmatcher.cc:88-119: F.N nulls, returns 0).  SURVEY.md §5 switch
+ * bow_kf_frame=full.  Restated from the published algorithm:
+ *   vpMapPointMatches = vector(F.N, NULL); merge-join of pKF->mFeatVec and
+ *   F.mFeatVec on NodeId (lower_bound jumps); per KF index in node order with
+ *   a non-null, non-bad MapPoint: bestDist1 = bestDist2 = 256, over the
+ *   node's Frame indices whose vpMapPointMatches entry is still NULL,
+ *   dist < bestDist1 -> (bestDist2, bestDist1, bestIdxF) = (bestDist1, dist,
+ *   idx), else dist < bestDist2 -> bestDist2 = dist; accept when bestDist1
+ *   <= TH_LOW and (float)bestDist1 < mfNNratio * (float)bestDist2:
+ *   vpMapPointMatches[bestIdxF] = pMP, rotation rot = kp(KF mvKeysUn).angle -
+ *   F.mvKeys[bestIdxF].angle (+360 if < 0), bin = round(rot / 30) (30 -> 0),
+ *   rotHist[bin] += bestIdxF; afterwards the bins outside ComputeThreeMaxima's
+ *   three reset their entries to NULL (nmatches--).
+ * Here: valid_kf[i] = the KF's MapPoint i is non-null and not bad;
+ * match_f[F.N] = KF index whose MapPoint Frame feature j received, -1 = NULL. */
+int oo_search_by_bow_kf_frame(int nk, const uint8_t* desc_k, const float* angle_k,
+                              const uint8_t* valid_k, int nnode_k, const uint32_t* node_id_k,
+                              const uint32_t* off_k, const uint32_t* feat_k, int nf,
+                              const uint8_t* desc_f, const float* angle_f, int nnode_f,
+                              const uint32_t* node_id_f, const uint32_t* off_f, const uint32_t* feat_f,
+                              float nnratio, int check_ori, int32_t* match_f) {
+  for (int j = 0; j < nf; ++j) match_f[j] = -1;
+  int* rot_idx = (int*)malloc(sizeof(int) * (size_t)(nf > 0 ? nf : 1));
+  int* rot_bin = (int*)malloc(sizeof(int) * (size_t)(nf > 0 ? nf : 1));
+  int nrot = 0, nmatches = 0;
+  const float factor = 1.0f / HISTO_LENGTH;
+  int kit = 0, fit = 0;
+  while (kit < nnode_k && fit < nnode_f) {
+    if (node_id_k[kit] == node_id_f[fit]) {
+      for (uint32_t a = off_k[kit]; a < off_k[kit + 1]; ++a) {
+        const int realIdxKF = (int)feat_k[a];
+        if (valid_k && !valid_k[realIdxKF]) continue; /* !pMP || pMP->isBad() */
+        const uint8_t* dKF = desc_k + (size_t)realIdxKF * 32;
+        int bestDist1 = 256, bestIdxF = -1, bestDist2 = 256;
+        for (uint32_t b = off_f[fit]; b < off_f[fit + 1]; ++b) {
+          const int realIdxF = (int)feat_f[b];
+          if (match_f[realIdxF] >= 0) continue; /* vpMapPointMatches[realIdxF] set */
+          const int dist = oo_descriptor_distance(dKF, desc_f + (size_t)realIdxF * 32);
+          if (dist < bestDist1) {
+            bestDist2 = bestDist1;
+            bestDist1 = dist;
+            bestIdxF = realIdxF;
+          } else if (dist < bestDist2) {
+            bestDist2 = dist;
+          }
+        }
+        if (bestDist1 <= TH_LOW && (float)bestDist1 < nnratio * (float)bestDist2) {
+          match_f[bestIdxF] = realIdxKF;
+          if (check_ori) {
+            float rot = angle_k[realIdxKF] - angle_f[bestIdxF];
+            if (rot < 0.0f) rot += 360.0f;
+            int bin = (int)roundf(rot * factor);
+            if (bin == HISTO_LENGTH) bin = 0;
+            rot_idx[nrot] = bestIdxF;
+            rot_bin[nrot] = bin;
+            ++nrot;
+          }
+          nmatches++;
+        }
+      }
+      ++kit;
+      ++fit;
+    } else if (node_id_k[kit] < node_id_f[fit]) {
+      kit = lower_bound_u32(node_id_k, nnode_k, kit, node_id_f[fit]);
+    } else {
+      fit = lower_bound_u32(node_id_f, nnode_f, fit, node_id_k[kit]);
+    }
+  }
+  if (check_ori) {
+    int sizes[HISTO_LENGTH];
+    memset(sizes, 0, sizeof(sizes));
+    for (int i = 0; i < nrot; ++i) sizes[rot_bin[i]]++;
+    int ind1 = -1, ind2 = -1, ind3 = -1;
+    compute_three_maxima(sizes, HISTO_LENGTH, &ind1, &ind2, &ind3);
+    for (int bin = 0; bin < HISTO_LENGTH; ++bin) {
+      if (bin == ind1 || bin == ind2 || bin == ind3) continue;
+      for (int i = 0; i < nrot; ++i)
+        if (rot_bin[i] == bin) {
+          match_f[rot_idx[i]] = -1;
+          nmatches--;
+        }
+    }
+  }
+  free(rot_idx);
+  free(rot_bin);
+  return nmatches;
+}
+
 /* ---------- Frame::ComputeStereoMatches (src/Frame.cc:446-620) ------------ */
 #define TH_HIGH 100
 

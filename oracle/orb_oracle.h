@@ -95,6 +95,14 @@ int oo_search_by_bow(int n1, const uint8_t* desc1, const float* angle1, const ui
                      const uint8_t* valid2, int nnode2, const uint32_t* node_id2,
                      const uint32_t* off2, const uint32_t* feat2, float nnratio, int check_ori,
                      int32_t* match12);
+/* upstream ORB-SLAM2's SearchByBoW(KeyFrame*, Frame&) (the reference ships a
+ * stub, src/ORBmatcher.cc:88-119); match_f[nf]: KF index or -1 */
+int oo_search_by_bow_kf_frame(int nk, const uint8_t* desc_k, const float* angle_k,
+                              const uint8_t* valid_k, int nnode_k, const uint32_t* node_id_k,
+                              const uint32_t* off_k, const uint32_t* feat_k, int nf,
+                              const uint8_t* desc_f, const float* angle_f, int nnode_f,
+                              const uint32_t* node_id_f, const uint32_t* off_f, const uint32_t* feat_f,
+                              float nnratio, int check_ori, int32_t* match_f);
 
 /* Frame::ComputeStereoMatches (src/Frame.cc:446-620).  Left/right keypoints
  * and descriptors of one rectified pair; lpyr/rpyr[l] = mvImagePyramid[l] of

@@ -333,11 +333,32 @@ class ORBmatcher {
   }
 
   // SearchByBoW(KeyFrame*, Frame&, vector<MapPoint*>&) (:88-119) is a stub
-  // in the reference: F.N null matches, returns 0.  Kept as is.
+  // in the reference: F.N null matches, returns 0.  That stays the default
+  // (SURVEY.md §5 switch bow_kf_frame=stub); SetBowKFFrame(BowKFFrame::Full)
+  // selects upstream ORB-SLAM2's search on the device
+  // (orbm_search_by_bow_kf_frame): KF MapPoints matched to the Frame's
+  // features over common vocabulary nodes.  FR: the reference's Frame (N,
+  // mvKeys, mFeatVec after ComputeBoW, mDescriptors).
+  enum class BowKFFrame { Stub, Full };
+  void SetBowKFFrame(BowKFFrame m) { mBowKFFrame = m; }
   template <class KF, class FR, class MP>
-  int SearchByBoW(KF* /*pKF*/, FR& F, std::vector<MP*>& vpMapPointMatches) {
-    vpMapPointMatches.resize(F.N, static_cast<MP*>(nullptr));  // :90
-    return 0;
+  int SearchByBoW(KF* pKF, FR& F, std::vector<MP*>& vpMapPointMatches) {
+    if (mBowKFFrame == BowKFFrame::Stub) {
+      vpMapPointMatches.resize(F.N, static_cast<MP*>(nullptr));  // :90
+      return 0;
+    }
+    const std::vector<MP*> vpMapPointsKF = pKF->GetMapPointMatches();
+    Flat fk, ff;
+    flatten(pKF, vpMapPointsKF, fk);
+    flatten_frame(F, ff);
+    std::vector<int32_t> mf(F.N > 0 ? (size_t)F.N : 1, -1);
+    int n = 0;
+    orbx_throw(orbm_search_by_bow_kf_frame(&fk.f, &ff.f, mfNNratio, mbCheckOrientation ? 1 : 0, 0, mf.data(), &n),
+               "SearchByBoW");
+    vpMapPointMatches.assign(F.N, static_cast<MP*>(nullptr));  // upstream: vector<MapPoint*>(F.N, NULL)
+    for (int i = 0; i < F.N; ++i)
+      if (mf[i] >= 0) vpMapPointMatches[i] = vpMapPointsKF[mf[i]];
+    return n;
   }
 
  protected:
@@ -369,8 +390,29 @@ class ORBmatcher {
     o.f.feat = o.feat.data();
   }
 
+  template <class FR>
+  static void flatten_frame(FR& F, Flat& o) {
+    o.angle.resize(F.mvKeys.size());
+    for (size_t i = 0; i < F.mvKeys.size(); ++i) o.angle[i] = F.mvKeys[i].angle;
+    o.off.push_back(0);
+    for (const auto& node : F.mFeatVec) {  // std::map: ascending NodeId
+      o.ids.push_back(node.first);
+      o.feat.insert(o.feat.end(), node.second.begin(), node.second.end());
+      o.off.push_back((uint32_t)o.feat.size());
+    }
+    o.f.n = F.N;
+    o.f.desc = F.mDescriptors.data;
+    o.f.angle = o.angle.data();
+    o.f.valid = nullptr;
+    o.f.nnodes = (int)o.ids.size();
+    o.f.node_id = o.ids.data();
+    o.f.node_off = o.off.data();
+    o.f.feat = o.feat.data();
+  }
+
   float mfNNratio;
   bool mbCheckOrientation;
+  BowKFFrame mBowKFFrame = BowKFFrame::Stub;
 };
 
 }  // namespace ORB_SLAM2

@@ -33,6 +33,11 @@ __global__ void k_quadtree_j6(const LevelInfo*, const CellInfo*, const uint32_t*
 __global__ void k_orient_brief(const uint8_t*, size_t, size_t, const uint8_t*, size_t,
                                const BriefArgs, const uint32_t*, size_t, const int*,
                                orbx_keypoint*, uint8_t*, int*, const uint32_t*, int);
+__global__ void k_orient_brief_lb(const uint8_t*, size_t, size_t, const uint8_t*, size_t,
+                                  const BriefArgs, const uint32_t*, size_t, const int*,
+                                  orbx_keypoint*, uint8_t*, int*, const uint32_t*, int,
+                                  const uint8_t*, size_t);
+__global__ void k_blur(const uint8_t*, size_t, size_t, const uint8_t*, size_t, uint8_t*, size_t, const BlurArgs);
 __global__ void k_synth(uint8_t*, int, int, size_t, int, int);
 __global__ void k_selftest_sincos(const float*, int, float*);
 __global__ void k_selftest_sincos_range(uint32_t, int, float*);
@@ -227,6 +232,33 @@ extern "C" int orbx_plan_create(const orbx_params* prm, int width, int height, i
     p->bargs.pyr_off[l] = lv.pyr_off;
     p->bargs.scale[l] = lv.scale;
     p->bargs.patch[l] = lv.patch_size;
+    p->bargs.bpitch[l] = lv.bpitch;
+    p->bargs.blur_off[l] = lv.blur_off;
+  }
+  // level-blur mode (k_blur + k_orient_brief_lb): blur every unique level
+  // once when the keypoints' per-keypoint patches (43 x 48 px each) would
+  // cover clearly more pixels than the levels hold (c1 /
+  // c2 / c5 blur their levels, c4's 1080p levels keep the per-keypoint blur)
+  {
+    memset(&p->blargs, 0, sizeof(p->blargs));
+    int nt = 0;
+    for (int l = 0; l < P.params.nlevels; ++l) {
+      const LevelInfo& lv = P.levels[l];
+      if (lv.unique != l) continue;
+      const int i = p->blargs.nu++;
+      p->blargs.tile_begin[i] = nt;
+      p->blargs.tiles_x[i] = (lv.w + ORBX_LB_TW - 1) / ORBX_LB_TW;
+      nt += p->blargs.tiles_x[i] * ((lv.h + ORBX_LB_TH - 1) / ORBX_LB_TH);
+      p->blargs.w[i] = lv.w;
+      p->blargs.h[i] = lv.h;
+      p->blargs.pitch[i] = lv.pitch;
+      p->blargs.src_off[i] = l == 0 ? -1 : lv.pyr_off;
+      p->blargs.bpitch[i] = lv.bpitch;
+      p->blargs.blur_off[i] = lv.blur_off;
+    }
+    p->blargs.tile_begin[p->blargs.nu] = nt;
+    const double patch_px = (double)P.params.nfeatures * (KP_PATCH_ROWS * KP_PATCH_COLS);
+    p->lb_auto = patch_px > ORBX_LB_RATIO * (double)P.geo.pixels ? 1 : 0;
   }
   // FAST strip LDS: tile + strength map + row masks + counts
   {
@@ -257,6 +289,10 @@ extern "C" int orbx_plan_create(const orbx_params* prm, int width, int height, i
   }
   p->pyr_stride = round_up((size_t)P.pyr_bytes, 256);
   p->blur_stride = round_up((size_t)P.blur_bytes, 256);
+  if (p->lb_auto && dev_alloc((void**)&p->d_blur, (size_t)max_batch * p->blur_stride)) {
+    plan_free(p);
+    return ORBX_ERR_HIP;
+  }
   p->slot_stride = round_up((size_t)P.nslots, 64);
   p->qk_stride = round_up((size_t)P.qk_elems, 64);
   p->qout_stride = round_up((size_t)P.kcap, 64);
@@ -364,6 +400,16 @@ static int extract_pass(orbx_plan* p, const uint8_t* frames, int n, size_t fstri
   }
   p->timer.end(ORBX_STAGE_FAST, s);
   if (p->dbg && p->dbg < 20) return ORBX_OK; /* phase probe: later stages would read partial results */
+  // level-blur mode: the 7x7 Gaussian of every unique level (the stage runs
+  // beside nothing: it reads the levels the pyramid wrote and the BRIEF
+  // kernel reads its output)
+  uint8_t* const d_blur = p->uses_lb() ? p->d_blur + f0 * p->blur_stride : nullptr;
+  if (d_blur) {
+    p->timer.begin(ORBX_STAGE_BLUR, s);
+    hipLaunchKernelGGL(k_blur, dim3((unsigned)p->blargs.tile_begin[p->blargs.nu], n), dim3(256), 0, s, frames,
+                       fstride, rstride, d_pyr, p->pyr_stride, d_blur, p->blur_stride, p->blargs);
+    p->timer.end(ORBX_STAGE_BLUR, s);
+  }
   // K3 DistributeOctTree
   p->timer.begin(ORBX_STAGE_QUADTREE, s);
   // keys per thread in registers: 8 for 1080p-class level 0, else 6 (qt_body)
@@ -392,10 +438,17 @@ static int extract_pass(orbx_plan* p, const uint8_t* frames, int n, size_t fstri
   const int ob_kpw = (long long)P.levels[0].w * P.levels[0].h >= (1 << 20) ? 6 : 12;
   int ob_waves = std::min(ob_full, std::max((ob_full + ob_kpw - 1) / ob_kpw, (16384 + n - 1) / n));
   if (p->ob_div > 0) ob_waves = std::max(4, ob_full / p->ob_div); /* profiling only */
-  hipLaunchKernelGGL(k_orient_brief, dim3((ob_waves + 3) / 4, n),
-                     dim3(256), 0, s, frames, fstride, rstride, d_pyr, p->pyr_stride, p->bargs,
-                     d_qout, p->qout_stride, d_lcount, kps, desc,
-                     counts, p->d_qperm + f0 * p->qout_stride, p->dbg);
+  if (p->uses_lb()) {
+    hipLaunchKernelGGL(k_orient_brief_lb, dim3((ob_waves + 3) / 4, n),
+                       dim3(256), 0, s, frames, fstride, rstride, d_pyr, p->pyr_stride, p->bargs,
+                       d_qout, p->qout_stride, d_lcount, kps, desc,
+                       counts, p->d_qperm + f0 * p->qout_stride, p->dbg, d_blur, p->blur_stride);
+  } else {
+    hipLaunchKernelGGL(k_orient_brief, dim3((ob_waves + 3) / 4, n),
+                       dim3(256), 0, s, frames, fstride, rstride, d_pyr, p->pyr_stride, p->bargs,
+                       d_qout, p->qout_stride, d_lcount, kps, desc,
+                       counts, p->d_qperm + f0 * p->qout_stride, p->dbg);
+  }
   p->timer.end(ORBX_STAGE_BRIEF, s);
   if (hipGetLastError() != hipSuccess) return ORBX_ERR_HIP;
   return ORBX_OK;
@@ -446,7 +499,14 @@ extern "C" int orbx_plan_check(orbx_plan* p, void* stream) {
 }
 
 extern "C" int orbx_plan_set_options(orbx_plan* p, int flags) {
-  if (!p || (flags & ~ORBX_PLAN_PYR_TILES)) return ORBX_ERR_ARG;
+  if (!p || (flags & ~(ORBX_PLAN_PYR_TILES | ORBX_PLAN_BRIEF_PATCH | ORBX_PLAN_BRIEF_LEVEL)) ||
+      (flags & (ORBX_PLAN_BRIEF_PATCH | ORBX_PLAN_BRIEF_LEVEL)) == (ORBX_PLAN_BRIEF_PATCH | ORBX_PLAN_BRIEF_LEVEL))
+    return ORBX_ERR_ARG;
+  if ((flags & ORBX_PLAN_BRIEF_LEVEL) && !p->d_blur) {
+    ORBX_TRY(hipSetDevice(p->device));
+    ORBX_TRY(hipStreamSynchronize(p->stream));
+    if (dev_alloc((void**)&p->d_blur, (size_t)p->max_batch * p->blur_stride)) return ORBX_ERR_HIP;
+  }
   p->options = flags;
   return ORBX_OK;
 }

@@ -156,9 +156,11 @@ void launch_match(const MProblem* d_probs, int nprob, const MNodePair* d_nps, in
 
 }  // namespace
 
-extern "C" int orbm_search_by_bow(const orbx_bow_frame* kf1, const orbx_bow_frame* kf2,
-                                  float nnratio, int check_ori, int device, int32_t* match12,
-                                  int* nmatches) {
+// the KF-KF search (th_low = ORBM_TH_LOW) or upstream's KF-Frame search
+// (th_low = ORBM_TH_LOW + 1, i.e. bestDist1 <= TH_LOW) of kf1's rows over
+// kf2's candidates: match12 indexed by kf1 feature
+static int bow_search(const orbx_bow_frame* kf1, const orbx_bow_frame* kf2, float nnratio,
+                      int check_ori, int device, int th_low, int32_t* match12, int* nmatches) {
   if (!nmatches || (kf1 && kf1->n > 0 && !match12)) return ORBX_ERR_ARG;
   int rc = check_frame(kf1);
   if (rc) return rc;
@@ -274,8 +276,8 @@ extern "C" int orbm_search_by_bow(const orbx_bow_frame* kf1, const orbx_bow_fram
   P.check_ori = check_ori ? 1 : 0;
   P.nnratio = nnratio;
   P.sequential = sequential;
-  P.dcap = orbm_dcap(nnratio);
-  P.pad = 0;
+  P.dcap = orbm_dcap(nnratio, th_low);
+  P.th_low = th_low;
   memcpy(h + o_prob, &P, sizeof(P));
   if (nnp) memcpy(h + o_nps, nps.data(), nnp * sizeof(MNodePair));
   memset(h + o_loff, 0, sizeof(int));
@@ -293,6 +295,36 @@ extern "C" int orbm_search_by_bow(const orbx_bow_frame* kf1, const orbx_bow_fram
   ORBX_TRY(stream_wait(s));
   memcpy(match12, h + o_m12, n1 * 4);
   memcpy(nmatches, h + o_nm, sizeof(int));
+  return ORBX_OK;
+}
+
+extern "C" int orbm_search_by_bow(const orbx_bow_frame* kf1, const orbx_bow_frame* kf2,
+                                  float nnratio, int check_ori, int device, int32_t* match12,
+                                  int* nmatches) {
+  return bow_search(kf1, kf2, nnratio, check_ori, device, ORBM_TH_LOW, match12, nmatches);
+}
+
+// upstream ORB-SLAM2's SearchByBoW(KeyFrame*, Frame&, vector<MapPoint*>&)
+// (this reference keeps only its stub, ORBmatcher.cc:88-119): the KF's
+// features are the rows (valid = a non-null, non-bad MapPoint), the Frame's
+// every feature a candidate, a claimed Frame feature is skipped, bestDist1 <=
+// TH_LOW; output indexed by Frame feature.  The same device search with
+// th_low = TH_LOW + 1, its row -> candidate result inverted here.
+extern "C" int orbm_search_by_bow_kf_frame(const orbx_bow_frame* kf, const orbx_bow_frame* frame,
+                                           float nnratio, int check_ori, int device, int32_t* match_f,
+                                           int* nmatches) {
+  if (!nmatches || !frame || (frame->n > 0 && !match_f)) return ORBX_ERR_ARG;
+  /* the sentinel scheme assumes a second-best of 256 (upstream's initial
+   * bestDist2) passes the ratio test for every acceptable best */
+  if (orbm_dcap(nnratio, ORBM_TH_LOW + 1) > 256) return ORBX_ERR_UNSUPPORTED;
+  orbx_bow_frame fr = *frame;
+  fr.valid = nullptr;  /* every Frame feature is a candidate */
+  std::vector<int32_t> m(kf && kf->n > 0 ? (size_t)kf->n : 1, -1);
+  const int rc = bow_search(kf, &fr, nnratio, check_ori, device, ORBM_TH_LOW + 1, m.data(), nmatches);
+  if (rc) return rc;
+  for (int i = 0; i < frame->n; ++i) match_f[i] = -1;
+  for (int i = 0; kf && i < kf->n; ++i)
+    if (m[i] >= 0) match_f[m[i]] = i;
   return ORBX_OK;
 }
 
@@ -368,7 +400,7 @@ __global__ void k_match_setup(MProblem* probs, MNodePair* nps, int npairs,
   P.nnratio = nnratio;
   P.sequential = 0;
   P.dcap = orbm_dcap(nnratio);
-  P.pad = 0;
+  P.th_low = ORBM_TH_LOW;
   probs[p] = P;
   MNodePair NP;
   NP.prob = p;

@@ -430,12 +430,14 @@ int plan_geometry(const orbx_params& p, int width, int height, Plan& P) {
       lv.pyr_off = (l == 0) ? -1 : pyr;
       if (l > 0) pyr += (long long)pitch_of(lv.w) * lv.h;
       lv.blur_off = blur;
+      lv.bpitch = pitch_of(lv.w);
       blur += (long long)pitch_of(lv.w) * lv.h;
     } else {
       const LevelInfo& u = P.levels[lv.unique];
       lv.pitch = u.pitch;
       lv.pyr_off = u.pyr_off;
       lv.blur_off = u.blur_off;
+      lv.bpitch = u.bpitch;
     }
     lv.scale = P.tables.scale[l];
     lv.patch_size = (int)(31 * P.tables.scale[l]); /* :345 int scaledPatchSize = 31 * float */

@@ -1423,9 +1423,125 @@ __device__ constexpr uint32_t kb_w(int m, int d) {
   }
   return w;
 }
+// ---------------------------------------------------------------------------
+// k_blur: GaussianBlur(clone(level), 7x7, 2, 2, BORDER_REFLECT_101)
+// (ORBextractor.cc:478-479) of every unique level, materialised once per
+// frame for the level-blur BRIEF (k_orient_brief_lb).  OpenCV's 8U
+// fixed-point path: H = sum_i k_i p (exact u16), out =
+// (sum_j k_j H_j + 32768) >> 16, reflect-101 in both passes.
+// Column walk, no LDS: a wave owns 62 dword columns (lanes 1..62; lanes 0 /
+// 63 only hold the neighbouring dwords) x LB_R rows.  Each lane loads its
+// dword of the LB_R + 6 rows (one coalesced 256-B row segment per load, all
+// in flight), takes the neighbours' dwords by DPP, forms the horizontal sums
+// of its 4 pixels (3 v_dot4 each) and the vertical sums from row pairs
+// packed as u16 x 2 (3 v_dot2 + 1 v_mad_u24 per pixel).  Dwords not wholly
+// inside the level (its first and last columns, the halo) are assembled
+// from reflected bytes.
+// ---------------------------------------------------------------------------
+#define KV_PAIR(a, b) ((uint32_t)(a) | ((uint32_t)(b) << 16))
+#define LB_R 32                 /* output rows per wave */
+#define LB_WC 62                /* dword columns per wave */
+static_assert(ORBX_LB_TW == 4 * LB_WC && ORBX_LB_TH == 4 * LB_R,
+              "tile = one wave's 62 dword columns x 4 waves of LB_R rows");
+__global__ __launch_bounds__(256) void k_blur(const uint8_t* __restrict__ frames, size_t fstride,
+                                              size_t rstride, const uint8_t* __restrict__ pyr,
+                                              size_t pstride, uint8_t* __restrict__ blur, size_t bstride,
+                                              const BlurArgs B) {
+  const int t = (int)blockIdx.x, f = (int)blockIdx.y;
+  const int lane = (int)threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+  int i = 0;
+  while (i + 1 < B.nu && t >= B.tile_begin[i + 1]) ++i;  // wave-uniform
+  const int W = B.w[i], H = B.h[i];
+  const int lt = t - B.tile_begin[i];
+  const int ty = lt / B.tiles_x[i], tx = lt - ty * B.tiles_x[i];
+  const int y0 = ty * ORBX_LB_TH + wave * LB_R;
+  if (y0 >= H) return;  // wave-uniform; no barrier in this kernel
+  // dword columns gc0 .. gc0 + 61 (the last tile column is moved left so
+  // that it ends at the level's last dword: its reflected bytes then always
+  // come from lanes of this wave; columns two tiles share are computed twice,
+  // identically)
+  const int nd = (W + 3) >> 2;
+  const int gc0 = min(tx * LB_WC, max(nd - LB_WC, 0));
+  const int gc = gc0 + lane - 1;  // this lane's dword column (halo lanes 0 / 63)
+  const int x = 4 * gc;
+  const bool l0 = B.src_off[i] < 0;
+  const uint8_t* src = l0 ? frames + (size_t)f * fstride : pyr + (size_t)f * pstride + B.src_off[i];
+  const uint32_t sp = l0 ? (uint32_t)rstride : (uint32_t)B.pitch[i];
+  // every lane loads a dword (all loads issued before the first use); a wave
+  // with a lane not wholly inside the level (the first and last tile
+  // columns) loads at clamped columns and then rebuilds every lane's dword
+  // from reflected bytes taken from the lanes that hold them (ds_bpermute)
+  const bool edge = gc0 == 0 || 4 * (gc0 + LB_WC) + 4 > W;  // wave-uniform
+  const uint32_t lbx = (uint32_t)(edge ? min(max(x, 0), W - 4) : x);
+  uint32_t V[LB_R + 6];
+#pragma unroll
+  for (int k = 0; k < LB_R + 6; ++k) {
+    const int gy = reflect101(min(y0 - 3 + k, H + 2), H);
+    V[k] = ld32u(src + (__umul24((uint32_t)gy, sp) + lbx));
+  }
+  if (edge) {
+    // byte j of this lane's dword is level column xq = reflect101(x + j)
+    // (clamped: lanes far past the level stay in range, their values feed no
+    // stored pixel); it lives in lane xq / 4 - gc0 + 1 at byte xq & 3, or, in
+    // the last (possibly partial) dword, in that dword's lane, which loaded
+    // columns W-4 .. W-1
+    int sl[4], sh[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int xq = reflect101(min(max(x + j, -4), W + 3), W);
+      const bool last = xq >= 4 * (nd - 1);
+      sl[j] = 4 * min(max((last ? nd - 1 : xq >> 2) - gc0 + 1, 0), 63);
+      sh[j] = last ? 8 * (xq - (W - 4)) : 8 * (xq & 3);
+    }
+#pragma unroll
+    for (int k = 0; k < LB_R + 6; ++k) {
+      uint32_t v = 0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        v |= ((uint32_t)__builtin_amdgcn_ds_bpermute(sl[j], (int)V[k]) >> sh[j] & 0xFFu) << (8 * j);
+      V[k] = v;
+    }
+  }
+  uint8_t* dst = blur + (size_t)f * bstride + B.blur_off[i];
+  const uint32_t bp = (uint32_t)B.bpitch[i];
+  const bool store = lane >= 1 && lane <= LB_WC && x < W;
+  uint32_t Hc[7][4];  // horizontal sums of the last 7 staged rows (fully unrolled: register renaming)
+  uint32_t Pr[7][4];  // (H of row k-1, H of row k) as u16 x 2
+#pragma unroll
+  for (int k = 0; k < LB_R + 6; ++k) {
+    const uint32_t w1 = V[k];
+    const uint32_t w0 = (uint32_t)__builtin_amdgcn_mov_dpp((int)w1, 0x138, 0xf, 0xf, true);  // wave_shr:1
+    const uint32_t w2 = (uint32_t)__builtin_amdgcn_mov_dpp((int)w1, 0x130, 0xf, 0xf, true);  // wave_shl:1
+    const int s = k % 7;
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      const uint32_t h = __builtin_amdgcn_udot4(
+          w2, kb_w(m, 2), __builtin_amdgcn_udot4(w1, kb_w(m, 1), __builtin_amdgcn_udot4(w0, kb_w(m, 0), 0u, false), false),
+          false);
+      if (k >= 1) Pr[s][m] = Hc[(k + 6) % 7][m] | (h << 16);
+      Hc[s][m] = h;
+    }
+    if (k >= 6) {
+      // output row o = k - 6 (staged rows o .. o + 6): pairs (o, o+1),
+      // (o+2, o+3), (o+4, o+5) and row o + 6 alone
+      const int o = k - 6, y = y0 + o;
+      uint32_t q[4];
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        uint32_t acc = __builtin_amdgcn_udot2(as_us2(Pr[(o + 1) % 7][m]), as_us2(KV_PAIR(18, 34)), 32768u, false);
+        acc = __builtin_amdgcn_udot2(as_us2(Pr[(o + 3) % 7][m]), as_us2(KV_PAIR(48, 56)), acc, false);
+        acc = __builtin_amdgcn_udot2(as_us2(Pr[(o + 5) % 7][m]), as_us2(KV_PAIR(48, 34)), acc, false);
+        q[m] = acc + __umul24(18u, Hc[s][m]);  // out = q >> 16 (<= 255: the taps sum to 65536)
+      }
+      const uint32_t lo = __builtin_amdgcn_perm(q[1], q[0], 0x0c0c0602u);  // bytes 2 of q[0..3]
+      const uint32_t hi = __builtin_amdgcn_perm(q[3], q[2], 0x06020c0cu);
+      if (store && y < H) *reinterpret_cast<uint32_t*>(dst + (__umul24((uint32_t)y, bp) + (uint32_t)x)) = lo | hi;
+    }
+  }
+}
+
 // vertical pairs (lo = first row, hi = second row) for taps starting at the
 // low half (E) or the high half (O) of the first row pair
-#define KV_PAIR(a, b) ((uint32_t)(a) | ((uint32_t)(b) << 16))
 #define KV_E0 KV_PAIR(18, 34)
 #define KV_E1 KV_PAIR(48, 56)
 #define KV_E2 KV_PAIR(48, 34)
@@ -1457,18 +1573,26 @@ struct BriefKp {
   const uint8_t* img;
   int pitch, UW, UH, px0, py0;
   bool inside;   // the whole patch lies in the level
+  // level-blur mode: the blurred level and the blurred patch's first column
+  const uint8_t* bimg;
+  int bpitch, bx0;
 };
 
 // the patch is 43 rows x 12 dwords: lane (< 60) owns column lane % 12 of
 // rows lane / 12 + 5u, u = 0..8 (row 43+ clamped).  The nine loads are issued
 // together from one uniform base (saddr) + a 32-bit lane offset and held in
 // registers (scalars in a struct: never spilled to scratch).
+// Level-blur mode (LB, k_orient_brief_lb): 11 registers -- the unblurred
+// disk rows y-15..y+15, patch dwords 1..10 (310 dwords: lane + 64u, u < 5)
+// and the blurred patch rows y-18..y+18, 10 dwords from bx0 = (x-18) & ~3
+// (370 dwords: lane + 64u, u < 6).
+template <bool LB>
 struct BriefRegs {
-  uint32_t r[9];
-  uint32_t ht;  // the keypoint's packed horizontal-pass tasks (c_htask)
+  uint32_t r[LB ? 11 : 9];
+  uint32_t ht;  // the keypoint's packed horizontal-pass tasks (c_htask), per-keypoint blur only
 };
 
-__device__ __forceinline__ void brief_issue(const BriefKp& k, BriefRegs& R, int lane) {
+__device__ __forceinline__ void brief_issue(const BriefKp& k, BriefRegs<false>& R, int lane) {
   const int ln = min(lane, 59);
   const uint32_t c4 = (uint32_t)(ln % 12) * 4u, r0 = (uint32_t)(ln / 12);
   R.ht = c_htask.v[k.x - k.px0 - 21][lane];  // cc = 21..24
@@ -1511,7 +1635,7 @@ __device__ __forceinline__ void brief_issue(const BriefKp& k, BriefRegs& R, int 
   }
 }
 
-__device__ __forceinline__ void brief_commit(const BriefRegs& R, uint32_t* P, int lane) {
+__device__ __forceinline__ void brief_commit(const BriefRegs<false>& R, uint32_t* P, int lane) {
   if (lane < 60) {
     const int c = lane % 12, r0 = lane / 12;
 #pragma unroll
@@ -1522,18 +1646,60 @@ __device__ __forceinline__ void brief_commit(const BriefRegs& R, uint32_t* P, in
   }
 }
 
+// Level-blur mode: every read lies inside its level (keypoints are >= 19 px
+// from every border: FAST cells span [16, dim - 16) less cv::FAST's 3-px
+// margin, ORBextractor.cc:316-331; the disk reaches 15 px, the blurred
+// samples 18 px), so no reflection here -- k_blur applied it.  Bytes read
+// past a row's last pixel (<= 3 of the unblurred rows, <= 2 of the blurred)
+// belong to the next row or the pitch padding and are never used.
+#define LB_DISK 310 /* 31 rows x 10 dwords */
+#define LB_BP 370   /* 37 rows x 10 dwords */
+__device__ __forceinline__ void brief_issue(const BriefKp& k, BriefRegs<true>& R, int lane) {
+  const uint8_t* b = k.img + ((uint32_t)(k.y - 15) * (uint32_t)k.pitch + (uint32_t)(k.px0 + 4));
+#pragma unroll
+  for (int u = 0; u < 5; ++u) {
+    const uint32_t e = (uint32_t)min(lane + 64 * u, LB_DISK - 1), row = e / 10u, dw = e - 10u * row;
+    R.r[u] = ld32u(b + (__umul24(row, (uint32_t)k.pitch) + 4u * dw));  // pitch < 2^24 (API check)
+  }
+  const uint8_t* bb = k.bimg + ((uint32_t)(k.y - 18) * (uint32_t)k.bpitch + (uint32_t)k.bx0);
+#pragma unroll
+  for (int u = 0; u < 6; ++u) {
+    const uint32_t e = (uint32_t)min(lane + 64 * u, LB_BP - 1), row = e / 10u, dw = e - 10u * row;
+    R.r[5 + u] = *reinterpret_cast<const uint32_t*>(bb + (__umul24(row, (uint32_t)k.bpitch) + 4u * dw));
+  }
+}
+
+__device__ __forceinline__ void brief_commit(const BriefRegs<true>& R, uint32_t* P, uint32_t* Bp, int lane) {
+#pragma unroll
+  for (int u = 0; u < 5; ++u) {
+    const int e = lane + 64 * u, row = e / 10, dw = e - 10 * row;
+    if (e < LB_DISK) P[row * KP_PSTRIDE + 1 + dw] = R.r[u];
+  }
+#pragma unroll
+  for (int u = 0; u < 6; ++u) {
+    const int e = lane + 64 * u;
+    if (e < LB_BP) Bp[e] = R.r[5 + u];  // row-major, 10 dwords (40 bytes) per row
+  }
+}
+
 #ifndef OB_WPE
 #define OB_WPE 7
 #endif
 #ifndef OB_PROBE
 #define OB_PROBE 0 /* profiling only: 1 / 2 / 3 skip the horizontal pass / IC_Angle sums / samples, 4 / 5 the fastAtan2 + sincos chain / sincos */
 #endif
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OB_WPE))) void k_orient_brief(
-    const uint8_t* __restrict__ frames, size_t fstride, size_t rstride,
-    const uint8_t* __restrict__ pyr, size_t pstride, const BriefArgs A,
-    const uint32_t* __restrict__ qout, size_t qout_stride, const int* __restrict__ lcount,
-    orbx_keypoint* __restrict__ kps, uint8_t* __restrict__ desc, int* __restrict__ counts,
-    const uint32_t* __restrict__ qperm, int dbg) {
+#define OB_KERNEL_ARGS                                                                             \
+  const uint8_t *__restrict__ frames, size_t fstride, size_t rstride, const uint8_t *__restrict__ pyr, \
+      size_t pstride, const BriefArgs A, const uint32_t *__restrict__ qout, size_t qout_stride,        \
+      const int *__restrict__ lcount, orbx_keypoint *__restrict__ kps, uint8_t *__restrict__ desc,     \
+      int *__restrict__ counts, const uint32_t *__restrict__ qperm, int dbg
+#define OB_KERNEL_PASS frames, fstride, rstride, pyr, pstride, A, qout, qout_stride, lcount, kps, desc, counts, qperm, dbg
+// LB = false: per-keypoint blur (the horizontal pass over the staged
+// unblurred patch, the vertical taps at every sample); LB = true: samples
+// read the level k_blur materialised (the planner picks per geometry,
+// Plan::lb)
+template <bool LB>
+__device__ __forceinline__ void ob_body(OB_KERNEL_ARGS, const uint8_t* __restrict__ blur, size_t bstride) {
   __shared__ uint32_t patch[4][KP_ROWS][KP_PSTRIDE];
   // horizontally blurred patch, column-major: hblur[w][patch col][row pair]
   // = (H(row 2k), H(row 2k+1)) as u16 pair, H = sum_i k_i p (7 taps)
@@ -1552,6 +1718,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OB_WPE))) v
   const uint32_t* Q = qout + (size_t)f * qout_stride;
   const uint32_t* QP = qperm + (size_t)f * qout_stride;
   uint32_t(*P)[KP_PSTRIDE] = patch[wave];
+  uint32_t* const Bp = &hblur[wave][0][0];  // LB: the blurred patch (37 x 40 bytes) in the hblur space
+  const uint8_t* const Bpb = reinterpret_cast<const uint8_t*>(Bp);
   orbx_keypoint* const kpsf = kps + (size_t)f * kcap;  // this frame's outputs
   // IC_Angle weights, the lane's part (b0 = 24 for odd lanes, else 4)
   const uint32_t Wlane = (uint32_t)((lane & 1) ? 24 + 19 : 4 + 19) * 0x01010101u + 0x03020100u;
@@ -1599,6 +1767,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OB_WPE))) v
     k.px0 = (k.x - KP_R) & ~3;
     k.py0 = k.y - KP_R;
     k.inside = k.px0 >= 0 && k.px0 + KP_COLS <= k.UW && k.py0 >= 0 && k.py0 + KP_ROWS <= k.UH;
+    if constexpr (LB) {
+      k.bimg = blur + (size_t)f * bstride + A.blur_off[u];
+      k.bpitch = A.bpitch[u];
+      k.bx0 = (k.x - 18) & ~3;
+    }
     return k;
   };
   // output position o (levels concatenated, :455-494); waves stride over
@@ -1618,12 +1791,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OB_WPE))) v
 #endif
   if (o >= oend) return;
   BriefKp cur = locate(o);
-  BriefRegs R;
+  BriefRegs<LB> R;
   brief_issue(cur, R, lane);
   for (; o < oend; o += stride) {  // wave-uniform
   // ---- stage this keypoint's patch (unblurred level), reflect-101 outside ----
-  brief_commit(R, &P[0][0], lane);
-  const uint32_t hte = R.ht;  // before the next keypoint's issue overwrites R
+  uint32_t hte = 0;
+  if constexpr (LB) {
+    brief_commit(R, &P[0][0], Bp, lane);
+  } else {
+    brief_commit(R, &P[0][0], lane);
+    hte = R.ht;  // before the next keypoint's issue overwrites R
+  }
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   const BriefKp me = cur;
@@ -1640,7 +1818,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OB_WPE))) v
   // reads + 4 v_dot2_u32_u16 down its hblur column -- 64 LDS ops per keypoint
   // instead of 21 dword reads per sample (126).  It runs before IC_Angle so
   // its LDS writes drain while the angle and sin/cos are computed.
-  {
+  if constexpr (!LB) {
     // task = (row pair rp, 4-column group q): patch columns 4q..4q+3, rows
     // 2rp, 2rp+1; the 7-byte windows c-3..c+3 lie in dwords q-1..q+1
     // cc = x - px0 is 21..24, so the columns cc-18..cc+18 always span the 10
@@ -1686,8 +1864,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OB_WPE))) v
   // four bits per dword spread to bytes by a multiply; sum I and
   // sum (u + 19) I are two v_dot4_u32_u8 per dword (weights u + 19 keep every
   // byte of a touched dword in 1..37: no borrow between bytes).
-  const int cc = x - px0, cr = KP_R;
+  const int cc = x - px0, cr = LB ? 15 : KP_R;  // LB: the staged disk rows start at y - 15
   const int hcc = cc - 4 * ((cc - 18) >> 2);  // hblur column of the keypoint (column 4 qlo is 0)
+  const int bxc = 18 * 40 + (x - me.bx0);     // LB: the keypoint's byte in the blurred patch
   int m10 = 0, m01 = 0;
   if (OB_PROBE != 2 && lane < 62) {  // OB_PROBE 2: no IC_Angle sums (profiling only)
     const int v = (lane >> 1) - 15, av = v < 0 ? -v : v;
@@ -1749,6 +1928,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OB_WPE))) v
       const float ya = fy * cs, yb = fy * sn;
       const int row = (int)__builtin_rintf(__builtin_fmaf(fx, sn, ya));
       const int col = (int)__builtin_rintf(__builtin_fmaf(fx, cs, -yb));
+      if constexpr (LB) {
+        t[e] = Bpb[bxc + __mul24(row, 40) + col];  // |row|, |col| <= 18
+        continue;
+      }
       const int rt = cr + row - 3;  // first vertical tap (patch row)
       const uint32_t* hc = &hblur[wave][0][0] + (__mul24(hcc + col, KP_HSTRIDE) + (rt >> 1));  // col may be < 0
       const uint32_t v0 = hc[0], v1 = hc[1], v2 = hc[2], v3 = hc[3];
@@ -1783,6 +1966,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OB_WPE))) v
     *reinterpret_cast<orbx_keypoint*>(reinterpret_cast<uint8_t*>(kpsf) + (uint32_t)me.oi * (uint32_t)sizeof(orbx_keypoint)) = kp;
   }
   }
+}
+
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OB_WPE))) void k_orient_brief(OB_KERNEL_ARGS) {
+  ob_body<false>(OB_KERNEL_PASS, nullptr, 0);
+}
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OB_WPE))) void k_orient_brief_lb(
+    OB_KERNEL_ARGS, const uint8_t* __restrict__ blur, size_t bstride) {
+  ob_body<true>(OB_KERNEL_PASS, blur, bstride);
 }
 
 // ---------------------------------------------------------------------------

@@ -260,7 +260,7 @@ __global__ __launch_bounds__(256) void k_match_cand_lds(
       nv += __shfl_xor(nv, s, 64);
     }
     if (lane == 0) rowinfo[r] = make_int4(1, nv, mn >= INF ? (1 << 20) : mn, idx1);
-    if (mn >= ORBM_TH_LOW) continue;
+    if (mn >= P.th_low) continue;
     uint2* out = cand + (size_t)r * ORBM_T;
     uint32_t key[NJ];
 #pragma unroll
@@ -521,7 +521,7 @@ __global__ __launch_bounds__(256) void k_match_cand_rows(
     const int minD = L[0] != 0xFFFFFFFFu ? (int)(L[0] >> 16) : (1 << 20);
     // .y > ORBM_T: the list may be incomplete (resolve rescans when exhausted)
     rowinfo[r] = make_int4(1, full ? ORBM_T + 1 : 0, minD, idx1[h]);
-    if (minD >= ORBM_TH_LOW) continue;
+    if (minD >= P.th_low) continue;
     uint4* out = reinterpret_cast<uint4*>(cand + (size_t)r * ORBM_T);
 #pragma unroll
     for (int t = 0; t < ORBM_T / 2; ++t) {
@@ -815,7 +815,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MC_WPE))) v
     }
     const int minD = Lt[0] != 0xFFFFFFFFu ? (int)(Lt[0] >> 16) : (1 << 20);
     rowinfo[r] = make_int4(1, full ? ORBM_T + 1 : 0, minD, idx1[t]);
-    if (minD >= ORBM_TH_LOW) continue;
+    if (minD >= P.th_low) continue;
     uint4* out = reinterpret_cast<uint4*>(cand + (size_t)r * ORBM_T);
 #pragma unroll
     for (int u = 0; u < ORBM_T / 2; ++u) {
@@ -874,7 +874,7 @@ __global__ __launch_bounds__(256) void k_match_resolve(
       // rows in list order, 64 at a time; only rows that can pass TH_LOW matter
       int4 inf = make_int4(0, 0, 0, 0);
       if (base + lane < NP.n1) inf = rowinfo[NP.row_base + base + lane];
-      uint64_t feas = __ballot(inf.x != 0 && inf.z < ORBM_TH_LOW);
+      uint64_t feas = __ballot(inf.x != 0 && inf.z < P.th_low);
       if (feas) {  // stage the chunk's candidate lists (contiguous rows) in LDS
         const int nr = min(64, NP.n1 - base);
         const uint4* src = reinterpret_cast<const uint4*>(cand + (size_t)(NP.row_base + base) * ORBM_T);
@@ -928,7 +928,7 @@ __global__ __launch_bounds__(256) void k_match_resolve(
             best2 = d2;
           }
         }
-        if (best1 < ORBM_TH_LOW && (float)best1 < P.nnratio * (float)best2) {
+        if (best1 < P.th_low && (float)best1 < P.nnratio * (float)best2) {
           if (lane == 0) {  // rotation bin: k_match_finalize
             bm[bidx2 >> 5] |= 1u << (bidx2 & 31);
             ev[r] = make_int2(bidx2, 0);
@@ -996,7 +996,7 @@ __global__ __launch_bounds__(64) void k_match_resolve_spec(
     // wave-uniform "list longer than the candidates" mask, and the rare
     // rescan re-reads its row's idx1
     const int4 inf = inf_n;
-    const bool feas = base + lane < NP.n1 && inf.x != 0 && inf.z < ORBM_TH_LOW;
+    const bool feas = base + lane < NP.n1 && inf.x != 0 && inf.z < P.th_low;
     const uint64_t longl = __ballot(inf.y > ORBM_T);
     uint2 c[ORBM_T];
 #pragma unroll
@@ -1051,7 +1051,7 @@ __global__ __launch_bounds__(64) void k_match_resolve_spec(
       const int k2 = U2 ? (int)(e2 >> 16) : INT_MAX;
       const int plen = U2 ? si + 1 : ORBM_T;  // slots the serial walk examined
       const bool hard = mine && U2 == 0u && ((longl >> lane) & 1ull);  // list exhausted: needs a rescan
-      const bool acc = mine && !hard && k1 < ORBM_TH_LOW && (float)k1 < P.nnratio * (float)k2;
+      const bool acc = mine && !hard && k1 < P.th_low && (float)k1 < P.nnratio * (float)k2;
       if (acc) atomicMin(&claim[id1], lane);
       __builtin_amdgcn_wave_barrier();
       int cl[ORBM_T];
@@ -1099,7 +1099,7 @@ __global__ __launch_bounds__(64) void k_match_resolve_spec(
         }
         if (kb != 0xFFFFFFFFu) {
           const int b1 = (int)(kb >> 16), bi = (int)gf2[kb & 0xFFFFu];
-          if (b1 < ORBM_TH_LOW && (float)b1 < P.nnratio * (float)d2 && lane == bnd) {
+          if (b1 < P.th_low && (float)b1 < P.nnratio * (float)d2 && lane == bnd) {
             atomicOr(&bm[bi >> 5], 1u << (bi & 31));
             ev[r] = make_int2(bi, 0);
           }

@@ -54,19 +54,21 @@ struct MProblem {
   float nnratio;
   int sequential;  /* 1: one wave walks all node pairs in order (malformed FeatureVectors) */
   int dcap;        /* candidate distance cap (orbm_dcap) */
-  int pad;
+  int th_low;      /* a best match needs d < th_low: ORBM_TH_LOW (KF-KF, :339), ORBM_TH_LOW + 1 for
+                      upstream's KF-Frame form (bestDist1 <= TH_LOW) */
 };
 
-/* Smallest distance D >= TH_LOW with (float)(TH_LOW-1) < nnratio * (float)D,
- * capped at 257.  Only candidates below D can change a SearchByBoW decision:
- * a best match needs d < TH_LOW <= D, and a second-best >= D always passes
- * the ratio test (ORBmatcher.cc:339-342), exactly like the true value. */
+/* Smallest distance D >= th with (float)(th-1) < nnratio * (float)D, capped
+ * at 257 (th = the problem's th_low).  Only candidates below D can change a
+ * SearchByBoW decision: a best match needs d < th <= D, and a second-best
+ * >= D always passes the ratio test (ORBmatcher.cc:339-342), exactly like the
+ * true value. */
 #if defined(__HIPCC__)
 __host__ __device__
 #endif
-static inline int orbm_dcap(float nnratio) {
-  for (int D = ORBM_TH_LOW; D <= 256; ++D)
-    if ((float)(ORBM_TH_LOW - 1) < nnratio * (float)D) return D;
+static inline int orbm_dcap(float nnratio, int th = ORBM_TH_LOW) {
+  for (int D = th; D <= 256; ++D)
+    if ((float)(th - 1) < nnratio * (float)D) return D;
   return 257;
 }
 

@@ -33,6 +33,7 @@ struct LevelInfo {
   int unique;          /* level whose storage holds these pixels                */
   long long pyr_off;   /* offset in the per-frame pyramid buffer (unique >= 1)  */
   long long blur_off;  /* offset in the per-frame blur buffer (unique levels)   */
+  int bpitch;          /* its row pitch (16-B multiple)                          */
   /* resize from level l-1 (unique levels >= 1) */
   int lut_x, lut_y;    /* offsets into the xofs/alpha and yofs/beta LUTs         */
   int src_level;       /* unique level the resize reads                          */
@@ -111,10 +112,37 @@ struct StereoArgs {
 
 /* per-level constants of k_orient_brief, passed by value (kernel arguments
  * live in SGPRs: no dependent global loads to find a keypoint's level) */
+/* level-blur mode (k_blur + k_orient_brief_lb, Plan::lb): the 7x7 Gaussian of
+ * every unique level materialised once per frame in the blur buffer (row
+ * pitch bpitch = pitch_of(w), offset blur_off), tiles of ORBX_LB_TW x
+ * ORBX_LB_TH, unique level i owning tiles [tile_begin[i], tile_begin[i+1]) */
+#define ORBX_LB_TW 248 /* k_blur tile: 62 dword columns (+ 2 halo lanes) x 4 waves of 32 rows */
+#define ORBX_LB_TH 128
+#define KP_PATCH_ROWS 43 /* the per-keypoint blur's staged patch (k_orient_brief) */
+#define KP_PATCH_COLS 48
+#ifndef ORBX_LB_RATIO
+/* level blur when nfeatures x patch > ratio x unique level pixels.  Measured
+ * (DESIGN §4 round 5): the blur pass costs more than the per-keypoint blur it
+ * saves at c1 (ratio 2.2), c5 (2.9) and c4 (0.66); c2 (6.7) is break-even. */
+#define ORBX_LB_RATIO 8.0
+#endif
+struct BlurArgs {
+  int nu;                                  /* unique levels */
+  int tile_begin[ORBX_MAX_LEVELS + 1];     /* cumulative tile counts */
+  int tiles_x[ORBX_MAX_LEVELS];
+  int w[ORBX_MAX_LEVELS], h[ORBX_MAX_LEVELS];
+  int pitch[ORBX_MAX_LEVELS];              /* source pitch (unique level 0: the caller's rstride) */
+  long long src_off[ORBX_MAX_LEVELS];      /* pyr offset, -1 = the caller's frame */
+  int bpitch[ORBX_MAX_LEVELS];
+  long long blur_off[ORBX_MAX_LEVELS];
+};
+
 struct BriefArgs {
   int nlevels, kcap;
   int kout_off[ORBX_MAX_LEVELS], lcap[ORBX_MAX_LEVELS];
   int unique[ORBX_MAX_LEVELS], w[ORBX_MAX_LEVELS], h[ORBX_MAX_LEVELS], pitch[ORBX_MAX_LEVELS];
+  int bpitch[ORBX_MAX_LEVELS];             /* level-blur mode: blurred level pitch / offset */
+  long long blur_off[ORBX_MAX_LEVELS];
   long long pyr_off[ORBX_MAX_LEVELS];
   float scale[ORBX_MAX_LEVELS];
   int patch[ORBX_MAX_LEVELS];

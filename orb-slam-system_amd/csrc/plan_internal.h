@@ -32,6 +32,8 @@ struct orbx_plan {
   size_t pyr_stride = 0, blur_stride = 0, slot_stride = 0, qk_stride = 0, qout_stride = 0;
   size_t qt_lds = 0;
   BriefArgs bargs;
+  BlurArgs blargs;  /* level-blur mode: k_blur's tiles */
+  int lb_auto = 0;  /* the planner's BRIEF blur choice: 1 = level blur (k_blur + k_orient_brief_lb) */
   LevelArgs largs;
   orbx::StageTimer timer;
   int dbg = 0; /* ORBX_DEBUG_STOP: kernel phase early-exit for profiling only */
@@ -44,6 +46,9 @@ struct orbx_plan {
   hipEvent_t ev_aux0 = nullptr, ev_aux1 = nullptr;
   int options = 0; /* ORBX_PLAN_* (include/orbx.h) */
   int nextracted = 0; /* frames of the last orbx_plan_extract (orbx_plan_level bound) */
+  int uses_lb() const {
+    return (options & ORBX_PLAN_BRIEF_LEVEL) ? 1 : (options & ORBX_PLAN_BRIEF_PATCH) ? 0 : lb_auto;
+  }
 };
 
 struct orbx_extractor {

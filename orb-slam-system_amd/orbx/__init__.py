@@ -42,7 +42,7 @@ assert KEYPOINT_DTYPE.itemsize == 28
 OK, ERR_ARG, ERR_CELL_ROI, ERR_LEVEL_SIZE, ERR_QUADTREE, ERR_CAPACITY, ERR_UNSUPPORTED, \
     ERR_HIP, ERR_NO_DEVICE = 0, -1, -2, -3, -4, -5, -6, -7, -8
 ORBM_PLAN_ZERO_TAIL, ORBM_PLAN_VALU = 1, 2  # orbm_plan_set_options flags (include/orbx.h)
-ORBX_PLAN_PYR_TILES = 1  # orbx_plan_set_options flag
+ORBX_PLAN_PYR_TILES, ORBX_PLAN_BRIEF_PATCH, ORBX_PLAN_BRIEF_LEVEL = 1, 8, 16  # orbx_plan_set_options flags
 
 EXPORTED = [
     "orbx_abi_version", "orbx_status_string", "orbx_device_count", "orbx_tables",
@@ -52,7 +52,7 @@ EXPORTED = [
     "orbx_boundary_record_bytes", "orbx_boundary_pack", "orbx_boundary_unpack",
     "orbx_plan_create", "orbx_plan_destroy", "orbx_plan_geometry", "orbx_plan_extract",
     "orbx_plan_check", "orbx_plan_debug_counters", "orbx_plan_set_options", "orbx_plan_level", "orbx_stage_count", "orbx_stage_name", "orbx_plan_set_timing",
-    "orbx_plan_stage_times", "orbx_synth_frames", "orbm_search_by_bow",
+    "orbx_plan_stage_times", "orbx_synth_frames", "orbm_search_by_bow", "orbm_search_by_bow_kf_frame",
     "orbm_descriptor_distance_batch", "orbm_plan_create", "orbm_plan_destroy",
     "orbm_plan_match_frames", "orbm_plan_set_timing", "orbm_plan_stage_times", "orbm_plan_set_options",
     "orbx_stereo_match", "orbs_plan_create", "orbs_plan_destroy", "orbs_plan_match",
@@ -141,6 +141,7 @@ _sig = {
     "orbx_plan_stage_times": (I, [P, P, P, I]),
     "orbx_synth_frames": (I, [P, I, I, SZ, I, I, I, P]),
     "orbm_search_by_bow": (I, [P, P, F, I, I, P, P]),
+    "orbm_search_by_bow_kf_frame": (I, [P, P, F, I, I, P, P]),
     "orbm_descriptor_distance_batch": (I, [P, I, P, I, P, P, I, I, P]),
     "orbm_plan_create": (I, [I, I, I, I, P]),
     "orbm_plan_destroy": (I, [P]),
@@ -437,6 +438,19 @@ def search_by_bow(kf1, kf2, nnratio=0.6, check_ori=True, device=0):
     return m[:b1.n].copy(), nm.value
 
 
+def search_by_bow_kf_frame(kf, fr, nnratio=0.6, check_ori=True, device=0):
+    """Upstream ORB-SLAM2's SearchByBoW(KF, Frame) (bow_kf_frame=full; the
+    reference ships a stub): returns (match_f int32[F.N], nmatches)."""
+    keep = []
+    b1, b2 = _bow_struct(kf, keep), _bow_struct(fr, keep)
+    m = np.full(max(b2.n, 1), -1, np.int32)
+    nm = ctypes.c_int(0)
+    _check(_lib.orbm_search_by_bow_kf_frame(ctypes.byref(b1), ctypes.byref(b2), float(nnratio),
+                                            1 if check_ori else 0, device, _p(m), ctypes.byref(nm)),
+           "orbm_search_by_bow_kf_frame")
+    return m[:b2.n].copy(), nm.value
+
+
 def descriptor_distance_batch(a, b, ia, ib, device=0):
     a = np.ascontiguousarray(a, np.uint8).reshape(-1, 32)
     b = np.ascontiguousarray(b, np.uint8).reshape(-1, 32)
@@ -567,10 +581,14 @@ class Plan:
         _check(_lib.orbx_plan_debug_counters(self._h, ctypes.byref(v)), "orbx_plan_debug_counters")
         return {"fast_overflow_strips": v.value}
 
-    def set_options(self, pyramid="auto"):
+    def set_options(self, pyramid="auto", brief="auto"):
         """pyramid: 'auto' or 'tiles' (k_pyramid, the one pyramid path since
-        the round-4 streaming kernels were retired)"""
+        the round-4 streaming kernels were retired); brief: 'auto' (the
+        planner's choice), 'patch' (per-keypoint blur, k_orient_brief) or
+        'level' (every level blurred once, k_blur + k_orient_brief_lb).
+        Every combination gives the same results."""
         flags = {"auto": 0, "tiles": ORBX_PLAN_PYR_TILES}[pyramid]
+        flags |= {"auto": 0, "patch": ORBX_PLAN_BRIEF_PATCH, "level": ORBX_PLAN_BRIEF_LEVEL}[brief]
         _check(_lib.orbx_plan_set_options(self._h, flags), "orbx_plan_set_options")
 
     def level(self, frame, lvl, stream=None):

@@ -55,6 +55,15 @@ struct TFrame {
   }
 };
 
+// the Frame members upstream's SearchByBoW(KeyFrame*, Frame&) reads
+// (Frame.h: N, mvKeys, mFeatVec after ComputeBoW, mDescriptors)
+struct TBowFrame {
+  int N = 0;
+  std::vector<cv::KeyPoint> mvKeys;
+  std::map<unsigned int, std::vector<unsigned int>> mFeatVec;
+  cv::Mat mDescriptors;
+};
+
 static std::vector<uint8_t> load(const char* p, size_t n) {
   std::vector<uint8_t> v(n);
   FILE* f = fopen(p, "rb");
@@ -146,6 +155,26 @@ int main(int argc, char** argv) {
   int tw[2] = {top.cols, top.rows};
   fwrite(tw, sizeof(int), 2, o);
   for (int r = 0; r < top.rows; ++r) fwrite(top.ptr(r), 1, top.cols, o);
+  // SearchByBoW(KeyFrame*, Frame&) as Tracking.cc:447 / :817 call it: the
+  // reference's stub (the default: F.N nulls, 0) and, switched to
+  // bow_kf_frame=full, upstream's search (KF1's MapPoints into frame D)
+  TBowFrame fd;
+  fd.N = (int)kf2.mvKeysUn.size();
+  fd.mvKeys = kf2.mvKeysUn;
+  fd.mFeatVec = kf2.mFeatVec;
+  fd.mDescriptors = kf2.mDescriptors;
+  ORBmatcher bm(0.7f, true);  // Tracking.cc:445 TrackReferenceKeyFrame
+  std::vector<TMapPoint*> vpm(3, &sentinel);
+  if (bm.SearchByBoW(&kf1, fd, vpm) != 0 || (int)vpm.size() != fd.N) return 4;
+  for (size_t i = 3; i < vpm.size(); ++i)
+    if (vpm[i]) return 4;
+  bm.SetBowKFFrame(ORBmatcher::BowKFFrame::Full);
+  const int nkf = bm.SearchByBoW(&kf1, fd, vpm);
+  std::vector<int> mf(fd.N, -1);
+  for (int i = 0; i < fd.N; ++i) mf[i] = vpm[i] ? (int)(vpm[i] - mp1.data()) : -1;
+  int h2[2] = {nkf, fd.N};
+  fwrite(h2, sizeof(int), 2, o);
+  fwrite(mf.data(), sizeof(int), mf.size(), o);
   fclose(o);
   delete left;
   delete right;

@@ -212,3 +212,10 @@ def test_reference_shaped_concurrent_call_sites(gpu, oracle, tmp_path):
         return dict(desc=dsc, angle=k["angle"], valid=valid, node_id=ids, off=offs, feat=feat)
     rm, rnm = oracle.search_by_bow(kf(kc, dc), kf(kd, dd), 0.75, True)
     assert nm == rnm and nm > 0 and np.array_equal(m12, rm)
+    # SearchByBoW(KF, Frame): stub by default (checked in C++), then
+    # bow_kf_frame=full against the oracle's upstream restatement
+    nkf, nfd = np.frombuffer(raw[off:off + 8], np.int32).tolist(); off += 8
+    mf = np.frombuffer(raw[off:off + 4 * nfd], np.int32)
+    fr = dict(kf(kd, dd), valid=None)
+    rmf, rnkf = oracle.search_by_bow_kf_frame(kf(kc, dc), fr, 0.7, True)
+    assert nfd == len(kd) and nkf == rnkf and nkf > 0 and np.array_equal(mf, rmf)

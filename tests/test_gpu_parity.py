@@ -166,10 +166,34 @@ def test_batched_plan_matches_single(gpu, oracle):
         assert np.array_equal(res[f][1], rd)
 
 
+# both BRIEF blur forms on every extraction shape: the per-keypoint patch
+# blur (k_orient_brief) and the materialised level blur (k_blur +
+# k_orient_brief_lb), forced through orbx_plan_set_options whatever the
+# planner would pick; two frames per batch (different kinds)
+@pytest.mark.parametrize("brief", ["patch", "level"])
+@pytest.mark.parametrize("w,h,nf,L,guard,kind,idx", [c for c in EXTRACT_CASES if c[5] != "flat"] +
+                         [(640, 480, 1000, 8, "strict", "pan", 80), (1241, 376, 2000, 8, "strict", "pan", 81),
+                          (641, 479, 1000, 8, "strict", "noise", 82), (643, 363, 1000, 3, "strict", "rects", 83)])
+def test_brief_blur_modes_match_oracle(gpu, oracle, brief, w, h, nf, L, guard, kind, idx):
+    import torch
+    B = 2
+    plan = gpu.Plan(gpu.params(nf, 1.2, L, 20, 7, guard), w, h, B)
+    plan.set_options(brief=brief)
+    frames = np.stack([synth.frame(w, h, idx, kind), synth.frame(w, h, idx + 100, "noise")])
+    plan.extract(torch.from_numpy(frames).cuda())
+    plan.check()
+    res = plan.results(B)
+    for f in range(B):
+        rk, rd = oracle.Extractor(nf, 1.2, L, 20, 7, cell_guard=guard).extract(frames[f])
+        _cmp_kps(res[f][0], rk, "frame %d (%s blur)" % (f, brief))
+        assert np.array_equal(res[f][1], rd), "descriptors differ (%s blur)" % brief
+
+
 def test_plan_argument_checks(gpu, oracle):
     """C-ABI argument checks of the batched plan:
-    * orbx_plan_set_options accepts 0 / ORBX_PLAN_PYR_TILES only; the retired
-      streaming / fused flags (2, 4) and every combination are ORBX_ERR_ARG;
+    * orbx_plan_set_options accepts ORBX_PLAN_PYR_TILES and one of the two
+      BRIEF flags; the retired streaming / fused flags (2, 4), unknown bits and
+      both BRIEF flags at once are ORBX_ERR_ARG;
     * orbx_plan_level copies only frames the last extraction wrote
       (ORBX_ERR_ARG before any extraction and past its frame count; the size
       query with dst = NULL stays valid);
@@ -180,10 +204,10 @@ def test_plan_argument_checks(gpu, oracle):
     lib = gpu._lib
     W, H, B = 640, 480, 3
     plan = gpu.Plan(gpu.params(1000, 1.2, 8, 20, 7), W, H, B)
-    for flags in (2, 4, 3, 5, 6, 7, 8, -1):
+    for flags in (2, 4, 3, 5, 6, 7, 24, 25, 32, -1):
         assert lib.orbx_plan_set_options(plan._h, flags) == gpu.ERR_ARG, flags
-    assert lib.orbx_plan_set_options(plan._h, gpu.ORBX_PLAN_PYR_TILES) == gpu.OK
-    assert lib.orbx_plan_set_options(plan._h, 0) == gpu.OK
+    for flags in (1, 8, 16, 9, 17, 0):
+        assert lib.orbx_plan_set_options(plan._h, flags) == gpu.OK, flags
     buf = np.zeros((H, W), np.uint8)
     w, h = ctypes.c_int(0), ctypes.c_int(0)
     assert lib.orbx_plan_level(plan._h, 0, 2, None, 0, ctypes.byref(w), ctypes.byref(h), None) == gpu.OK
@@ -276,6 +300,49 @@ def test_search_by_bow_matches_oracle(gpu, oracle, seed, nnratio, check_ori):
     rm, rnm = oracle.search_by_bow(kf1, kf2, nnratio, check_ori)
     assert nm == rnm
     assert np.array_equal(m, rm)
+
+
+@pytest.mark.parametrize("seed", range(5))
+@pytest.mark.parametrize("nnratio,check_ori", [(0.6, True), (0.75, True), (0.9, False)])
+def test_search_by_bow_kf_frame_matches_oracle(gpu, oracle, seed, nnratio, check_ori):
+    """bow_kf_frame=full: upstream's SearchByBoW(KeyFrame*, Frame&) on the
+    device (orbm_search_by_bow_kf_frame) vs the oracle's restatement: rows =
+    KF features with a valid MapPoint, every Frame feature a candidate (the
+    Frame dict's valid mask must be ignored), bestDist1 <= TH_LOW; distances of
+    exactly 50 are planted so the inclusive bound is exercised."""
+    rng = np.random.default_rng(100 + seed)
+    nk, nf = int(rng.integers(50, 700)), int(rng.integers(50, 700))
+    dk = rng.integers(0, 256, (nk, 32), dtype=np.uint8)
+    src = dk[rng.integers(0, nk, nf)]
+    flips = rng.choice([0, 5, 30, 49, 50, 50, 51, 60, 90], nf)
+    df = _correlated(rng, src, flips)
+    kf = _random_bow(rng, nk, int(rng.integers(1, 10)), 30, dk)
+    fr = _random_bow(rng, nf, int(rng.integers(1, 10)), 30, df)
+    m, nm = gpu.search_by_bow_kf_frame(kf, fr, nnratio, check_ori)
+    rm, rnm = oracle.search_by_bow_kf_frame(kf, fr, nnratio, check_ori)
+    assert nm == rnm and np.array_equal(m, rm)
+    # the Frame side's valid mask plays no part
+    fr2 = dict(fr, valid=None)
+    m2, nm2 = gpu.search_by_bow_kf_frame(kf, fr2, nnratio, check_ori)
+    assert nm2 == nm and np.array_equal(m2, m)
+
+
+def test_search_by_bow_kf_frame_threshold_inclusive(gpu, oracle):
+    """One KF row, two Frame candidates at distances 50 and 80: upstream's
+    KF-Frame form accepts (bestDist1 <= TH_LOW), the KF-KF form does not
+    (best < TH_LOW, src/ORBmatcher.cc:339)."""
+    rng = np.random.default_rng(7)
+    d = rng.integers(0, 256, (1, 32), dtype=np.uint8)
+    f = np.concatenate([_correlated(rng, d, [50]), _correlated(rng, d, [80])])
+    one = lambda desc: dict(desc=desc, angle=np.zeros(len(desc), np.float32), valid=None,
+                            node_id=np.array([3], np.uint32), off=np.array([0, len(desc)], np.uint32),
+                            feat=np.arange(len(desc), dtype=np.uint32))
+    m, nm = gpu.search_by_bow_kf_frame(one(d), one(f), 0.75, True)
+    assert nm == 1 and m.tolist() == [0, -1]
+    assert oracle.search_by_bow_kf_frame(one(d), one(f), 0.75, True)[1] == 1
+    assert gpu.search_by_bow(one(d), one(f), 0.75, True)[1] == 0
+    with pytest.raises(gpu.OrbxError):
+        gpu.search_by_bow_kf_frame(one(d), one(f), 0.19, True)
 
 
 def test_search_by_bow_single_node_bruteforce(gpu, oracle):

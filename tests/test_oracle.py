@@ -249,3 +249,108 @@ def test_oracle_resize_area2_matches_definition(oracle):
     # (a0 = a1 = b0 = b1 = 1024: ((a+b) + (c+d) + 2) >> 2)
     assert np.array_equal(e.level(2), oracle.resize_linear(e.level(1), 320, 240))
 
+
+
+def _bow_kf_frame_literal(kf, fr, nnratio, check_ori):
+    """Upstream ORB-SLAM2's SearchByBoW(KeyFrame*, Frame&) written out with
+    Python containers as the published C++ reads (std::map FeatureVectors,
+    vector<MapPoint*> output, rotHist lists, ComputeThreeMaxima); the
+    reference itself ships only a stub (src/ORBmatcher.cc:88-119)."""
+    def fv(k):
+        return {int(n): [int(x) for x in k["feat"][k["off"][j]:k["off"][j + 1]]]
+                for j, n in enumerate(k["node_id"])}
+    fk, ff = fv(kf), fv(fr)
+    nf = len(fr["desc"])
+    out = [None] * nf
+    hist = [[] for _ in range(30)]
+    nm = 0
+
+    def dist(a, b):
+        return int(np.unpackbits(np.bitwise_xor(a, b)).sum())
+    for node in sorted(set(fk) & set(ff)):  # the merge-join visits common NodeIds in order
+        for ik in fk[node]:
+            if kf["valid"] is not None and not kf["valid"][ik]:
+                continue
+            b1, b2, bi = 256, 256, -1
+            for jf in ff[node]:
+                if out[jf] is not None:
+                    continue
+                d = dist(kf["desc"][ik], fr["desc"][jf])
+                if d < b1:
+                    b2, b1, bi = b1, d, jf
+                elif d < b2:
+                    b2 = d
+            if b1 <= 50 and np.float32(b1) < np.float32(nnratio) * np.float32(b2):
+                out[bi] = ik
+                if check_ori:
+                    rot = np.float32(kf["angle"][ik]) - np.float32(fr["angle"][bi])
+                    if rot < 0:
+                        rot = np.float32(rot + np.float32(360.0))
+                    b = int(np.floor(np.float32(rot * np.float32(1.0 / 30)) + np.float32(0.5)))
+                    if b == 30:
+                        b = 0
+                    hist[b].append(bi)
+                nm += 1
+    if check_ori:
+        sizes = [len(h) for h in hist]
+        order = []
+        for _ in range(3):  # ComputeThreeMaxima: strict >, lower bin wins ties
+            best = -1
+            for i in range(30):
+                if i not in order and (best < 0 or sizes[i] > sizes[best]):
+                    best = i
+            order.append(best)
+        i1, i2, i3 = order
+        if sizes[i2] < 0.1 * sizes[i1]:
+            i2 = i3 = -1
+        elif sizes[i3] < 0.1 * sizes[i1]:
+            i3 = -1
+        for b in range(30):
+            if b in (i1, i2, i3):
+                continue
+            for jf in hist[b]:
+                out[jf] = None
+                nm -= 1
+    return np.array([-1 if x is None else x for x in out], np.int32), nm
+
+
+def _kf_frame_case(seed, nk, nf, nnodes):
+    rng = np.random.default_rng(seed)
+    base = rng.integers(0, 256, (nk, 32), dtype=np.uint8)
+    fdesc = rng.integers(0, 256, (nf, 32), dtype=np.uint8)
+    # half of the Frame's features are noisy copies of KF features: near
+    # matches, exact-50 distances and ties
+    for j in range(0, nf, 2):
+        src = base[rng.integers(0, nk)].copy()
+        flips = rng.choice(256, int(rng.choice([3, 20, 49, 50, 51, 70])), replace=False)
+        for b in flips:
+            src[b // 8] ^= np.uint8(1 << (b % 8))
+        fdesc[j] = src
+    nodes = np.sort(rng.choice(1000, nnodes, replace=False)).astype(np.uint32)
+    def fvec(n, sub):
+        assign = rng.integers(0, nnodes, n)
+        use = np.sort(rng.choice(nnodes, sub, replace=False))
+        off, feat, ids = [0], [], []
+        for j in use:
+            f = np.nonzero(assign == j)[0].tolist()
+            ids.append(nodes[j]); feat.extend(f); off.append(len(feat))
+        return np.array(ids, np.uint32), np.array(off, np.uint32), np.array(feat, np.uint32)
+    ki, ko, kfe = fvec(nk, max(1, nnodes - 1))
+    fi, fo, ffe = fvec(nf, max(1, nnodes - 1))
+    kf = dict(desc=base, angle=rng.uniform(0, 360, nk).astype(np.float32),
+              valid=(rng.uniform(size=nk) > 0.15).astype(np.uint8), node_id=ki, off=ko, feat=kfe)
+    fr = dict(desc=fdesc, angle=rng.uniform(0, 360, nf).astype(np.float32), valid=None,
+              node_id=fi, off=fo, feat=ffe)
+    return kf, fr
+
+
+@pytest.mark.parametrize("seed", range(4))
+@pytest.mark.parametrize("nnratio,ori", [(0.6, True), (0.75, True), (0.9, False)])
+def test_oracle_search_by_bow_kf_frame_literal(oracle, seed, nnratio, ori):
+    """The C restatement of upstream's SearchByBoW(KF, Frame) against the
+    container-level literal form above: identical matches and count."""
+    kf, fr = _kf_frame_case(seed, 120, 150, 4)
+    m, n = oracle.search_by_bow_kf_frame(kf, fr, nnratio, ori)
+    rm, rn = _bow_kf_frame_literal(kf, fr, nnratio, ori)
+    assert n == rn and np.array_equal(m, rm)
+    assert n > 0
