@@ -214,6 +214,7 @@ def test_reference_shaped_concurrent_call_sites(gpu, oracle, tmp_path):
     assert nm == rnm and nm > 0 and np.array_equal(m12, rm)
     # SearchByBoW(KF, Frame): stub by default (checked in C++), then
     # bow_kf_frame=full against the oracle's upstream restatement
+    off += tw * th  # past mvImagePyramid[7]
     nkf, nfd = np.frombuffer(raw[off:off + 8], np.int32).tolist(); off += 8
     mf = np.frombuffer(raw[off:off + 4 * nfd], np.int32)
     fr = dict(kf(kd, dd), valid=None)
