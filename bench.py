@@ -92,6 +92,9 @@ def parse():
                     help="pipelined step: extract the batch as this many sub-batches, each on its own "
                          "stream (same frames and work); default 2 for c1-c4 (measured +0.5-1.5 %%), "
                          "1 for c5 (2 measured -12 %%)")
+    ap.add_argument("--match-priority", choices=["high", "low"], default="high",
+                    help="pipelined step: the matcher's stream above the extraction streams (high) "
+                         "or below them (low: its kernels fill the slots extraction leaves)")
     ap.add_argument("--match-whole", action="store_true",
                     help="with --split: match the whole batch after every sub-batch is extracted "
                          "(default: sub-batch j is matched as soon as it and its predecessor frame exist)")
@@ -659,9 +662,10 @@ def main_mono(args, wl):
         # (each plan creates a stream of its own): HIP hands out its hardware
         # queues (GPU_MAX_HW_QUEUES, 4 on the box) in creation order, and
         # streams on one queue serialise
-        sa = torch.cuda.Stream(device=dev)
-        sb = torch.cuda.Stream(device=dev, priority=-1)
-        sx = [sa] + [torch.cuda.Stream(device=dev) for _ in range(S - 1)]
+        xp, mpri = (0, -1) if args.match_priority == "high" else (-1, 0)
+        sa = torch.cuda.Stream(device=dev, priority=xp)
+        sb = torch.cuda.Stream(device=dev, priority=mpri)
+        sx = [sa] + [torch.cuda.Stream(device=dev, priority=xp) for _ in range(S - 1)]
         ev_s = [torch.cuda.Event() for _ in range(S)]
         bufs = [(kps, desc, counts),
                 (torch.zeros_like(kps), torch.zeros_like(desc), torch.zeros_like(counts))]
@@ -897,9 +901,10 @@ def main_c5(args, wl):
                 a_.set_options(pyramid=args.pyramid, brief=args.brief)
                 b_.set_options(pyramid=args.pyramid, brief=args.brief)
                 subs.append((a_, b_, orbx.StereoPlan(a_, device=local)))
-        sa = torch.cuda.Stream(device=dev)  # back to back, after every plan (main_mono)
-        sb = torch.cuda.Stream(device=dev, priority=-1)
-        sx = [sa] + [torch.cuda.Stream(device=dev) for _ in range(S - 1)]
+        xp, mpri = (0, -1) if args.match_priority == "high" else (-1, 0)
+        sa = torch.cuda.Stream(device=dev, priority=xp)  # back to back, after every plan (main_mono)
+        sb = torch.cuda.Stream(device=dev, priority=mpri)
+        sx = [sa] + [torch.cuda.Stream(device=dev, priority=xp) for _ in range(S - 1)]
         ev_s = [torch.cuda.Event() for _ in range(S)]
 
         def pipe():

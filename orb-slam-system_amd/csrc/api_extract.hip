@@ -176,6 +176,7 @@ extern "C" int orbx_plan_create(const orbx_params* prm, int width, int height, i
    * inherited environment cannot change its results) */
   if (const char* e = getenv("ORBX_DEBUG_STOP")) p->dbg = atoi(e);
   if (const char* e = getenv("ORBX_DEBUG_OBDIV")) p->ob_div = atoi(e);
+  if (const char* e = getenv("ORBX_DEBUG_LDSPAD")) sscanf(e, "%d,%d,%d", &p->pad_pyr, &p->pad_fast, &p->pad_brief);
   if (const char* e = getenv("ORBX_CHUNK")) p->chunk = atoi(e);
   if (const char* e = getenv("ORBX_DEBUG_OVERLAP")) p->overlap = atoi(e); /* FAST level 0 beside the pyramid */
 #endif
@@ -356,7 +357,7 @@ static int extract_pass(orbx_plan* p, const uint8_t* frames, int n, size_t fstri
   int* const d_lcount = p->d_lcount + f0 * (size_t)L;
   auto fast_launch = [&](int strip0, int nstrips, hipStream_t st) {
     if (nstrips <= 0) return;
-    hipLaunchKernelGGL(p->fs_tpitch == 288 ? k_fast_strips_p288 : k_fast_strips, dim3((unsigned)nstrips, n), dim3(FS_NT), p->fs_lds, st,
+    hipLaunchKernelGGL(p->fs_tpitch == 288 ? k_fast_strips_p288 : k_fast_strips, dim3((unsigned)nstrips, n), dim3(FS_NT), p->fs_lds + p->pad_fast, st,
                        frames, fstride, rstride, d_pyr, p->pyr_stride, p->largs, p->d_cells,
                        p->d_strips, d_slots, p->slot_stride, d_ccount, P.ncells, P.ini_th,
                        P.min_th, p->fs_tpitch, p->fs_tmaxh, p->fs_mcells, p->fs_ccap,
@@ -383,7 +384,7 @@ static int extract_pass(orbx_plan* p, const uint8_t* frames, int n, size_t fstri
       continue;
     }
     hipLaunchKernelGGL(k_pyramid, dim3(g.ntx * g.nty, n), dim3(256),
-                       g.lds_a + g.lds_b + g.lds_yl, s, frames, fstride, rstride,
+                       g.lds_a + g.lds_b + g.lds_yl + p->pad_pyr, s, frames, fstride, rstride,
                        d_pyr, p->pyr_stride, g, reinterpret_cast<const int4*>(p->d_pyr_xs),
                        reinterpret_cast<const int4*>(p->d_pyr_ys),
                        reinterpret_cast<const uint4*>(p->d_pyr_blob), p->d_pyr_bo, p->dbg);
@@ -440,12 +441,12 @@ static int extract_pass(orbx_plan* p, const uint8_t* frames, int n, size_t fstri
   if (p->ob_div > 0) ob_waves = std::max(4, ob_full / p->ob_div); /* profiling only */
   if (p->uses_lb()) {
     hipLaunchKernelGGL(k_orient_brief_lb, dim3((ob_waves + 3) / 4, n),
-                       dim3(256), 0, s, frames, fstride, rstride, d_pyr, p->pyr_stride, p->bargs,
+                       dim3(256), p->pad_brief, s, frames, fstride, rstride, d_pyr, p->pyr_stride, p->bargs,
                        d_qout, p->qout_stride, d_lcount, kps, desc,
                        counts, p->d_qperm + f0 * p->qout_stride, p->dbg, d_blur, p->blur_stride);
   } else {
     hipLaunchKernelGGL(k_orient_brief, dim3((ob_waves + 3) / 4, n),
-                       dim3(256), 0, s, frames, fstride, rstride, d_pyr, p->pyr_stride, p->bargs,
+                       dim3(256), p->pad_brief, s, frames, fstride, rstride, d_pyr, p->pyr_stride, p->bargs,
                        d_qout, p->qout_stride, d_lcount, kps, desc,
                        counts, p->d_qperm + f0 * p->qout_stride, p->dbg);
   }

@@ -38,6 +38,9 @@ struct orbx_plan {
   orbx::StageTimer timer;
   int dbg = 0; /* ORBX_DEBUG_STOP: kernel phase early-exit for profiling only */
   int ob_div = 0; /* ORBX_DEBUG_OBDIV: k_orient_brief grid divisor, profiling only */
+  /* ORBX_DEBUG_LDSPAD=pyr,fast,brief: extra dynamic LDS per workgroup
+   * (occupancy probes: room for other streams' kernels), profiling only */
+  int pad_pyr = 0, pad_fast = 0, pad_brief = 0;
   int fs_ccap = 0; /* FAST per-strip corner list entries used (FS_CCAP; ORBX_DEBUG_CCAP lowers it) */
   int chunk = 0;  /* frames per extraction pass (0 = the whole batch in one pass) */
   hipEvent_t ev_after_pyr = nullptr; /* recorded after the pyramid launch when set (orbx_extract) */
