@@ -433,6 +433,31 @@ int orbm_search_by_projection(int mode, const orbx_proj_frame* frame, const orbx
                               const uint8_t* qdesc, int nq, float nnratio, int th_dist,
                               int check_ori, int device, int32_t* match, int* nmatches);
 
+/* Batched device form of orbm_search_by_projection: nprob independent
+ * problems (e.g. the current frames of many streams, each with its projected
+ * map points) searched in one set of launches -- the grid of every frame, a
+ * wavefront per (query, problem), the greedy walk of every problem in
+ * parallel.  Every pointer of a problem is DEVICE memory (frame.keys / desc
+ * / uright / occupied, q, qdesc; outputs match[frame.n] and *nmatches);
+ * asynchronous on `stream`.  Same results as orbm_search_by_projection on
+ * each problem.  A plan holds the scratch for max_problems problems of at
+ * most max_n features (<= 8192) and max_nq queries; one call at a time per
+ * plan (the problem table is staged in pinned memory; a call waits for the
+ * previous call's table upload, not for its kernels). */
+typedef struct {
+  orbx_proj_frame frame;
+  const orbx_query_proj* q;
+  const uint8_t* qdesc;
+  int nq;
+  int32_t* match;
+  int* nmatches;
+} orbx_proj_problem;
+typedef struct orbm_proj_plan orbm_proj_plan;
+int orbm_proj_plan_create(int max_problems, int max_n, int max_nq, int device, orbm_proj_plan** out);
+int orbm_proj_plan_destroy(orbm_proj_plan* plan);
+int orbm_proj_plan_search(orbm_proj_plan* plan, int mode, int nprob, const orbx_proj_problem* probs,
+                          float nnratio, int th_dist, int check_ori, void* stream);
+
 /* ---------------------------------------------------------------------------
  * SURVEY.md §8f rank 4.
  * ------------------------------------------------------------------------- */

@@ -15,14 +15,25 @@ struct ProjFrame {
   int n;
   float minX, minY, wInv, hInv;
 };
-__global__ void k_grid_build(const orbx_keypoint*, const ProjFrame, int, int*, int*);
-__global__ void k_proj_cand(const ProjFrame, const orbx_keypoint*, const uint8_t*, const float*,
-                            const uint8_t*, const int*, const int*, const orbx_query_proj*,
-                            const uint8_t*, int, int, uint32_t*, int*);
-__global__ void k_proj_resolve(const ProjFrame, const orbx_keypoint*, const uint8_t*, const float*,
-                               const uint8_t*, const int*, const int*, const orbx_query_proj*,
-                               const uint8_t*, int, int, float, int, int, const uint32_t*,
-                               const int*, int32_t*, int*);
+struct ProjProblem {  // kernels_proj.hip
+  ProjFrame F;
+  const orbx_keypoint* keys;
+  const uint8_t* desc;
+  const float* uright;
+  const uint8_t* occupied;
+  const orbx_query_proj* qs;
+  const uint8_t* qdesc;
+  int nq;
+  int32_t* match;
+  int* nmatches;
+  int* cell_off;
+  int* cell_feat;
+  uint32_t* cand;
+  int* ncand;
+};
+__global__ void k_grid_build(const ProjProblem*);
+__global__ void k_proj_cand(const ProjProblem*, int);
+__global__ void k_proj_resolve(const ProjProblem*, int, float, int, int);
 }  // namespace orbx
 
 using namespace orbx;
@@ -30,6 +41,31 @@ using namespace orbx;
 #define PJ_T 8
 #define PJ_MAXN 8192
 #define PG_CELLS (64 * 48)
+
+static ProjFrame proj_frame(const orbx_proj_frame* F) {
+  ProjFrame PF;
+  PF.n = F->n;
+  PF.minX = F->min_x;
+  PF.minY = F->min_y;
+  PF.wInv = F->grid_w_inv;
+  PF.hInv = F->grid_h_inv;
+  return PF;
+}
+
+// the three launches over nprob problems (device table d_probs): grid per
+// problem, candidates per (query, problem), the greedy walk per problem
+static void launch_proj(const ProjProblem* d_probs, int nprob, int max_n, int max_nq, int mode,
+                        float nnratio, int th_dist, int check_ori, hipStream_t s) {
+  int P = 1;
+  while (P < max_n) P <<= 1;
+  hipLaunchKernelGGL(k_grid_build, dim3((unsigned)nprob), dim3(1024), (size_t)P * 4, s, d_probs);
+  if (max_nq > 0)
+    hipLaunchKernelGGL(k_proj_cand, dim3((unsigned)((max_nq + 3) / 4), (unsigned)nprob), dim3(256), 0, s,
+                       d_probs, mode);
+  const size_t lds = (size_t)((max_n + 31) / 32) * 4 + (size_t)max_n;
+  hipLaunchKernelGGL(k_proj_resolve, dim3((unsigned)nprob), dim3(64), lds, s, d_probs, mode, nnratio,
+                     th_dist, check_ori);
+}
 
 extern "C" int orbm_search_by_projection(int mode, const orbx_proj_frame* F,
                                          const orbx_query_proj* q, const uint8_t* qdesc, int nq,
@@ -56,6 +92,7 @@ extern "C" int orbm_search_by_projection(int mode, const orbx_proj_frame* F,
   const size_t o_keys = C.take((size_t)n * sizeof(orbx_keypoint)), o_desc = C.take((size_t)n * 32);
   const size_t o_ur = F->uright ? C.take((size_t)n * 4) : 0, o_occ = F->occupied ? C.take(n) : 0;
   const size_t o_q = C.take((size_t)nq * sizeof(orbx_query_proj)), o_qd = C.take((size_t)nq * 32);
+  const size_t o_prob = C.take(sizeof(ProjProblem));
   const size_t in_end = C.off;
   const size_t o_match = C.take((size_t)n * 4), o_nm = C.take(4), out_end = C.off;
   const size_t o_off = C.take((PG_CELLS + 1) * 4), o_feat = C.take((size_t)n * 4);
@@ -70,39 +107,134 @@ extern "C" int orbm_search_by_projection(int mode, const orbx_proj_frame* F,
   if (F->occupied) memcpy(h + o_occ, F->occupied, n);
   memcpy(h + o_q, q, (size_t)nq * sizeof(orbx_query_proj));
   memcpy(h + o_qd, qdesc, (size_t)nq * 32);
+  ProjProblem* hp = reinterpret_cast<ProjProblem*>(h + o_prob);
+  ProjProblem* dp = reinterpret_cast<ProjProblem*>(d + o_prob);
+  hp->F = proj_frame(F);
+  hp->keys = reinterpret_cast<orbx_keypoint*>(d + o_keys);
+  hp->desc = d + o_desc;
+  hp->uright = F->uright ? reinterpret_cast<float*>(d + o_ur) : nullptr;
+  hp->occupied = F->occupied ? d + o_occ : nullptr;
+  hp->qs = reinterpret_cast<orbx_query_proj*>(d + o_q);
+  hp->qdesc = d + o_qd;
+  hp->nq = nq;
+  hp->match = reinterpret_cast<int32_t*>(d + o_match);
+  hp->nmatches = reinterpret_cast<int*>(d + o_nm);
+  hp->cell_off = reinterpret_cast<int*>(d + o_off);
+  hp->cell_feat = reinterpret_cast<int*>(d + o_feat);
+  hp->cand = reinterpret_cast<uint32_t*>(d + o_cand);
+  hp->ncand = reinterpret_cast<int*>(d + o_nc);
   ORBX_TRY(hipMemcpyAsync(d, h, in_end, hipMemcpyHostToDevice, s));
-  orbx_keypoint* d_keys = reinterpret_cast<orbx_keypoint*>(d + o_keys);
-  uint8_t* d_desc = d + o_desc;
-  float* d_ur = F->uright ? reinterpret_cast<float*>(d + o_ur) : nullptr;
-  uint8_t* d_occ = F->occupied ? d + o_occ : nullptr;
-  int* d_off = reinterpret_cast<int*>(d + o_off);
-  int* d_feat = reinterpret_cast<int*>(d + o_feat);
-  orbx_query_proj* d_q = reinterpret_cast<orbx_query_proj*>(d + o_q);
-  uint8_t* d_qd = d + o_qd;
-  uint32_t* d_cand = reinterpret_cast<uint32_t*>(d + o_cand);
-  int* d_nc = reinterpret_cast<int*>(d + o_nc);
-  int32_t* d_match = reinterpret_cast<int32_t*>(d + o_match);
-  int* d_nm = reinterpret_cast<int*>(d + o_nm);
-  ProjFrame PF;
-  PF.n = n;
-  PF.minX = F->min_x;
-  PF.minY = F->min_y;
-  PF.wInv = F->grid_w_inv;
-  PF.hInv = F->grid_h_inv;
-  int P = 1;
-  while (P < n) P <<= 1;
-  hipLaunchKernelGGL(k_grid_build, dim3(1), dim3(1024), (size_t)P * 4, s, d_keys, PF, P, d_off,
-                     d_feat);
-  hipLaunchKernelGGL(k_proj_cand, dim3((nq + 3) / 4), dim3(256), 0, s, PF, d_keys, d_desc, d_ur,
-                     d_occ, d_off, d_feat, d_q, d_qd, nq, mode, d_cand, d_nc);
-  const size_t lds = (size_t)((n + 31) / 32) * 4 + (size_t)n;
-  hipLaunchKernelGGL(k_proj_resolve, dim3(1), dim3(64), lds, s, PF, d_keys, d_desc, d_ur, d_occ,
-                     d_off, d_feat, d_q, d_qd, nq, mode, nnratio, th_dist, check_ori, d_cand,
-                     d_nc, d_match, d_nm);
+  launch_proj(dp, 1, n, nq, mode, nnratio, th_dist, check_ori, s);
   if (hipGetLastError() != hipSuccess) return ORBX_ERR_HIP;
   ORBX_TRY(hipMemcpyAsync(h + in_end, d + in_end, out_end - in_end, hipMemcpyDeviceToHost, s));
   ORBX_TRY(stream_wait(s));
   memcpy(match, h + o_match, (size_t)n * 4);
   memcpy(nmatches, h + o_nm, sizeof(int));
+  return ORBX_OK;
+}
+
+// ---------------------------------------------------------------------------
+// Batched device form: many SearchByProjection problems (frames, each with
+// its query set) in one set of launches on device-resident inputs.
+// ---------------------------------------------------------------------------
+struct orbm_proj_plan {
+  int device = 0, max_prob = 0, max_n = 0, max_nq = 0;
+  ProjProblem* d_probs = nullptr;
+  ProjProblem* h_probs = nullptr;  // pinned staging of the problem table
+  hipEvent_t ev = nullptr;         // the last table upload (h_probs reusable after it)
+  int* d_cell_off = nullptr;
+  int* d_cell_feat = nullptr;
+  uint32_t* d_cand = nullptr;
+  int* d_ncand = nullptr;
+};
+
+static void proj_plan_free(orbm_proj_plan* p) {
+  if (!p) return;
+  hipSetDevice(p->device);
+  if (p->ev) hipEventDestroy(p->ev);
+  if (p->h_probs) hipHostFree(p->h_probs);
+  void* bufs[] = {p->d_probs, p->d_cell_off, p->d_cell_feat, p->d_cand, p->d_ncand};
+  for (void* b : bufs)
+    if (b) hipFree(b);
+  delete p;
+}
+
+extern "C" int orbm_proj_plan_create(int max_problems, int max_n, int max_nq, int device, orbm_proj_plan** out) {
+  if (!out || max_problems < 1 || max_n < 1 || max_nq < 0) return ORBX_ERR_ARG;
+  *out = nullptr;
+  if (max_n > PJ_MAXN || max_problems > 65535) return ORBX_ERR_UNSUPPORTED;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) return ORBX_ERR_NO_DEVICE;
+  ORBX_TRY(hipSetDevice(device));
+  orbm_proj_plan* p = new orbm_proj_plan();
+  p->device = device;
+  p->max_prob = max_problems;
+  p->max_n = max_n;
+  p->max_nq = max_nq;
+  const size_t B = (size_t)max_problems;
+  if (hipMalloc((void**)&p->d_probs, B * sizeof(ProjProblem)) != hipSuccess ||
+      hipHostMalloc((void**)&p->h_probs, B * sizeof(ProjProblem), hipHostMallocDefault) != hipSuccess ||
+      hipEventCreateWithFlags(&p->ev, hipEventDisableTiming) != hipSuccess ||
+      hipMalloc((void**)&p->d_cell_off, B * (PG_CELLS + 1) * sizeof(int)) != hipSuccess ||
+      hipMalloc((void**)&p->d_cell_feat, B * (size_t)max_n * sizeof(int)) != hipSuccess ||
+      hipMalloc((void**)&p->d_cand, B * (size_t)std::max(max_nq, 1) * PJ_T * sizeof(uint32_t)) != hipSuccess ||
+      hipMalloc((void**)&p->d_ncand, B * (size_t)std::max(max_nq, 1) * sizeof(int)) != hipSuccess) {
+    proj_plan_free(p);
+    return ORBX_ERR_HIP;
+  }
+  if (set_max_dynamic_lds((const void*)k_grid_build, device) ||
+      set_max_dynamic_lds((const void*)k_proj_resolve, device)) {
+    proj_plan_free(p);
+    return ORBX_ERR_HIP;
+  }
+  *out = p;
+  return ORBX_OK;
+}
+
+extern "C" int orbm_proj_plan_destroy(orbm_proj_plan* p) {
+  proj_plan_free(p);
+  return ORBX_OK;
+}
+
+extern "C" int orbm_proj_plan_search(orbm_proj_plan* p, int mode, int nprob, const orbx_proj_problem* probs,
+                                     float nnratio, int th_dist, int check_ori, void* stream) {
+  if (!p || mode < 1 || mode > 3 || nprob < 0 || nprob > p->max_prob || (nprob > 0 && !probs))
+    return ORBX_ERR_ARG;
+  int max_n = 1, max_nq = 0;
+  for (int i = 0; i < nprob; ++i) {
+    const orbx_proj_problem& q = probs[i];
+    const orbx_proj_frame& F = q.frame;
+    if (F.n < 0 || F.n > p->max_n || q.nq < 0 || q.nq > p->max_nq || !q.match || !q.nmatches ||
+        (F.n > 0 && (!F.keys || !F.desc)) || (q.nq > 0 && (!q.q || !q.qdesc)))
+      return ORBX_ERR_ARG;
+    max_n = std::max(max_n, F.n);
+    max_nq = std::max(max_nq, q.nq);
+  }
+  if (nprob == 0) return ORBX_OK;
+  ORBX_TRY(hipSetDevice(p->device));
+  hipStream_t s = (hipStream_t)stream;
+  ORBX_TRY(hipEventSynchronize(p->ev));  // the previous call's table has left the staging buffer
+  for (int i = 0; i < nprob; ++i) {
+    const orbx_proj_problem& q = probs[i];
+    ProjProblem& P = p->h_probs[i];
+    P.F = proj_frame(&q.frame);
+    P.keys = q.frame.keys;
+    P.desc = q.frame.desc;
+    P.uright = q.frame.uright;
+    P.occupied = q.frame.occupied;
+    P.qs = q.q;
+    P.qdesc = q.qdesc;
+    P.nq = q.nq;
+    P.match = q.match;
+    P.nmatches = q.nmatches;
+    P.cell_off = p->d_cell_off + (size_t)i * (PG_CELLS + 1);
+    P.cell_feat = p->d_cell_feat + (size_t)i * p->max_n;
+    P.cand = p->d_cand + (size_t)i * std::max(p->max_nq, 1) * PJ_T;
+    P.ncand = p->d_ncand + (size_t)i * std::max(p->max_nq, 1);
+  }
+  ORBX_TRY(hipMemcpyAsync(p->d_probs, p->h_probs, (size_t)nprob * sizeof(ProjProblem), hipMemcpyHostToDevice, s));
+  ORBX_TRY(hipEventRecord(p->ev, s));
+  launch_proj(p->d_probs, nprob, max_n, max_nq, mode, nnratio, th_dist, check_ori, s);
+  if (hipGetLastError() != hipSuccess) return ORBX_ERR_HIP;
   return ORBX_OK;
 }

@@ -1909,6 +1909,30 @@ __device__ __forceinline__ void ob_body(OB_KERNEL_ARGS, const uint8_t* __restric
   (void)exk0, (void)exk1;
   const float angle = fast_atan2((float)m01, (float)m10);
   float sn = angle * 1e-3f, cs = 1.0f - sn;
+#elif !defined(OB_FULL_WAVE_CHAIN)
+  // the wave-uniform fastAtan2 + double-precision sin/cos chain runs on
+  // lane 0 only and is broadcast (a VALU instruction whose upper 32 lanes
+  // are all inactive costs one pass of the SIMD-32 instead of two: BRIEF
+  // c4 0.496 -> 0.485 ms, c1 0.910 -> 0.887, round 5); the exception lookup
+  // (brief_sincos's ballot) still needs every lane
+  const float factorPI = (float)(3.1415926535897932384626433832795 / 180.f);
+  float angle0 = 0.f, sn0 = 0.f, cs0 = 0.f;
+  if (lane == 0) {
+    angle0 = fast_atan2((float)m01, (float)m10);
+    orbx_sincos_core(angle0 * factorPI, &sn0, &cs0);
+  }
+  const float angle = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, angle0)));
+  float sn = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, sn0)));
+  float cs = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, cs0)));
+  {
+    const uint32_t b = orbx_f2u(angle * factorPI);
+    const uint64_t e0 = __ballot(exk0 == b), e1 = __ballot(exk1 == b);
+    if (e0 | e1) {
+      const int i = e0 ? __ffsll((unsigned long long)e0) - 1 : 64 + __ffsll((unsigned long long)e1) - 1;
+      sn = orbx_u2f(ORBX_SINCOS_EXC[i][1]);
+      cs = orbx_u2f(ORBX_SINCOS_EXC[i][2]);
+    }
+  }
 #else
   const float angle = fast_atan2((float)m01, (float)m10);
   const float factorPI = (float)(3.1415926535897932384626433832795 / 180.f);
@@ -1926,8 +1950,17 @@ __device__ __forceinline__ void ob_body(OB_KERNEL_ARGS, const uint8_t* __restric
     for (int e = 0; e < 2; ++e) {
       const float fx = pfx[rr][e], fy = pfy[rr][e];
       const float ya = fy * cs, yb = fy * sn;
+#ifdef OB_RINT_CVT  // A/B: rint + conversion
       const int row = (int)__builtin_rintf(__builtin_fmaf(fx, sn, ya));
       const int col = (int)__builtin_rintf(__builtin_fmaf(fx, cs, -yb));
+#else
+      // cvRound = rint (round half to even): for |v| < 2^22, v + 1.5 * 2^23
+      // is rounded (RNE) to an integer and its bits are 0x4B400000 + rint(v)
+      // -- one add instead of v_rndne + v_cvt (|v| <= 18.4 here)
+      const float kM = 12582912.0f;
+      const int row = __builtin_bit_cast(int, __builtin_fmaf(fx, sn, ya) + kM) - 0x4B400000;
+      const int col = __builtin_bit_cast(int, __builtin_fmaf(fx, cs, -yb) + kM) - 0x4B400000;
+#endif
       if constexpr (LB) {
         t[e] = Bpb[bxc + __mul24(row, 40) + col];  // |row|, |col| <= 18
         continue;

@@ -29,15 +29,40 @@ struct ProjFrame {
   float minX, minY, wInv, hInv;
 };
 
+// one SearchByProjection call: the frame, its queries, outputs and grid /
+// candidate scratch (device pointers).  The drop-in call launches one; the
+// batched plan (orbm_proj_plan_search) launches many at once, problem =
+// blockIdx.y (candidates) or blockIdx.x (grid, walk).
+struct ProjProblem {
+  ProjFrame F;
+  const orbx_keypoint* keys;
+  const uint8_t* desc;
+  const float* uright;
+  const uint8_t* occupied;
+  const orbx_query_proj* qs;
+  const uint8_t* qdesc;
+  int nq;
+  int32_t* match;
+  int* nmatches;
+  int* cell_off;   // PG_CELLS + 1
+  int* cell_feat;  // n
+  uint32_t* cand;  // nq x PJ_T
+  int* ncand;      // nq
+};
+
 // one workgroup: cells of every feature, ix-major stable order by an LDS
 // bitonic sort of (cell << 16 | index) keys (index order inside a cell, as
 // push_back in index order)
-__global__ __launch_bounds__(1024) void k_grid_build(const orbx_keypoint* __restrict__ keys,
-                                                     const ProjFrame F, int P,
-                                                     int* __restrict__ cell_off,
-                                                     int* __restrict__ cell_feat) {
-  extern __shared__ uint32_t sk[];  // P keys
+__global__ __launch_bounds__(1024) void k_grid_build(const ProjProblem* __restrict__ probs) {
+  extern __shared__ uint32_t sk[];  // P keys (LDS sized for the largest problem)
   __shared__ int cnt[PG_CELLS];
+  const ProjProblem& PP = probs[blockIdx.x];
+  const ProjFrame F = PP.F;
+  const orbx_keypoint* __restrict__ keys = PP.keys;
+  int* __restrict__ cell_off = PP.cell_off;
+  int* __restrict__ cell_feat = PP.cell_feat;
+  int P = 1;
+  while (P < F.n) P <<= 1;
   const int tid = threadIdx.x;
   for (int c = tid; c < PG_CELLS; c += 1024) cnt[c] = 0;
   __syncthreads();
@@ -128,15 +153,22 @@ __device__ __forceinline__ uint32_t proj_key(const orbx_query_proj& Q, const orb
 // One wavefront per query: the PJ_T smallest (distance << 16 | rank) keys
 // over the candidates not occupied before the call (claims made during the
 // walk are resolved by k_proj_resolve), and whether that list is complete.
-__global__ __launch_bounds__(256) void k_proj_cand(
-    const ProjFrame F, const orbx_keypoint* __restrict__ keys, const uint8_t* __restrict__ desc,
-    const float* __restrict__ uright, const uint8_t* __restrict__ occupied,
-    const int* __restrict__ cell_off, const int* __restrict__ cell_feat,
-    const orbx_query_proj* __restrict__ qs, const uint8_t* __restrict__ qdesc, int nq, int mode,
-    uint32_t* __restrict__ cand, int* __restrict__ ncand) {
+__global__ __launch_bounds__(256) void k_proj_cand(const ProjProblem* __restrict__ probs, int mode) {
+  const ProjProblem& PP = probs[blockIdx.y];
   const int lane = threadIdx.x & 63;
   const int qi = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (qi >= nq) return;
+  if (qi >= PP.nq) return;
+  const ProjFrame F = PP.F;
+  const orbx_keypoint* __restrict__ keys = PP.keys;
+  const uint8_t* __restrict__ desc = PP.desc;
+  const float* __restrict__ uright = PP.uright;
+  const uint8_t* __restrict__ occupied = PP.occupied;
+  const int* __restrict__ cell_off = PP.cell_off;
+  const int* __restrict__ cell_feat = PP.cell_feat;
+  const orbx_query_proj* __restrict__ qs = PP.qs;
+  const uint8_t* __restrict__ qdesc = PP.qdesc;
+  uint32_t* __restrict__ cand = PP.cand;
+  int* __restrict__ ncand = PP.ncand;
   const orbx_query_proj Q = qs[qi];
   const uint4* qd = reinterpret_cast<const uint4*>(qdesc + (size_t)qi * 32);
   const uint4 q0 = qd[0], q1 = qd[1];
@@ -234,14 +266,24 @@ __device__ void proj_rescan(const ProjFrame& F, const orbx_query_proj& Q,
 // One wavefront walks the queries in order (the reference's greedy loop):
 // best = first unclaimed entry of the query's list, second = the next
 // unclaimed entry's distance; an exhausted incomplete list is rescanned.
-__global__ __launch_bounds__(64) void k_proj_resolve(
-    const ProjFrame F, const orbx_keypoint* __restrict__ keys, const uint8_t* __restrict__ desc,
-    const float* __restrict__ uright, const uint8_t* __restrict__ occupied,
-    const int* __restrict__ cell_off, const int* __restrict__ cell_feat,
-    const orbx_query_proj* __restrict__ qs, const uint8_t* __restrict__ qdesc, int nq, int mode,
-    float nnratio, int th_dist, int check_ori, const uint32_t* __restrict__ cand,
-    const int* __restrict__ ncand, int32_t* __restrict__ match, int* __restrict__ nmatches) {
+__global__ __launch_bounds__(64) void k_proj_resolve(const ProjProblem* __restrict__ probs, int mode,
+                                                    float nnratio, int th_dist, int check_ori) {
   extern __shared__ uint32_t taken[];  // (n + 31) / 32 bits, then n bins (int8 in int32)
+  const ProjProblem& PP = probs[blockIdx.x];
+  const ProjFrame F = PP.F;
+  const orbx_keypoint* __restrict__ keys = PP.keys;
+  const uint8_t* __restrict__ desc = PP.desc;
+  const float* __restrict__ uright = PP.uright;
+  const uint8_t* __restrict__ occupied = PP.occupied;
+  const int* __restrict__ cell_off = PP.cell_off;
+  const int* __restrict__ cell_feat = PP.cell_feat;
+  const orbx_query_proj* __restrict__ qs = PP.qs;
+  const uint8_t* __restrict__ qdesc = PP.qdesc;
+  const int nq = PP.nq;
+  const uint32_t* __restrict__ cand = PP.cand;
+  const int* __restrict__ ncand = PP.ncand;
+  int32_t* __restrict__ match = PP.match;
+  int* __restrict__ nmatches = PP.nmatches;
   int8_t* bin_of = reinterpret_cast<int8_t*>(taken + ((F.n + 31) >> 5));
   __shared__ int hist[32];
   const int lane = threadIdx.x;

@@ -59,6 +59,7 @@ EXPORTED = [
     "orbs_plan_check", "orbs_plan_set_timing", "orbs_plan_stage_times",
     "orbv_vocab_load_text", "orbv_vocab_create", "orbv_vocab_destroy", "orbv_vocab_info",
     "orbv_transform", "orbv_transform_batch", "orbv_check", "orbm_search_by_projection",
+    "orbm_proj_plan_create", "orbm_proj_plan_destroy", "orbm_proj_plan_search",
     "orbm_compute_distinctive_descriptors", "orbx_undistort_keypoints", "orbx_selftest_sincos",
     "orbx_selftest_sincos_range",
 ]
@@ -100,6 +101,11 @@ class ProjFrame(ctypes.Structure):
                 ("uright", ctypes.c_void_p), ("occupied", ctypes.c_void_p),
                 ("min_x", ctypes.c_float), ("min_y", ctypes.c_float),
                 ("grid_w_inv", ctypes.c_float), ("grid_h_inv", ctypes.c_float)]
+
+
+class ProjProblem(ctypes.Structure):
+    _fields_ = [("frame", ProjFrame), ("q", ctypes.c_void_p), ("qdesc", ctypes.c_void_p),
+                ("nq", ctypes.c_int), ("match", ctypes.c_void_p), ("nmatches", ctypes.c_void_p)]
 
 
 class BowFrame(ctypes.Structure):
@@ -164,6 +170,9 @@ _sig = {
     "orbv_transform_batch": (I, [P, I, P, P, I, I, P, P, P, P, P, P, P, P]),
     "orbv_check": (I, [P, P]),
     "orbm_search_by_projection": (I, [I, P, P, P, I, F, I, I, I, P, P]),
+    "orbm_proj_plan_create": (I, [I, I, I, I, P]),
+    "orbm_proj_plan_destroy": (I, [P]),
+    "orbm_proj_plan_search": (I, [P, I, I, P, F, I, I, P]),
     "orbm_compute_distinctive_descriptors": (I, [P, P, I, I, P]),
     "orbx_undistort_keypoints": (I, [P, I, P, P, I, I, P]),
     "orbx_selftest_sincos": (I, [P, I, P, P]),
@@ -482,6 +491,42 @@ def search_by_projection(mode, frame, queries, qdesc, nnratio=0.6, th_dist=100, 
                                           device, _p(m), ctypes.byref(nm)),
            "orbm_search_by_projection")
     return m[:len(keys)].copy(), nm.value
+
+
+class ProjPlan:
+    """Batched SearchByProjection (orbm_proj_plan_*): many (frame, queries)
+    problems on device-resident data in one set of launches."""
+
+    def __init__(self, max_problems, max_n, max_nq, device=0):
+        h = ctypes.c_void_p()
+        _check(_lib.orbm_proj_plan_create(max_problems, max_n, max_nq, device, ctypes.byref(h)),
+               "orbm_proj_plan_create")
+        self._h, self.device = h, device
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            _lib.orbm_proj_plan_destroy(self._h)
+            self._h = None
+
+    def search(self, mode, problems, nnratio=0.6, th_dist=100, check_ori=True, stream=None):
+        """problems: list of dicts of cuda tensors -- keys [n, 28] u8 (orbx_keypoint
+        rows), desc [n, 32] u8, uright [n] f32 or None, occupied [n] u8 or None,
+        q [nq] rows of PROJ_QUERY_DTYPE as u8 [nq, 28], qdesc [nq, 32] u8,
+        match [n] i32 and nmatches [1] i32 (outputs) -- plus the grid floats
+        min_x, min_y, grid_w_inv, grid_h_inv.  Asynchronous."""
+        def ptr(t):
+            return None if t is None else t.data_ptr()
+        arr = (ProjProblem * max(len(problems), 1))()
+        for i, pb in enumerate(problems):
+            n = pb["keys"].shape[0]
+            arr[i].frame = ProjFrame(n, ptr(pb["keys"]), ptr(pb["desc"]), ptr(pb.get("uright")),
+                                     ptr(pb.get("occupied")), pb["min_x"], pb["min_y"],
+                                     pb["grid_w_inv"], pb["grid_h_inv"])
+            arr[i].q, arr[i].qdesc, arr[i].nq = ptr(pb["q"]), ptr(pb["qdesc"]), pb["q"].shape[0]
+            arr[i].match, arr[i].nmatches = ptr(pb["match"]), ptr(pb["nmatches"])
+        _check(_lib.orbm_proj_plan_search(self._h, mode, len(problems), ctypes.cast(arr, ctypes.c_void_p),
+                                          float(nnratio), int(th_dist), 1 if check_ori else 0,
+                                          _stream_handle(stream)), "orbm_proj_plan_search")
 
 
 def compute_distinctive_descriptors(groups, device=0):

@@ -150,3 +150,56 @@ def test_search_by_projection_exhausted_lists(gpu, oracle, mode):
     gm, gn = gpu.search_by_projection(mode, fr, q, qd, 0.9, 100, mode != 1)
     assert gn == rn and rn > 40
     assert np.array_equal(gm, rm)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode,ratio,thd,ori", [(1, 0.8, 100, False), (2, 0.6, 100, True), (3, 0.6, 64, True)])
+def test_projection_plan_batched_matches_oracle(gpu, oracle, mode, ratio, thd, ori):
+    """orbm_proj_plan_search: 9 problems of different frames, query counts and
+    gates (one with no queries, one with an empty frame) in one set of
+    launches on device-resident inputs; every problem's match array and count
+    equal the oracle's (and the drop-in call's)."""
+    import torch
+    probs, refs = [], []
+    for i in range(9):
+        fr = _frame(oracle, 30 + i, uright=(mode == 1 and i % 2 == 0), occ_frac=0.1 * (i % 3), seed=i)
+        if i == 7:  # an empty frame
+            fr = dict(fr, keys=fr["keys"][:0], desc=fr["desc"][:0],
+                      uright=None if fr["uright"] is None else fr["uright"][:0],
+                      occupied=None if fr["occupied"] is None else fr["occupied"][:0])
+        nq = 0 if i == 4 else [300, 1500, 2500, 800][i % 4]
+        q, qd = _queries(oracle, fr if len(fr["keys"]) else _frame(oracle, 30), nq, 200 + i, mode, dup=0.3 * (i % 3))
+        refs.append(oracle.search_by_projection(mode, fr, q, qd, ratio, thd, ori))
+        t = lambda a, dt=None: None if a is None else torch.from_numpy(np.ascontiguousarray(a)).cuda()
+        n = len(fr["keys"])
+        probs.append(dict(keys=t(fr["keys"].view(np.uint8).reshape(n, 28)), desc=t(fr["desc"].reshape(n, 32)),
+                          uright=t(fr["uright"]), occupied=t(fr["occupied"]),
+                          q=t(q.view(np.uint8).reshape(nq, 28)), qdesc=t(qd.reshape(nq, 32)),
+                          match=torch.full((max(n, 1),), 7, dtype=torch.int32, device="cuda"),
+                          nmatches=torch.full((1,), -5, dtype=torch.int32, device="cuda"),
+                          min_x=fr["min_x"], min_y=fr["min_y"], grid_w_inv=fr["grid_w_inv"],
+                          grid_h_inv=fr["grid_h_inv"]))
+    plan = gpu.ProjPlan(len(probs), 8192, 2500)
+    plan.search(mode, probs, ratio, thd, ori)
+    torch.cuda.synchronize()
+    for i, (pb, (rm, rn)) in enumerate(zip(probs, refs)):
+        n = pb["keys"].shape[0]
+        gm, gn = pb["match"].cpu().numpy()[:n], int(pb["nmatches"].cpu()[0])
+        assert gn == rn, (i, gn, rn)
+        assert np.array_equal(gm, rm), (i, np.nonzero(gm != rm)[0][:10])
+    # a second call on the same plan (staging reuse) gives the same results
+    for pb in probs:
+        pb["match"].fill_(7)
+    plan.search(mode, probs, ratio, thd, ori)
+    torch.cuda.synchronize()
+    for pb, (rm, rn) in zip(probs, refs):
+        n = pb["keys"].shape[0]
+        assert np.array_equal(pb["match"].cpu().numpy()[:n], rm)
+
+
+def test_projection_plan_argument_checks_cpu():
+    """The batched plan's C ABI rejects malformed problem tables before any
+    device work (no GPU needed for the NULL-plan path)."""
+    import orbx
+    assert orbx._lib.orbm_proj_plan_search(None, 1, 0, None, 0.6, 100, 1, None) == orbx.ERR_ARG
+    assert orbx._lib.orbm_proj_plan_destroy(None) == orbx.OK
