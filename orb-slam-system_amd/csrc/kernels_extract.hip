@@ -1345,8 +1345,14 @@ __device__ __forceinline__ void qt_body(QT_KERNEL_ARGS) {
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k_quadtree(QT_KERNEL_ARGS) {
   qt_body<8>(QT_KERNEL_PASS);
 }
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k_quadtree_j6(QT_KERNEL_ARGS) {
-  qt_body<6>(QT_KERNEL_PASS);
+#ifndef QT_JSMALL
+#define QT_JSMALL 6 /* keys per thread in registers below 1 Mpx levels */
+#endif
+#ifndef QT_WPE_SMALL
+#define QT_WPE_SMALL 8
+#endif
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(QT_WPE_SMALL))) void k_quadtree_j6(QT_KERNEL_ARGS) {
+  qt_body<QT_JSMALL>(QT_KERNEL_PASS);
 }
 
 // ---------------------------------------------------------------------------
