@@ -1429,6 +1429,21 @@ __device__ constexpr uint32_t kb_w(int m, int d) {
   }
   return w;
 }
+// H of window column m (0..3) of the 12 bytes d0|d1|d2: the dot4 of each dword
+// with its tap weights, dwords whose weights are all 0 skipped (m = 0 never
+// reaches d2, m = 3 never d0; the compiler does not fold a zero-weight dot4)
+template <int M>
+__device__ __forceinline__ uint32_t kb_hsum(uint32_t d0, uint32_t d1, uint32_t d2) {
+  uint32_t h = 0u;
+  if constexpr (kb_w(M, 0) != 0u) h = __builtin_amdgcn_udot4(d0, kb_w(M, 0), h, false);
+  if constexpr (kb_w(M, 1) != 0u) h = __builtin_amdgcn_udot4(d1, kb_w(M, 1), h, false);
+  if constexpr (kb_w(M, 2) != 0u) h = __builtin_amdgcn_udot4(d2, kb_w(M, 2), h, false);
+  return h;
+}
+__device__ __forceinline__ uint32_t kb_hsum(int m, uint32_t d0, uint32_t d1, uint32_t d2) {
+  return m == 0 ? kb_hsum<0>(d0, d1, d2) : m == 1 ? kb_hsum<1>(d0, d1, d2)
+       : m == 2 ? kb_hsum<2>(d0, d1, d2) : kb_hsum<3>(d0, d1, d2);  // m is a compile-time index
+}
 // ---------------------------------------------------------------------------
 // k_blur: GaussianBlur(clone(level), 7x7, 2, 2, BORDER_REFLECT_101)
 // (ORBextractor.cc:478-479) of every unique level, materialised once per
@@ -1521,9 +1536,7 @@ __global__ __launch_bounds__(256) void k_blur(const uint8_t* __restrict__ frames
     const int s = k % 7;
 #pragma unroll
     for (int m = 0; m < 4; ++m) {
-      const uint32_t h = __builtin_amdgcn_udot4(
-          w2, kb_w(m, 2), __builtin_amdgcn_udot4(w1, kb_w(m, 1), __builtin_amdgcn_udot4(w0, kb_w(m, 0), 0u, false), false),
-          false);
+      const uint32_t h = kb_hsum(m, w0, w1, w2);
       if (k >= 1) Pr[s][m] = Hc[(k + 6) % 7][m] | (h << 16);
       Hc[s][m] = h;
     }
@@ -1856,9 +1869,8 @@ __device__ __forceinline__ void ob_body(OB_KERNEL_ARGS, const uint8_t* __restric
 #pragma unroll
       for (int m = 0; m < 4; ++m) {
         // taps k0..k6 at window bytes m+1..m+7 of the 12 bytes a0|a1|a2
-        const uint32_t W0 = kb_w(m, 0), W1 = kb_w(m, 1), W2 = kb_w(m, 2);
-        const uint32_t h0 = __builtin_amdgcn_udot4(a2, W2, __builtin_amdgcn_udot4(a1, W1, __builtin_amdgcn_udot4(a0, W0, 0u, false), false), false);
-        const uint32_t h1 = __builtin_amdgcn_udot4(b2, W2, __builtin_amdgcn_udot4(b1, W1, __builtin_amdgcn_udot4(b0, W0, 0u, false), false), false);
+        const uint32_t h0 = kb_hsum(m, a0, a1, a2);
+        const uint32_t h1 = kb_hsum(m, b0, b1, b2);
         (&hblur[wave][0][0])[hcol + m * KP_HSTRIDE] = h0 | (h1 << 16);  // column 4 q + m - 4 qlo
       }
     }

@@ -1,0 +1,7 @@
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+TAG=r05ob2 bash tools/gpu_tests.sh tests/test_gpu_parity.py -k "extract or brief or sincos" || exit $?
+tail -1 gpurun_out/gtests_r05ob2.log
+for wl in c4 c1 c2; do
+VARS="prev prof prev prof" EXTRA_ARGS=--serial WL=$wl STEPS=20 bash tools/variant_probe.sh || exit $?
+done
