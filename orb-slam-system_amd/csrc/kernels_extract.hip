@@ -22,6 +22,10 @@
 #include "brief_pattern.inc"
 #define ORBX_SINCOS_STORAGE static __constant__ const
 #include "sincos_exceptions.inc"
+#ifndef OB_HPASS
+#define OB_HPASS 1 /* BRIEF horizontal blur pass: 1 = i8 MFMA over the signed patch, 0 = v_dot4 tasks (A/B) */
+#endif
+#if OB_HPASS == 0
 // the horizontal-blur task table, packed per lane for k_orient_brief: entry
 // (cc - 21, lane) holds the lane's three rounds as bytes 10 rp + q (0xFF =
 // none), one dword load per keypoint instead of an LDS copy of the table
@@ -48,6 +52,7 @@ constexpr BriefHtaskPacked brief_htask_pack() {
   return t;
 }
 static __constant__ const BriefHtaskPacked c_htask = brief_htask_pack();
+#endif
 
 namespace orbx {
 
@@ -1582,6 +1587,13 @@ __global__ __launch_bounds__(256) void k_blur(const uint8_t* __restrict__ frames
 #define KP_HSTRIDE 22 /* hblur column stride, dwords */
 #endif
 #define KP_PSTRIDE (KP_COLS / 4) /* patch row, dwords (+1 padding: no change measured) */
+#ifndef OB_HPASS_GROUP
+#define OB_HPASS_GROUP 1 /* MFMA blocks between scheduling barriers (A/B: 1, 3, 9) */
+#endif
+#define KP_PGUARD_LO 2
+typedef short ob_s2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ ob_s2 as_s2(uint32_t x) { return __builtin_bit_cast(ob_s2, x); }
+#define KP_PGUARD_HI (5 * KP_PSTRIDE + 2)
 
 // One keypoint of the frame's level-major output list: where its level
 // lives and where its patch starts (all wave-uniform).
@@ -1608,13 +1620,17 @@ struct BriefKp {
 template <bool LB>
 struct BriefRegs {
   uint32_t r[LB ? 11 : 9];
+#if OB_HPASS == 0
   uint32_t ht;  // the keypoint's packed horizontal-pass tasks (c_htask), per-keypoint blur only
+#endif
 };
 
 __device__ __forceinline__ void brief_issue(const BriefKp& k, BriefRegs<false>& R, int lane) {
   const int ln = min(lane, 59);
   const uint32_t c4 = (uint32_t)(ln % 12) * 4u, r0 = (uint32_t)(ln / 12);
+#if OB_HPASS == 0
   R.ht = c_htask.v[k.x - k.px0 - 21][lane];  // cc = 21..24
+#endif
   if (k.inside) {
     // wave-uniform; every row offset of a level fits 32 bits (levels >= 2
     // are orbx's own buffers; for level 0, the caller's frame,
@@ -1660,7 +1676,13 @@ __device__ __forceinline__ void brief_commit(const BriefRegs<false>& R, uint32_t
 #pragma unroll
     for (int u = 0; u < 9; ++u) {
       const int row = r0 + 5 * u;
+#if OB_HPASS == 1
+      // stored signed (p - 128, the i8 MFMA's operand form): IC_Angle's sums
+      // are unchanged (sec. ob_body), the pass's H is offset by -128 * 256
+      if (row < KP_ROWS) P[row * KP_PSTRIDE + c] = R.r[u] ^ 0x80808080u;
+#else
       if (row < KP_ROWS) P[row * KP_PSTRIDE + c] = R.r[u];
+#endif
     }
   }
 }
@@ -1719,7 +1741,13 @@ __device__ __forceinline__ void brief_commit(const BriefRegs<true>& R, uint32_t*
 // Plan::lb)
 template <bool LB>
 __device__ __forceinline__ void ob_body(OB_KERNEL_ARGS, const uint8_t* __restrict__ blur, size_t bstride) {
+#if OB_HPASS == 1
+  // guard dwords: the MFMA pass's windows start 2 dwords before a row and its
+  // last row block reads 5 rows + 2 dwords past a patch (never weighted)
+  __shared__ uint32_t patchbuf[KP_PGUARD_LO + 4 * KP_ROWS * KP_PSTRIDE + KP_PGUARD_HI];
+#else
   __shared__ uint32_t patch[4][KP_ROWS][KP_PSTRIDE];
+#endif
   // horizontally blurred patch, column-major: hblur[w][patch col][row pair]
   // = (H(row 2k), H(row 2k+1)) as u16 pair, H = sum_i k_i p (7 taps)
   __shared__ uint32_t hblur[4][KP_HCOLS][KP_HSTRIDE];
@@ -1736,7 +1764,24 @@ __device__ __forceinline__ void ob_body(OB_KERNEL_ARGS, const uint8_t* __restric
   const int excl = incl - lcv;
   const uint32_t* Q = qout + (size_t)f * qout_stride;
   const uint32_t* QP = qperm + (size_t)f * qout_stride;
+#if OB_HPASS == 1
+  uint32_t(*P)[KP_PSTRIDE] = reinterpret_cast<uint32_t(*)[KP_PSTRIDE]>(patchbuf + KP_PGUARD_LO + wave * (KP_ROWS * KP_PSTRIDE));
+  // B operand of the horizontal pass (lane = output column c of a 16-column
+  // block, 8 k-bytes 8 (lane >> 4) + j = window columns): tap t = k - c - 5
+  // of [18, 34, 48, 56, 48, 34, 18] (the window starts 8 columns left of the
+  // block), 0 elsewhere -- one constant for every block and keypoint
+  uint64_t hbw = 0;
+  {
+    const int c = lane & 15, k0 = 8 * (lane >> 4);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int t = k0 + j - c - 5;
+      if (t >= 0 && t <= 6) hbw |= (uint64_t)kb_tap(t) << (8 * j);
+    }
+  }
+#else
   uint32_t(*P)[KP_PSTRIDE] = patch[wave];
+#endif
   uint32_t* const Bp = &hblur[wave][0][0];  // LB: the blurred patch (37 x 40 bytes) in the hblur space
   const uint8_t* const Bpb = reinterpret_cast<const uint8_t*>(Bp);
   orbx_keypoint* const kpsf = kps + (size_t)f * kcap;  // this frame's outputs
@@ -1814,12 +1859,14 @@ __device__ __forceinline__ void ob_body(OB_KERNEL_ARGS, const uint8_t* __restric
   brief_issue(cur, R, lane);
   for (; o < oend; o += stride) {  // wave-uniform
   // ---- stage this keypoint's patch (unblurred level), reflect-101 outside ----
-  uint32_t hte = 0;
+  [[maybe_unused]] uint32_t hte = 0;  // OB_HPASS 0: the keypoint's task bytes
   if constexpr (LB) {
     brief_commit(R, &P[0][0], Bp, lane);
   } else {
     brief_commit(R, &P[0][0], lane);
+#if OB_HPASS == 0
     hte = R.ht;  // before the next keypoint's issue overwrites R
+#endif
   }
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -1833,10 +1880,51 @@ __device__ __forceinline__ void ob_body(OB_KERNEL_ARGS, const uint8_t* __restric
   // out = (sum_j k_j H(r+j-3) + 32768) >> 16 with H = sum_i k_i p(c+i-3)
   // (OpenCV's fixed-point 8U path, [18,34,48,56,48,34,18]).  The horizontal
   // pass runs once per keypoint over the patch (hblur, column-major, row
-  // pairs packed as u16 x 2); each of the 364 live samples is then 4 dword
-  // reads + 4 v_dot2_u32_u16 down its hblur column -- 64 LDS ops per keypoint
-  // instead of 21 dword reads per sample (126).  It runs before IC_Angle so
-  // its LDS writes drain while the angle and sin/cos are computed.
+  // pairs packed as 16-bit x 2: H - 32768 as i16 from the matrix cores, or H
+  // as u16 from the v_dot4 tasks of OB_HPASS 0); each of the 364 live samples
+  // is then 4 dword reads + 4 v_dot2 down its hblur column -- 64 LDS ops per
+  // keypoint instead of 21 dword reads per sample (126).  It runs before
+  // IC_Angle so its LDS writes drain while the angle and sin/cos are computed.
+  // Matrix-core pass (round 5): 9 MFMAs + 18 v_perm per keypoint replace
+  // ~130 VALU of v_dot4 tasks (BRIEF c4 0.456 -> 0.416 ms, c1 0.833 -> 0.738,
+  // c2 0.434 -> 0.393)
+#if OB_HPASS == 1
+  if constexpr (!LB) {
+    // one v_mfma_i32_16x16x32_i8 per 16 rows x 16 output columns: A = the
+    // signed patch (lane: row r0 + (lane & 15), window bytes 8 (lane >> 4) ..
+    // +7 -- one ds_read2_b32), B = hbw, D lane: rows 4 (lane >> 4) .. +3 of
+    // column lane & 15 = H - 32768 (the taps sum to 256), packed as i16 row
+    // pairs.  Blocks: rows 0..47 x hblur columns 0..47 (columns 4 qlo ..);
+    // rows >= 44 and columns >= 40 are not stored, and every window byte
+    // outside the patch or the block's taps has weight 0 (KP_PGUARD_*).
+    const int cc = me.x - me.px0;
+    const int qlo = (cc - 18) >> 2;
+    typedef int v4i __attribute__((ext_vector_type(4)));
+    const uint32_t* ab = &P[0][0] + (__mul24(lane & 15, KP_PSTRIDE) + 2 * (lane >> 4) - 2 + qlo);
+    uint32_t* hb = &hblur[wave][0][0] + (__mul24(lane & 15, KP_HSTRIDE) + 2 * (lane >> 4));
+#pragma unroll
+    for (int rb = 0; rb < 3; ++rb) {
+#pragma unroll
+      for (int cb = 0; cb < 3; ++cb) {
+        const uint32_t* a = ab + (16 * KP_PSTRIDE * rb + 4 * cb);
+        const uint64_t av = (uint64_t)a[0] | ((uint64_t)a[1] << 32);
+        const v4i h = __builtin_amdgcn_mfma_i32_16x16x32_i8((long)av, (long)hbw, (v4i){0, 0, 0, 0}, 0, 0, 0);
+        const bool st = (cb < 2 || (lane & 15) < KP_HCOLS - 32) && (rb < 2 || (lane >> 4) < 3);
+        if (st) {
+          const uint32_t p01 = __builtin_amdgcn_perm((uint32_t)h[1], (uint32_t)h[0], 0x05040100u);
+          const uint32_t p23 = __builtin_amdgcn_perm((uint32_t)h[3], (uint32_t)h[2], 0x05040100u);
+          *reinterpret_cast<uint2*>(hb + (16 * KP_HSTRIDE * cb + 8 * rb)) = make_uint2(p01, p23);
+        }
+#if OB_HPASS_GROUP == 1
+        __builtin_amdgcn_sched_barrier(0);  // one block's registers at a time (72 VGPRs)
+#endif
+      }
+#if OB_HPASS_GROUP == 3
+      __builtin_amdgcn_sched_barrier(0);
+#endif
+    }
+  }
+#else
   if constexpr (!LB) {
     // task = (row pair rp, 4-column group q): patch columns 4q..4q+3, rows
     // 2rp, 2rp+1; the 7-byte windows c-3..c+3 lie in dwords q-1..q+1
@@ -1875,6 +1963,7 @@ __device__ __forceinline__ void ob_body(OB_KERNEL_ARGS, const uint8_t* __restric
       }
     }
   }
+#endif
   // IC_Angle (:21-48) on the unblurred level (integer sums: order-free).
   // Lane (< 62) = patch row v = lane/2 - 15, half = lane & 1: five dwords of
   // the row (columns 4..23 or 24..43; the disk spans cc-15..cc+15 <= 39).
@@ -1910,6 +1999,16 @@ __device__ __forceinline__ void ob_body(OB_KERNEL_ARGS, const uint8_t* __restric
       // (ones * 255 would be a quarter-rate v_mul_lo_u32)
       const uint32_t bmask = __builtin_amdgcn_perm(0u, 0u, 0x0C0C0C0Cu + ones);
       const uint32_t I = rowp[k];
+#if OB_HPASS == 1
+      if constexpr (!LB) {
+        // signed patch bytes p - 128: each lane's sums move by -128 n and
+        // -128 sum(u + 19); after the wave sums m10 and m01 move by
+        // -128 sum u and -128 sum v over the disk, both 0 (it is symmetric)
+        s = (uint32_t)__builtin_amdgcn_sdot4((int)I, (int)ones, (int)s, false);
+        m = (uint32_t)__builtin_amdgcn_sdot4((int)I, (int)((W + 0x04040404u * k) & bmask), (int)m, false);
+        continue;
+      }
+#endif
       s = __builtin_amdgcn_udot4(I, ones, s, false);
       m = __builtin_amdgcn_udot4(I, (W + 0x04040404u * k) & bmask, m, false);
     }
@@ -1989,11 +2088,22 @@ __device__ __forceinline__ void ob_body(OB_KERNEL_ARGS, const uint8_t* __restric
       // row pairs (2k, 2k+1): taps rt..rt+6 start at the pair's low half
       // (rt even) or high half (rt odd)
       const bool odd = rt & 1;
-      uint32_t acc = __builtin_amdgcn_udot2(as_us2(v0), as_us2(odd ? KV_O0 : KV_E0), 0u, false);
+      // the rounding 32768 rides in as the first dot2's accumulator (-1 VALU
+      // per sample); <= 255 after the shift: the taps sum to 65536
+#if OB_HPASS == 1
+      // i16 H - 32768 (the MFMA pass): + 32768 * 256 restores sum k_j H_j
+      int acc = __builtin_amdgcn_sdot2(as_s2(v0), as_s2(odd ? KV_O0 : KV_E0), 32768 + (32768 << 8), false);
+      acc = __builtin_amdgcn_sdot2(as_s2(v1), as_s2(odd ? KV_O1 : KV_E1), acc, false);
+      acc = __builtin_amdgcn_sdot2(as_s2(v2), as_s2(odd ? KV_O2 : KV_E2), acc, false);
+      acc = __builtin_amdgcn_sdot2(as_s2(v3), as_s2(odd ? KV_O3 : KV_E3), acc, false);
+      t[e] = (int)((uint32_t)acc >> 16);
+#else
+      uint32_t acc = __builtin_amdgcn_udot2(as_us2(v0), as_us2(odd ? KV_O0 : KV_E0), 32768u, false);
       acc = __builtin_amdgcn_udot2(as_us2(v1), as_us2(odd ? KV_O1 : KV_E1), acc, false);
       acc = __builtin_amdgcn_udot2(as_us2(v2), as_us2(odd ? KV_O2 : KV_E2), acc, false);
       acc = __builtin_amdgcn_udot2(as_us2(v3), as_us2(odd ? KV_O3 : KV_E3), acc, false);
-      t[e] = (int)((acc + 32768u) >> 16);  // <= 255: the taps sum to 65536
+      t[e] = (int)(acc >> 16);
+#endif
     }
     words[rr] = __ballot(t[0] < t[1]);
   }
