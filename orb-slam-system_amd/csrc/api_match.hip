@@ -22,7 +22,7 @@ __global__ void k_match_gather2(const MProblem*, const MNodePair*, uint4*, uint3
 typedef int v4i_ __attribute__((ext_vector_type(4)));
 template <int NK>
 __global__ void k_match_expand2(const MProblem*, const MNodePair*, v4i_*);
-template <int NK, int RT>
+template <int NK, int RT, bool PK>
 __global__ void k_match_cand_mfma(const MProblem*, const MNodePair*, const v4i_*, uint2*, int4*,
                                   int2*);
 
@@ -96,13 +96,22 @@ void launch_match(const MProblem* d_probs, int nprob, const MNodePair* d_nps, in
         if (six_words) {
           hipLaunchKernelGGL(k_match_expand2<6>, dim3((max_n2 * ORBM_EXPAND_PER_POS(6) + 255) / 256, nnp), dim3(256), 0, s,
                              d_probs, d_nps, gx2);
-          hipLaunchKernelGGL((k_match_cand_mfma<6, MC_RT>), dim3((max_n1 + 128 * MC_RT - 1) / (128 * MC_RT), nnp), dim3(256), 0, s,
-                             d_probs, d_nps, gx2, d_cand, d_rowinfo, d_ev);
+          // positions in the accumulator while they fit its 2^MC_PB(6) slots
+          if (ORBM_FP4 && MC_PK && max_n2 <= (1 << 14))
+            hipLaunchKernelGGL((k_match_cand_mfma<6, MC_RT, ORBM_FP4 != 0>), dim3((max_n1 + 128 * MC_RT - 1) / (128 * MC_RT), nnp), dim3(256), 0, s,
+                               d_probs, d_nps, gx2, d_cand, d_rowinfo, d_ev);
+          else
+            hipLaunchKernelGGL((k_match_cand_mfma<6, MC_RT, false>), dim3((max_n1 + 128 * MC_RT - 1) / (128 * MC_RT), nnp), dim3(256), 0, s,
+                               d_probs, d_nps, gx2, d_cand, d_rowinfo, d_ev);
         } else {
           hipLaunchKernelGGL(k_match_expand2<8>, dim3((max_n2 * ORBM_EXPAND_PER_POS(8) + 255) / 256, nnp), dim3(256), 0, s,
                              d_probs, d_nps, gx2);
-          hipLaunchKernelGGL((k_match_cand_mfma<8, MC_RT>), dim3((max_n1 + 128 * MC_RT - 1) / (128 * MC_RT), nnp), dim3(256), 0, s,
-                             d_probs, d_nps, gx2, d_cand, d_rowinfo, d_ev);
+          if (ORBM_FP4 && MC_PK && max_n2 <= (1 << 13))
+            hipLaunchKernelGGL((k_match_cand_mfma<8, MC_RT, ORBM_FP4 != 0>), dim3((max_n1 + 128 * MC_RT - 1) / (128 * MC_RT), nnp), dim3(256), 0, s,
+                               d_probs, d_nps, gx2, d_cand, d_rowinfo, d_ev);
+          else
+            hipLaunchKernelGGL((k_match_cand_mfma<8, MC_RT, false>), dim3((max_n1 + 128 * MC_RT - 1) / (128 * MC_RT), nnp), dim3(256), 0, s,
+                               d_probs, d_nps, gx2, d_cand, d_rowinfo, d_ev);
         }
       } else {
         // list2 descriptors gathered into node order, then two rows per lane,

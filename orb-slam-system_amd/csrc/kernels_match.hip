@@ -690,6 +690,104 @@ __device__ __forceinline__ void mfma_tile(const v4i_ (&af)[NS], const v4i_ (&bf)
   }
 }
 
+#if ORBM_FP4
+// Positions in the accumulator (fp4 form, round 5).  With A's MX block scale
+// 2^PB every product is +-2^PB, so an accumulator started at
+// 2^23 + K 2^PB + p (p = the element's list position, < 2^PB) ends at
+// 2^23 + 2h 2^PB + p: an integer below 2^24 (2h <= 2K <= 384 for NK 6 with
+// PB 14, <= 512 for NK 8 with PB 13), exact in f32, whose bit pattern
+// 0x4B000000 + h 2^(PB+1) + p orders like (h, p) -- the key itself, with
+// no per-key VALU (the plain form spends a shift and an add per key).  The
+// per-tile start values are the lane's 16 constants plus t0 (8 v_pk_add_f32).
+// Keys become (h << 16 | p) when the row's list is written out.
+#define MC_PB(NK) ((NK) == 6 ? 14 : 13)
+#define MC_KBASE 0x4B000000u
+#ifndef MC_TOP3
+#define MC_TOP3 1 /* 1: per-lane top-3 of the tile's 16 keys, two insertions (A/B: 0 = one per key) */
+#endif
+typedef float v2f_ __attribute__((ext_vector_type(2)));
+
+template <int NS, int PB>
+__device__ __forceinline__ void mfma_tile_pk(const v4i_ (&af)[NS], const v4i_ (&bf)[NS], float t0f,
+                                             int n2, bool last, uint32_t (&L)[ORBM_T], const v16f_& cb) {
+  v16f_ ci;
+#pragma unroll
+  for (int i = 0; i < 16; i += 2) {
+    const v2f_ v = v2f_{cb[i], cb[i + 1]} + v2f_{t0f, t0f};
+    ci[i] = v[0];
+    ci[i + 1] = v[1];
+  }
+  v16f_ C = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(fp4_slot(af[0]), fp4_slot(bf[0]), ci, 4, 4,
+                                                            0, 0x7F + PB, 0, 0x7F);
+#pragma unroll
+  for (int s = 1; s < NS; ++s)
+    C = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(fp4_slot(af[s]), fp4_slot(bf[s]), C, 4, 4, 0,
+                                                        0x7F + PB, 0, 0x7F);
+  uint32_t k[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) k[i] = __float_as_uint(C[i]);
+  if (last) {  // wave-uniform: positions past the list
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+      if ((k[i] & ((1u << PB) - 1u)) >= (uint32_t)n2) k[i] = 0xFFFFFFFFu;
+  }
+#if MC_TOP3
+  // the lane's three smallest keys (two running chains of med3 insertions,
+  // then the lower half of the bitonic 6-sequence a1 a2 a3 b3 b2 b1); on
+  // these frames most tiles hold a lane with one key under its list's last
+  // entry, few a lane with three: two wave-level insertions replace up to 16
+  uint32_t a1 = min(k[0], k[1]), a2 = max(k[0], k[1]), a3 = 0xFFFFFFFFu;
+  uint32_t b1 = min(k[8], k[9]), b2 = max(k[8], k[9]), b3 = 0xFFFFFFFFu;
+#pragma unroll
+  for (int i = 2; i < 8; ++i) {
+    a3 = med3u(a2, k[i], a3);
+    a2 = med3u(a1, k[i], a2);
+    a1 = min(a1, k[i]);
+    b3 = med3u(b2, k[8 + i], b3);
+    b2 = med3u(b1, k[8 + i], b2);
+    b1 = min(b1, k[8 + i]);
+  }
+  const uint32_t l1 = min(a1, b3), l2 = min(a2, b2), l3 = min(a3, b1);
+  const uint32_t m1 = min(min(l1, l2), l3), m3 = max(max(l1, l2), l3);
+  const uint32_t m2 = med3u(l1, l2, l3);
+  if (__ballot(m1 < L[ORBM_T - 1])) {
+    topk_insert(L, m1);
+    if (__ballot(m2 < L[ORBM_T - 1])) {
+      topk_insert(L, m2);
+      if (__ballot(m3 < L[ORBM_T - 1])) {
+        // some lane has a third key under its last entry: the remaining keys
+        // (> m2; keys are unique in a lane) against the current threshold.
+        // An insertion runs in every lane once any lane needs it, so keys a
+        // lane already inserted (<= m2) become no-op keys first
+        const uint32_t l7 = L[ORBM_T - 1];
+        unsigned long long bm[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          k[i] = k[i] > m2 ? k[i] : 0xFFFFFFFFu;
+          bm[i] = __ballot(k[i] < l7);
+        }
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+          if (bm[i]) topk_insert(L, k[i]);
+      }
+    }
+  }
+#else
+  uint32_t m = min(min(min(k[0], k[1]), min(k[2], k[3])), min(min(k[4], k[5]), min(k[6], k[7])));
+  m = min(m, min(min(min(k[8], k[9]), min(k[10], k[11])), min(min(k[12], k[13]), min(k[14], k[15]))));
+  if (__ballot(m < L[ORBM_T - 1])) {
+    const uint32_t l7 = L[ORBM_T - 1];
+    unsigned long long bm[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) bm[i] = __ballot(k[i] < l7);
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+      if (bm[i]) topk_insert(L, k[i]);
+  }
+#endif
+}
+#endif
+
 // 128 * RT rows per workgroup, 32 * RT per wave: lane l holds rows
 // a0 + 32 (RT w + t) + (l & 31), t < RT, as B operands (K bits of its half
 // h = l >> 5 per step), and gets back C[position][row] for the 16 positions
@@ -699,7 +797,9 @@ __device__ __forceinline__ void mfma_tile(const v4i_ (&af)[NS], const v4i_ (&bf)
 // gx2 (L1/L2: the waves of a workgroup and the node pair's other workgroups
 // read the same tiles), one tile ahead; each fragment feeds RT MFMA chains.
 // Validity arrays are not supported (k_match_cand_rows).
-template <int NK, int RT>
+// PK (fp4 form, max n2 <= 2^MC_PB(NK)): positions in the accumulator
+// (mfma_tile_pk); otherwise keys built per element (mfma_tile)
+template <int NK, int RT, bool PK>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MC_WPE))) void k_match_cand_mfma(
     const MProblem* __restrict__ probs, const MNodePair* __restrict__ nps,
     const v4i_* __restrict__ gx2, uint2* __restrict__ cand, int4* __restrict__ rowinfo,
@@ -722,7 +822,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MC_WPE))) v
   bool act[RT], v1[RT];
   v4i_ bf[RT][NS];
   uint32_t L[RT][ORBM_T];
+#if ORBM_FP4
+  constexpr int PB = MC_PB(NK);
+  const uint32_t sent = PK ? MC_KBASE + ((uint32_t)P.dcap << (PB + 1)) : (uint32_t)P.dcap << 16;
+#else
+  static_assert(!PK, "positions in the accumulator need the fp4 form");
   const uint32_t sent = (uint32_t)P.dcap << 16;
+#endif
 #pragma unroll
   for (int t = 0; t < RT; ++t) {
     a[t] = a0 + 32 * (RT * wave + t) + c;
@@ -753,8 +859,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MC_WPE))) v
   v4i_ af[NS], an[NS];
 #if ORBM_FP4
   const v16f_ ci = fp4_acc_init<NS>();
+  // PK: element i's start value without t0: 2^23 + K 2^PB + 4h + (i & 3) + 8 (i >> 2)
+  v16f_ cb;
+#pragma unroll
+  for (int i = 0; i < 16; ++i)
+    cb[i] = (float)(8388608 + (64 * NS << PB) + 4 * h + (i & 3) + 8 * (i >> 2));
+#define MC_TILE(F, T0) \
+  (PK ? mfma_tile_pk<NS, PB>(F, bf[t], (float)(T0), n2, (T0) + 32 > n2, L[t], cb) \
+      : mfma_tile<NS>(F, bf[t], (uint32_t)(T0), n2, hoff, L[t], ci))
 #else
   const v16f_ ci = {};
+#define MC_TILE(F, T0) mfma_tile<NS>(F, bf[t], (uint32_t)(T0), n2, hoff, L[t], ci)
 #endif
 #pragma unroll
   for (int s = 0; s < NS; ++s) af[s] = n2 > 0 ? gx[(size_t)min(c, n2 - 1) * NS * 2 + 2 * s] : v4i_{0, 0, 0, 0};
@@ -764,7 +879,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MC_WPE))) v
 #pragma unroll
     for (int s = 0; s < NS; ++s) an[s] = gx[(size_t)pn * NS * 2 + 2 * s];  // next tile (clamped)
 #pragma unroll
-    for (int t = 0; t < RT; ++t) mfma_tile<NS>(af, bf[t], (uint32_t)t0, n2, hoff, L[t], ci);
+    for (int t = 0; t < RT; ++t) MC_TILE(af, t0);
 #pragma unroll
     for (int s = 0; s < NS; ++s) af[s] = an[s];
   }
@@ -776,15 +891,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MC_WPE))) v
 #pragma unroll
     for (int s = 0; s < NS; ++s) an[s] = gx[(size_t)pn * NS * 2 + 2 * s];
 #pragma unroll
-    for (int t = 0; t < RT; ++t) mfma_tile<NS>(af, bf[t], (uint32_t)t0, n2, hoff, L[t], ci);
+    for (int t = 0; t < RT; ++t) MC_TILE(af, t0);
     if (t0 + 32 >= n2) break;  // wave-uniform
     const int pf = min(t0 + 64 + c, n2 - 1);
 #pragma unroll
     for (int s = 0; s < NS; ++s) af[s] = gx[(size_t)pf * NS * 2 + 2 * s];
 #pragma unroll
-    for (int t = 0; t < RT; ++t) mfma_tile<NS>(an, bf[t], (uint32_t)(t0 + 32), n2, hoff, L[t], ci);
+    for (int t = 0; t < RT; ++t) MC_TILE(an, t0 + 32);
   }
 #endif
+#undef MC_TILE
   // merge the two halves' lists of each row (keys unique: position inside)
   if (h) {
 #pragma unroll
@@ -804,8 +920,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MC_WPE))) v
     }
     const bool full = Lt[ORBM_T - 1] < sent;
 #pragma unroll
-    for (int u = 0; u < ORBM_T; ++u)
-      if (Lt[u] >= sent) Lt[u] = 0xFFFFFFFFu;
+    for (int u = 0; u < ORBM_T; ++u) {
+#if ORBM_FP4
+      // PK: 0x4B000000 + h 2^(PB+1) + p -> h << 16 | p
+      if (PK) Lt[u] = ((Lt[u] - MC_KBASE) >> (PB + 1) << 16) | (Lt[u] & ((1u << PB) - 1u));
+#endif
+      if (Lt[u] >= (PK ? (uint32_t)P.dcap << 16 : sent)) Lt[u] = 0xFFFFFFFFu;
+    }
     if (!act[t]) continue;
     const int r = NP.row_base + a[t];
     ev[r] = make_int2(-1, 0);
@@ -825,10 +946,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MC_WPE))) v
     }
   }
 }
-template __global__ void k_match_cand_mfma<6, MC_RT>(const MProblem*, const MNodePair*, const v4i_*,
-                                                     uint2*, int4*, int2*);
-template __global__ void k_match_cand_mfma<8, MC_RT>(const MProblem*, const MNodePair*, const v4i_*,
-                                                     uint2*, int4*, int2*);
+template __global__ void k_match_cand_mfma<6, MC_RT, false>(const MProblem*, const MNodePair*, const v4i_*,
+                                                            uint2*, int4*, int2*);
+template __global__ void k_match_cand_mfma<8, MC_RT, false>(const MProblem*, const MNodePair*, const v4i_*,
+                                                            uint2*, int4*, int2*);
+#if ORBM_FP4
+template __global__ void k_match_cand_mfma<6, MC_RT, true>(const MProblem*, const MNodePair*, const v4i_*,
+                                                           uint2*, int4*, int2*);
+template __global__ void k_match_cand_mfma<8, MC_RT, true>(const MProblem*, const MNodePair*, const v4i_*,
+                                                           uint2*, int4*, int2*);
+#endif
 
 // ---------------------------------------------------------------------------
 // k_match_resolve: greedy, in list order.  unit = node pair (parallel mode)

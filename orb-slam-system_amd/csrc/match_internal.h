@@ -32,6 +32,12 @@
 #ifndef MC_WPE
 #define MC_WPE 5
 #endif
+/* k_match_cand_mfma: list positions carried in the MFMA accumulator (fp4
+ * form, lists up to 2^14 / 2^13 positions for 6 / 8 live dwords; round 5),
+ * 0 = keys built per element (A/B) */
+#ifndef MC_PK
+#define MC_PK 1
+#endif
 /* k_match_expand2 threads per list position: one per MFMA K step */
 #define ORBM_EXPAND_PER_POS(NK) (ORBM_FP4 ? (NK) / 2 : (NK))
 

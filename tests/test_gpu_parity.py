@@ -487,3 +487,55 @@ def test_search_by_bow_large_kf2(gpu, oracle, n2):
         rm, rnm = oracle.search_by_bow(kf1, kf2, ratio, True)
         assert nm == rnm and np.array_equal(m, rm), ratio
         assert nm > 100  # the resolver commits at real density
+
+
+@pytest.mark.parametrize("n2,six", [(16384, True), (16385, True), (8192, False), (8193, False)])
+def test_search_by_bow_accumulator_position_bounds(gpu, oracle, n2, six):
+    """The candidate kernel's positions-in-the-accumulator keys (round 5:
+    2^14 list positions with 6 live descriptor dwords, 2^13 with 8) at their
+    bound and one past it (the per-element key form), with zero tails (the
+    728-entry pattern's bytes 24..31) or full descriptors."""
+    rng = np.random.default_rng(n2 + 7 * six)
+    n1 = 300
+    d2 = rng.integers(0, 256, (n2, 32), dtype=np.uint8)
+    if six:
+        d2[:, 24:] = 0
+    d1 = _correlated(rng, d2[rng.integers(0, n2, n1)], rng.integers(0, 40, n1))
+    if six:
+        d1[:, 24:] = 0
+    one = lambda d: dict(desc=d, angle=rng.uniform(0, 360, len(d)).astype(np.float32), valid=None,
+                         node_id=np.array([5], np.uint32), off=np.array([0, len(d)], np.uint32),
+                         feat=np.arange(len(d), dtype=np.uint32))
+    kf1, kf2 = one(d1), one(d2)
+    for ratio in (0.75, 1.0):
+        m, nm = gpu.search_by_bow(kf1, kf2, ratio, True)
+        rm, rnm = oracle.search_by_bow(kf1, kf2, ratio, True)
+        assert nm == rnm and np.array_equal(m, rm), ratio
+        assert nm > 50
+
+
+def test_search_by_bow_complement_distances(gpu, oracle):
+    """Distance 256 (exact complements, 8 live dwords) under a ratio whose
+    candidate cap is 257, so such keys enter the lists and decide the ratio
+    test: the largest value the accumulator-position key takes
+    (2^23 + 2^22 + position).  Node j of KF1 holds feature j; node j of KF2
+    a copy of it with 2-45 flipped bits, its complement and the complement
+    with one bit restored (distances d, 256, 255)."""
+    rng = np.random.default_rng(256)
+    n1 = 300
+    d1 = rng.integers(0, 256, (n1, 32), dtype=np.uint8)
+    near = _correlated(rng, d1, rng.integers(2, 46, n1))
+    comp = ~d1
+    comp1 = comp.copy()
+    comp1[:, 0] ^= 1
+    d2 = np.stack([near, comp, comp1], axis=1).reshape(3 * n1, 32)
+    ids = np.arange(n1, dtype=np.uint32) * 2 + 1
+    kf1 = dict(desc=d1, angle=rng.uniform(0, 360, n1).astype(np.float32), valid=None, node_id=ids,
+               off=np.arange(n1 + 1, dtype=np.uint32), feat=np.arange(n1, dtype=np.uint32))
+    kf2 = dict(desc=d2, angle=rng.uniform(0, 360, 3 * n1).astype(np.float32), valid=None, node_id=ids,
+               off=(3 * np.arange(n1 + 1)).astype(np.uint32), feat=np.arange(3 * n1, dtype=np.uint32))
+    for ratio in (0.1, 0.15, 0.75):
+        m, nm = gpu.search_by_bow(kf1, kf2, ratio, False)
+        rm, rnm = oracle.search_by_bow(kf1, kf2, ratio, False)
+        assert nm == rnm and np.array_equal(m, rm), ratio
+        assert nm > 0
