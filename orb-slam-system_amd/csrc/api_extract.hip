@@ -181,8 +181,12 @@ extern "C" int orbx_plan_create(const orbx_params* prm, int width, int height, i
   if (const char* e = getenv("ORBX_DEBUG_OVERLAP")) p->overlap = atoi(e); /* FAST level 0 beside the pyramid */
 #endif
   p->fs_ccap = FS_CCAP;
+  bool ccap_fixed = false;
   /* testing only: a smaller FAST corner list, so the overflow path runs */
-  if (const char* e = getenv("ORBX_DEBUG_CCAP")) p->fs_ccap = std::max(0, std::min(FS_CCAP, atoi(e)));
+  if (const char* e = getenv("ORBX_DEBUG_CCAP")) {
+    p->fs_ccap = std::max(0, std::min(FS_CCAP, atoi(e)));
+    ccap_fixed = true;
+  }
   int rc = plan_geometry(*prm, width, height, p->P);
   if (rc) { delete p; return rc; }
   const Plan& P = p->P;
@@ -267,12 +271,33 @@ extern "C" int orbx_plan_create(const orbx_params* prm, int width, int height, i
     p->fs_tmaxh = std::max(P.strip_max_h, 7);
     p->fs_qcap = 0;
     p->fs_mcells = std::max(P.strip_max_cells, 1);
-    /* tile + band-row strength map + counts; the NMS masks reuse the tile
+    /* tile + band-row strength map + counts + cell slots; the NMS masks reuse the tile
      * when they fit (k_fast_strips) */
     const size_t tile = (size_t)p->fs_tpitch * p->fs_tmaxh;
     const size_t masks = 16 * (size_t)p->fs_mcells * (p->fs_tmaxh - 6);
-    p->fs_lds = tile + (size_t)p->fs_tpitch * (p->fs_tmaxh - 6) + 4 * (size_t)((p->fs_mcells + 3) & ~3) +
-                (masks <= tile ? 0 : masks);
+    const size_t fixed = tile + (size_t)p->fs_tpitch * (p->fs_tmaxh - 6) + 8 * (size_t)((p->fs_mcells + 3) & ~3) +
+                         (masks <= tile ? 0 : masks);
+    const auto lds_of = [&](int ccap) { return fixed + 2 * (size_t)((ccap + 3) & ~3); };
+    if (!ccap_fixed) {
+      /* the corner list (FS_CCAP entries, ~60 used per strip at 1080p) is
+       * shortened, down to FS_CCAP_MIN, when that fits one more workgroup per
+       * CU, up to the 6 that k_fast_strips' 75 VGPRs allow (LDS per
+       * workgroup in 1-KB steps -- conservative -- plus the kernel's static
+       * LDS): 640x480 x 8 levels (40-row strips) 5 -> 6 workgroups, 830
+       * entries, FAST -8 %, no strip over the list on the bench frames; a
+       * strip over it takes the strength-map scan (round 5) */
+      hipFuncAttributes fa;
+      const size_t st = hipFuncGetAttributes(&fa, (const void*)k_fast_strips_p288) == hipSuccess ? fa.sharedSizeBytes : 4096;
+      const auto wgs = [&](size_t lds) { return std::min<size_t>(6, 163840 / (((lds + st) + 1023) & ~(size_t)1023)); };
+      const size_t w0 = wgs(lds_of(FS_CCAP));
+      if (w0 < 6) {
+        int best = FS_CCAP;
+        for (int c = FS_CCAP - 2; c >= FS_CCAP_MIN; c -= 2)
+          if (wgs(lds_of(c)) > w0) { best = c; break; }
+        p->fs_ccap = best;
+      }
+    }
+    p->fs_lds = lds_of(p->fs_ccap);
 #ifdef FS_LDS_PAD  // profiling variant: occupancy sensitivity of k_fast_strips
     p->fs_lds += FS_LDS_PAD;
 #endif

@@ -954,14 +954,16 @@ __device__ __forceinline__ void fs_kernel(
   uint8_t* tile = reinterpret_cast<uint8_t*>(sm);                    // tpitch * tmax_h
   uint8_t* amap_mem = tile + tpitch * tmax_h;                         // tpitch * (tmax_h - 6)
   int* cnt = reinterpret_cast<int*>(amap_mem + tpitch * (tmax_h - 6));  // mcells
+  int* cslot = cnt + ((mcells + 3) & ~3);                               // mcells
+  // corners at t_lo (A > t_lo), any order: ccap entries (the plan sizes it,
+  // orbx_internal.h FS_CCAP)
+  uint16_t* clist = reinterpret_cast<uint16_t*>(cslot + ((mcells + 3) & ~3));
   const bool masks_in_tile = 16 * mcells * (tmax_h - 6) <= tpitch * tmax_h;
   unsigned long long* mask = masks_in_tile ? reinterpret_cast<unsigned long long*>(tile)
-                                           : reinterpret_cast<unsigned long long*>(cnt + ((mcells + 3) & ~3));
+                                           : reinterpret_cast<unsigned long long*>(clist + ((ccap + 3) & ~3));
   unsigned long long* mask2 = mask + mcells * (tmax_h - 6);
   __shared__ uint16_t wlist1[FS_NW][FS_L1CAP];
   __shared__ uint16_t wlist2[FS_NW][FS_L2CAP];
-  __shared__ uint16_t clist[FS_CCAP];  // corners at t_lo (A > t_lo), any order
-  __shared__ int cslot[ORBX_STRIP_MAXCELLS];
   __shared__ int ncorner;
   const int tid = threadIdx.x;
   // plain grid: with 8 strip columns at 1080p level 0, XCD (f*S + s) % 8 is
@@ -1023,7 +1025,7 @@ __device__ __forceinline__ void fs_kernel(
 #define FS_KERNEL_PASS \
   frames, fstride, rstride, pyr, pstride, LA, cells, strips, slots, slot_stride, ccount, ncells, ini_th, min_th, tpitch, tmax_h, mcells, ccap, ovf, strip0, dbg
 
-#ifdef FS_WPE  // profiling variant: occupancy target
+#ifdef FS_WPE  // profiling variant: occupancy target (7 measured +20 % at c4: 72 VGPRs)
 #define FS_ATTR __attribute__((amdgpu_waves_per_eu(FS_WPE)))
 #else
 #define FS_ATTR

@@ -103,7 +103,11 @@ struct StereoArgs {
 #define FS_NT 256 /* threads per k_fast_strips workgroup (one strip) */
 #endif
 #ifndef FS_CCAP
-#define FS_CCAP 1024 /* per-strip corner list (overflow falls back to a map scan) */
+#define FS_CCAP 1024 /* per-strip corner list (overflow falls back to a map scan); the plan may take
+                        * fewer entries (>= FS_CCAP_MIN) where that buys a workgroup per CU */
+#ifndef FS_CCAP_MIN
+#define FS_CCAP_MIN 384
+#endif
 #endif
 /* d_err[ORBX_ERRW_FAST_OVF]: strips whose corner list overflowed (debug counter) */
 #define ORBX_ERRW_FAST_OVF 1
