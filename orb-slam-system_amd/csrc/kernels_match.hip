@@ -805,7 +805,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MC_WPE))) v
     const v4i_* __restrict__ gx2, uint2* __restrict__ cand, int4* __restrict__ rowinfo,
     int2* __restrict__ ev) {
   static_assert(NK == 6 || NK == 8, "6 or 8 live descriptor dwords");
-  __shared__ uint32_t ml[4][RT][ORBM_T][32];  // upper halves' lists
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int h = lane >> 5, c = lane & 31;
@@ -901,21 +900,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MC_WPE))) v
   }
 #endif
 #undef MC_TILE
-  // merge the two halves' lists of each row (keys unique: position inside)
-  if (h) {
+  // merge the two halves' lists of each row (keys unique: position inside):
+  // lane c takes lane c + 32's list by cross-lane reads, so the kernel holds
+  // no LDS and can share a CU with the extraction kernels of the next step
+  // (k_pyramid leaves VGPRs but no LDS)
+  uint32_t up[RT][ORBM_T];
 #pragma unroll
-    for (int t = 0; t < RT; ++t)
+  for (int t = 0; t < RT; ++t)
 #pragma unroll
-      for (int u = 0; u < ORBM_T; ++u) ml[wave][t][u][c] = L[t][u];
-  }
-  __syncthreads();
+    for (int u = 0; u < ORBM_T; ++u) up[t][u] = (uint32_t)__shfl_down((int)L[t][u], 32, 64);
   if (h) return;
 #pragma unroll
   for (int t = 0; t < RT; ++t) {
     uint32_t (&Lt)[ORBM_T] = L[t];
 #pragma unroll
     for (int u = 0; u < ORBM_T; ++u) {
-      const uint32_t kk = ml[wave][t][u][c];
+      const uint32_t kk = up[t][u];
       if (__ballot(kk < Lt[ORBM_T - 1])) topk_insert(Lt, kk);
     }
     const bool full = Lt[ORBM_T - 1] < sent;
