@@ -181,11 +181,11 @@ extern "C" int orbx_plan_create(const orbx_params* prm, int width, int height, i
   if (const char* e = getenv("ORBX_DEBUG_OVERLAP")) p->overlap = atoi(e); /* FAST level 0 beside the pyramid */
 #endif
   p->fs_ccap = FS_CCAP;
-  bool ccap_fixed = false;
-  /* testing only: a smaller FAST corner list, so the overflow path runs */
+  /* testing only: a smaller FAST corner list, so the overflow path runs
+   * (one launch group, this list length) */
   if (const char* e = getenv("ORBX_DEBUG_CCAP")) {
     p->fs_ccap = std::max(0, std::min(FS_CCAP, atoi(e)));
-    ccap_fixed = true;
+    p->ccap_fixed_dbg = true;
   }
   int rc = plan_geometry(*prm, width, height, p->P);
   if (rc) { delete p; return rc; }
@@ -265,43 +265,80 @@ extern "C" int orbx_plan_create(const orbx_params* prm, int width, int height, i
     const double patch_px = (double)P.params.nfeatures * (KP_PATCH_ROWS * KP_PATCH_COLS);
     p->lb_auto = patch_px > ORBX_LB_RATIO * (double)P.geo.pixels ? 1 : 0;
   }
-  // FAST strip LDS: tile + strength map + row masks + counts
+  // FAST strip LDS: tile + strength map + row masks + counts + cell slots +
+  // corner list, per launch group
   {
     p->fs_tpitch = (15 + P.strip_max_w + 8 + 15) & ~15; /* lead <= 15, row reads up to +8 */
-    p->fs_tmaxh = std::max(P.strip_max_h, 7);
-    p->fs_qcap = 0;
-    p->fs_mcells = std::max(P.strip_max_cells, 1);
-    /* tile + band-row strength map + counts + cell slots; the NMS masks reuse the tile
-     * when they fit (k_fast_strips) */
-    const size_t tile = (size_t)p->fs_tpitch * p->fs_tmaxh;
-    const size_t masks = 16 * (size_t)p->fs_mcells * (p->fs_tmaxh - 6);
-    const size_t fixed = tile + (size_t)p->fs_tpitch * (p->fs_tmaxh - 6) + 8 * (size_t)((p->fs_mcells + 3) & ~3) +
-                         (masks <= tile ? 0 : masks);
-    const auto lds_of = [&](int ccap) { return fixed + 2 * (size_t)((ccap + 3) & ~3); };
-    if (!ccap_fixed) {
-      /* the corner list (FS_CCAP entries, ~60 used per strip at 1080p) is
-       * shortened, down to FS_CCAP_MIN, when that fits one more workgroup per
-       * CU, up to the 6 that k_fast_strips' 75 VGPRs allow (LDS per
-       * workgroup in 1-KB steps -- conservative -- plus the kernel's static
-       * LDS): 640x480 x 8 levels (40-row strips) 5 -> 6 workgroups, 830
-       * entries, FAST -8 %, no strip over the list on the bench frames; a
-       * strip over it takes the strength-map scan (round 5) */
-      hipFuncAttributes fa;
-      const size_t st = hipFuncGetAttributes(&fa, (const void*)k_fast_strips_p288) == hipSuccess ? fa.sharedSizeBytes : 4096;
-      const auto wgs = [&](size_t lds) { return std::min<size_t>(6, 163840 / (((lds + st) + 1023) & ~(size_t)1023)); };
-      const size_t w0 = wgs(lds_of(FS_CCAP));
-      if (w0 < 6) {
-        int best = FS_CCAP;
-        for (int c = FS_CCAP - 2; c >= FS_CCAP_MIN; c -= 2)
-          if (wgs(lds_of(c)) > w0) { best = c; break; }
-        p->fs_ccap = best;
-      }
+    hipFuncAttributes fa;
+    const size_t st = hipFuncGetAttributes(&fa, (const void*)k_fast_strips_p288) == hipSuccess ? fa.sharedSizeBytes : 4096;
+    /* dynamic LDS of a workgroup (the NMS masks reuse the tile when they fit,
+     * k_fast_strips), and the workgroups per CU it leaves: up to the 6 that
+     * k_fast_strips' 75 VGPRs allow, LDS counted in 1-KB steps (conservative)
+     * with the kernel's static LDS */
+    const auto lds_for = [&](int tmaxh, int mcells, int ccap) {
+      const size_t tile = (size_t)p->fs_tpitch * tmaxh;
+      const size_t masks = 16 * (size_t)mcells * (tmaxh - 6);
+      return tile + (size_t)p->fs_tpitch * (tmaxh - 6) + 8 * (size_t)((mcells + 3) & ~3) +
+             (masks <= tile ? 0 : masks) + 2 * (size_t)((ccap + 3) & ~3);
+    };
+    const auto wgs = [&](size_t lds) { return std::min<size_t>(6, 163840 / (((lds + st) + 1023) & ~(size_t)1023)); };
+    const int mcells = std::max(P.strip_max_cells, 1);
+    /* When the tallest strip keeps even a shortened corner list below 6
+     * workgroups per CU, the strips no taller than hA (6 workgroups with the
+     * whole list) go first and the taller ones (a few small levels with
+     * taller cells: KITTI levels 5-6 have 44-46-row strips, 37-39 elsewhere)
+     * behind them, in a second launch: they no longer set every strip's LDS
+     * (round 5: c5 FAST 0.649 -> 0.616 ms).  Where a shortened list reaches
+     * 6 for all strips, one launch stays (640x480: a second launch for its
+     * ten 40-row strips measured +3.5 %).  Strip order changes no result:
+     * each strip writes its own cells. */
+    int hA = 0;
+    for (const StripInfo& si : P.strips)
+      if (wgs(lds_for(std::max(si.h, 7), mcells, FS_CCAP)) >= 6) hA = std::max(hA, si.h);
+    Plan& PM = p->P;
+    const int tallest = std::max(P.strip_max_h, 7);
+    const bool one_fits = wgs(lds_for(tallest, mcells, FS_CCAP_MIN)) >= 6;
+    if (hA > 0 && hA < P.strip_max_h && !one_fits && !p->ccap_fixed_dbg) {
+      std::stable_partition(PM.strips.begin(), PM.strips.end(), [&](const StripInfo& si) { return si.h <= hA; });
+      int na = 0;
+      while (na < (int)PM.strips.size() && PM.strips[na].h <= hA) ++na;
+      PM.nstrips_l0 = 0;
+      while (PM.nstrips_l0 < na && PM.strips[PM.nstrips_l0].level == 0) ++PM.nstrips_l0;
+      p->fs_ngrp = 2;
+      p->fs_grp[0].begin = 0;
+      p->fs_grp[0].end = na;
+      p->fs_grp[0].tmaxh = std::max(hA, 7);
+      p->fs_grp[1].begin = na;
+      p->fs_grp[1].end = (int)PM.strips.size();
+      p->fs_grp[1].tmaxh = tallest;
+    } else {
+      p->fs_ngrp = 1;
+      p->fs_grp[0].begin = 0;
+      p->fs_grp[0].end = (int)PM.strips.size();
+      p->fs_grp[0].tmaxh = tallest;
     }
-    p->fs_lds = lds_of(p->fs_ccap);
+    for (int g = 0; g < p->fs_ngrp; ++g) {
+      orbx_plan::FsGroup& G = p->fs_grp[g];
+      G.mcells = 1;
+      for (int k = G.begin; k < G.end; ++k) G.mcells = std::max(G.mcells, PM.strips[k].ncells);
+      G.ccap = p->fs_ccap;
+      if (!p->ccap_fixed_dbg) {
+        /* the corner list (FS_CCAP entries, ~60 used per strip at 1080p) is
+         * shortened, down to FS_CCAP_MIN, when that fits one more workgroup
+         * per CU: 640x480 x 8 levels (40-row strips) 5 -> 6 workgroups, 830
+         * entries, FAST -8 %, no strip over the list on the bench frames; a
+         * strip over it takes the strength-map scan (round 5) */
+        const size_t w0 = wgs(lds_for(G.tmaxh, G.mcells, FS_CCAP));
+        if (w0 < 6)
+          for (int c = FS_CCAP - 2; c >= FS_CCAP_MIN; c -= 2)
+            if (wgs(lds_for(G.tmaxh, G.mcells, c)) > w0) { G.ccap = c; break; }
+      }
+      G.lds = lds_for(G.tmaxh, G.mcells, G.ccap);
 #ifdef FS_LDS_PAD  // profiling variant: occupancy sensitivity of k_fast_strips
-    p->fs_lds += FS_LDS_PAD;
+      G.lds += FS_LDS_PAD;
 #endif
-    if (p->fs_lds > 150 * 1024) { plan_free(p); return ORBX_ERR_UNSUPPORTED; }
+      if (G.lds > 150 * 1024) { plan_free(p); return ORBX_ERR_UNSUPPORTED; }
+    }
   }
   hipStream_t us = p->stream;
   if (upload(&p->d_lv, P.levels, us) || upload(&p->d_cells, P.cells, us) ||
@@ -380,22 +417,23 @@ static int extract_pass(orbx_plan* p, const uint8_t* frames, int n, size_t fstri
   int32_t* const d_qnode = p->d_qnode + f0 * p->qk_stride;
   uint32_t* const d_qout = p->d_qout + f0 * p->qout_stride;
   int* const d_lcount = p->d_lcount + f0 * (size_t)L;
-  auto fast_launch = [&](int strip0, int nstrips, hipStream_t st) {
-    if (nstrips <= 0) return;
-    hipLaunchKernelGGL(p->fs_tpitch == 288 ? k_fast_strips_p288 : k_fast_strips, dim3((unsigned)nstrips, n), dim3(FS_NT), p->fs_lds + p->pad_fast, st,
+  // strips [strip0, strip1) of launch group g
+  auto fast_launch = [&](int g, int strip0, int strip1, hipStream_t st) {
+    if (strip1 <= strip0) return;
+    const orbx_plan::FsGroup& G = p->fs_grp[g];
+    hipLaunchKernelGGL(p->fs_tpitch == 288 ? k_fast_strips_p288 : k_fast_strips, dim3((unsigned)(strip1 - strip0), n), dim3(FS_NT), G.lds + p->pad_fast, st,
                        frames, fstride, rstride, d_pyr, p->pyr_stride, p->largs, p->d_cells,
                        p->d_strips, d_slots, p->slot_stride, d_ccount, P.ncells, P.ini_th,
-                       P.min_th, p->fs_tpitch, p->fs_tmaxh, p->fs_mcells, p->fs_ccap,
+                       P.min_th, p->fs_tpitch, G.tmaxh, G.mcells, G.ccap,
                        p->d_err + ORBX_ERRW_FAST_OVF, strip0, p->dbg);
   };
-  const int nstrips = (int)P.strips.size();
   const bool overlap = p->overlap && p->s_aux && P.nstrips_l0 > 0;
   if (overlap) {
     // FAST on level 0 (which needs no pyramid) runs on the auxiliary stream
     // beside the pyramid kernel; the other levels' strips follow the pyramid
     if (hipEventRecord(p->ev_aux0, s) != hipSuccess || hipStreamWaitEvent(p->s_aux, p->ev_aux0, 0) != hipSuccess)
       return ORBX_ERR_HIP;
-    fast_launch(0, P.nstrips_l0, p->s_aux);
+    fast_launch(0, 0, P.nstrips_l0, p->s_aux);  // level 0's strips lead group 0
     if (hipEventRecord(p->ev_aux1, p->s_aux) != hipSuccess) return ORBX_ERR_HIP;
   }
   // K1 pyramid: the tile chain (many small workgroups per frame; the
@@ -418,12 +456,9 @@ static int extract_pass(orbx_plan* p, const uint8_t* frames, int n, size_t fstri
   if (p->ev_after_pyr && hipEventRecord(p->ev_after_pyr, s) != hipSuccess) return ORBX_ERR_HIP;
   // K2 FAST cells
   p->timer.begin(ORBX_STAGE_FAST, s);
-  if (overlap) {
-    fast_launch(P.nstrips_l0, nstrips - P.nstrips_l0, s);
-    if (hipStreamWaitEvent(s, p->ev_aux1, 0) != hipSuccess) return ORBX_ERR_HIP;
-  } else {
-    fast_launch(0, nstrips, s);
-  }
+  for (int g = 0; g < p->fs_ngrp; ++g)
+    fast_launch(g, overlap && g == 0 ? P.nstrips_l0 : p->fs_grp[g].begin, p->fs_grp[g].end, s);
+  if (overlap && hipStreamWaitEvent(s, p->ev_aux1, 0) != hipSuccess) return ORBX_ERR_HIP;
   p->timer.end(ORBX_STAGE_FAST, s);
   if (p->dbg && p->dbg < 20) return ORBX_OK; /* phase probe: later stages would read partial results */
   // level-blur mode: the 7x7 Gaussian of every unique level (the stage runs

@@ -17,8 +17,15 @@ struct orbx_plan {
   LevelInfo* d_lv = nullptr;
   CellInfo* d_cells = nullptr;
   StripInfo* d_strips = nullptr;
-  int fs_tpitch = 0, fs_tmaxh = 0, fs_qcap = 0, fs_mcells = 0;
-  size_t fs_lds = 0;
+  int fs_tpitch = 0;
+  /* k_fast_strips launches: strips [begin, end) of the (height-partitioned)
+   * strip table with their tile rows, cells, corner-list entries and LDS */
+  struct FsGroup {
+    int begin = 0, end = 0, tmaxh = 7, mcells = 1, ccap = 0;
+    size_t lds = 0;
+  };
+  FsGroup fs_grp[2];
+  int fs_ngrp = 1;
   int32_t *d_xofs = nullptr, *d_xofs1 = nullptr, *d_yofs = nullptr;
   int32_t *d_pyr_xs = nullptr, *d_pyr_ys = nullptr, *d_pyr_bo = nullptr;
   uint32_t* d_pyr_blob = nullptr;
@@ -41,7 +48,8 @@ struct orbx_plan {
   /* ORBX_DEBUG_LDSPAD=pyr,fast,brief: extra dynamic LDS per workgroup
    * (occupancy probes: room for other streams' kernels), profiling only */
   int pad_pyr = 0, pad_fast = 0, pad_brief = 0;
-  int fs_ccap = 0; /* FAST per-strip corner list entries used (FS_CCAP; ORBX_DEBUG_CCAP lowers it) */
+  int fs_ccap = 0; /* FAST per-strip corner list entries (FS_CCAP; ORBX_DEBUG_CCAP fixes a lower one) */
+  bool ccap_fixed_dbg = false; /* ORBX_DEBUG_CCAP set: one launch group, that list length */
   int chunk = 0;  /* frames per extraction pass (0 = the whole batch in one pass) */
   hipEvent_t ev_after_pyr = nullptr; /* recorded after the pyramid launch when set (orbx_extract) */
   int overlap = 0; /* FAST on level 0 beside the pyramid on s_aux */
