@@ -1212,6 +1212,9 @@ __device__ __forceinline__ void qt_body(QT_KERNEL_ARGS) {
 
   int newS = 0;
   for (int pass = 0;; ++pass) {
+#ifdef QT_PROBE_MAXPASS  // profiling only: stop after this many passes (wrong keypoints)
+    if (pass >= QT_PROBE_MAXPASS) break;
+#endif
     if (pass >= ORBX_QT_MAX_PASSES) {
       if (tid == 0) atomicOr(err, ORBX_DEVERR_QUADTREE);
       newS = 0;
