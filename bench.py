@@ -95,6 +95,9 @@ def parse():
     ap.add_argument("--match-priority", choices=["high", "low"], default="high",
                     help="pipelined step: the matcher's stream above the extraction streams (high) "
                          "or below them (low: its kernels fill the slots extraction leaves)")
+    ap.add_argument("--xch-stream", choices=["extract", "match", "own"], default="match",
+                    help="N GPUs, pipelined step: the stream the boundary all-gather is issued on "
+                         "(the first sub-batch's extraction stream, the matcher's, or its own)")
     ap.add_argument("--match-whole", action="store_true",
                     help="with --split: match the whole batch after every sub-batch is extracted "
                          "(default: sub-batch j is matched as soon as it and its predecessor frame exist)")
@@ -549,10 +552,26 @@ def host_fed_leg(torch, orbx, plan, mp, wl, args, dev, ref_counts, steps=6, warm
 
 
 # --------------------------------------------------------------------------- distributed
+_BENCH_OUT = None  # stdout for the bench line once a process group exists (dist_setup)
+
+
+# hardware queues per process for a multi-rank run: the pipelined step
+# drives the first sub-batch's extraction, the others', the matcher's and
+# RCCL's own stream at once; with the box's 4 queues RCCL's stream shares
+# one with an extraction stream and serialises behind it (one-rank RCCL
+# rehearsal, c4: 2.60 -> 3.01 ms per step at 4 queues, 2.72 at 8)
+MULTI_HW_QUEUES = 8
+
+
 def dist_setup(args):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world > 1 or os.environ.get("ORBX_BENCH_RCCL1") == "1":
+        # read once by the HIP runtime when it initialises (below: torch)
+        cur = os.environ.get("GPU_MAX_HW_QUEUES", "")
+        if not cur.isdigit() or int(cur) < MULTI_HW_QUEUES:
+            os.environ["GPU_MAX_HW_QUEUES"] = str(MULTI_HW_QUEUES)
     import torch
     import torch.distributed as dist
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus and not (world == 1 and args.gpus == 1):
@@ -560,9 +579,26 @@ def dist_setup(args):
     if _share_gpu():
         local = 0
     torch.cuda.set_device(local)
-    if world > 1:
+    # ORBX_BENCH_RCCL1=1 (rehearsal on a one-GPU box): a one-rank RCCL process
+    # group, so the N-GPU code path -- the boundary all-gather in every step,
+    # the barriers, the max-over-ranks time -- runs through RCCL; rank 0 then
+    # takes its own previous step's last frame from the gathered records, the
+    # same predecessor the single-process copy gives
+    rehearsal = world == 1 and os.environ.get("ORBX_BENCH_RCCL1") == "1"
+    if world > 1 or rehearsal:
+        # RCCL writes its version banner to fd 1: the process's fd 1 goes to
+        # stderr from here on and the bench line to a private copy of stdout,
+        # so stdout carries the one JSON line the driver reads
+        global _BENCH_OUT
+        _BENCH_OUT = os.fdopen(os.dup(1), "w")
+        sys.stdout.flush()
+        os.dup2(2, 1)
         import datetime
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if rehearsal:
+            os.environ.setdefault("MASTER_PORT", "29517")
+            os.environ.setdefault("RANK", "0")
+            os.environ.setdefault("WORLD_SIZE", "1")
         # collective timeout: a rank that stops answering makes the
         # others fail (non-zero exit; launch_ranks then stops the siblings)
         # instead of hanging the job
@@ -581,7 +617,7 @@ def dist_record(torch, dist, world, local):
     props = torch.cuda.get_device_properties(local)
     me = {"local_rank": local, "device": props.name,
           "uuid": str(getattr(props, "uuid", "")), "pci_bus": getattr(props, "pci_bus_id", None)}
-    if world == 1 or not dist.is_initialized():
+    if not dist.is_initialized():
         return {"backend": "none (single process)", "world_size": 1, "ranks": [me]}
     ranks = [None] * dist.get_world_size()
     dist.all_gather_object(ranks, me)
@@ -594,7 +630,7 @@ def xch_device(torch, dev):
 
 
 def finish_time(torch, dist, world, dev, el):
-    if world > 1:
+    if dist.is_initialized():
         t = torch.tensor([el], dtype=torch.float64, device=xch_device(torch, dev))
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
@@ -604,6 +640,7 @@ def finish_time(torch, dist, world, dev, el):
 # --------------------------------------------------------------------------- mono workloads
 def main_mono(args, wl):
     torch, dist, world, rank, local = dist_setup(args)
+    multi = dist.is_initialized()  # N ranks, or the one-rank RCCL rehearsal
     import orbx
     from orbx.dist import BoundaryExchange, shard_first_frame
 
@@ -627,13 +664,13 @@ def main_mono(args, wl):
         # slot 0 <- the predecessor of this step's first frame: on 1 GPU the
         # previous step's last frame; frame-sharded over N GPUs the previous
         # rank's last frame of this step, via an RCCL all-gather (orbx.dist)
-        if match and world == 1:
+        if match and not multi:
             kps[0].copy_(kps[B])
             desc[0].copy_(desc[B])
             counts[0:1].copy_(counts[B:B + 1])
         plan.extract(frames, out=(kps[1:], desc[1:], counts[1:]))
         if match:
-            if world > 1:
+            if multi:
                 xch.ring_step(dist, rank, (kps[B], desc[B], counts[B:B + 1]),
                               (kps[0], desc[0], counts[0:1]))
             mp.match(B, kps[1:], desc[1:], counts[1:], kps, desc, counts, args.nnratio, True)
@@ -671,6 +708,7 @@ def main_mono(args, wl):
                 (torch.zeros_like(kps), torch.zeros_like(desc), torch.zeros_like(counts))]
         ev_x = [torch.cuda.Event(), torch.cuda.Event()]
         ev_m = [torch.cuda.Event(), torch.cuda.Event()]
+        sxch = torch.cuda.Stream(device=dev, priority=xp) if multi and args.xch_stream == "own" else None
         it = [0]
 
         def pipe():
@@ -685,7 +723,7 @@ def main_mono(args, wl):
             (k_i, d_i, c_i), (k_j, d_j, c_j) = bufs[i], bufs[1 - i]
             with torch.cuda.stream(sa):
                 sa.wait_event(ev_m[i])  # the matcher of two steps ago read buffer i
-                if world == 1:
+                if not multi:
                     k_i[0].copy_(k_j[B])
                     d_i[0].copy_(d_j[B])
                     c_i[0:1].copy_(c_j[B:B + 1])
@@ -697,12 +735,25 @@ def main_mono(args, wl):
                     subplans[j].extract(frames[j * sub:(j + 1) * sub], stream=sx[j],
                                         out=(k_i[lo:hi], d_i[lo:hi], c_i[lo:hi]))
                     ev_s[j].record(sx[j])
+            # the boundary exchange (N GPUs): this step's last frame (slot B, the
+            # last sub-batch's) to every rank, slot 0 <- its predecessor; on the
+            # stream --xch-stream names (the matcher's: after the last
+            # sub-batch, in order before the matches; its own: after the last
+            # sub-batch and the matches of two steps ago, which read slot 0)
+            # (sa waits for every sub-batch in any case: the next step's
+            # sub-batches then start together -- left free to drift apart they
+            # run staggered, which measured slower)
+            xs = sb if multi and args.xch_stream == "match" else sxch if sxch is not None else sa
             with torch.cuda.stream(sa):
                 for j in range(1, S):
                     sa.wait_event(ev_s[j])
-                if world > 1:
+            with torch.cuda.stream(xs):
+                if xs is not sa:
+                    xs.wait_event(ev_s[S - 1])
+                    xs.wait_event(ev_m[i])
+                if multi:
                     xch.ring_step(dist, rank, (k_i[B], d_i[B], c_i[B:B + 1]), (k_i[0], d_i[0], c_i[0:1]))
-                ev_x[i].record(sa)
+                ev_x[i].record(xs)
             with torch.cuda.stream(sb):
                 if S == 1 or args.match_whole:
                     sb.wait_event(ev_x[i])
@@ -713,7 +764,7 @@ def main_mono(args, wl):
                     # previous step (1 GPU) or the ring exchange (N GPUs)
                     for j in range(S):
                         lo, hi = 1 + j * sub, 1 + (j + 1) * sub
-                        sb.wait_event(ev_x[i] if (j == 0 and world > 1) else ev_s[j])
+                        sb.wait_event(ev_x[i] if (j == 0 and multi) else ev_s[j])
                         if j:
                             sb.wait_event(ev_s[j - 1])
                         mp.match(sub, k_i[lo:hi], d_i[lo:hi], c_i[lo:hi], k_i[lo - 1:hi - 1],
@@ -728,14 +779,14 @@ def main_mono(args, wl):
     plan.set_timing(True)
     if mp:
         mp.set_timing(True)
-    if world > 1:
+    if multi:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
     torch.cuda.synchronize()
-    if world > 1:
+    if multi:
         dist.barrier()
     el = time.perf_counter() - t0
     plan.check()
@@ -756,14 +807,14 @@ def main_mono(args, wl):
         for _ in range(args.warmup):
             pipe()
         torch.cuda.synchronize()
-        if world > 1:
+        if multi:
             dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(args.steps):
             pipe()
         torch.cuda.synchronize()
-        if world > 1:
+        if multi:
             dist.barrier()
         el = finish_time(torch, dist, world, dev, time.perf_counter() - t0)
         for p_ in subplans:
@@ -775,7 +826,7 @@ def main_mono(args, wl):
             raise SystemExit("bench.py: pipelined matches differ from the serial step")
     drec = dist_record(torch, dist, world, local)  # collective: every rank
     if rank != 0:
-        if world > 1:
+        if multi:
             dist.destroy_process_group()
         return
     geo = plan.geo
@@ -824,14 +875,15 @@ def main_mono(args, wl):
     out["distributed"] = drec
     if world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args, wl)
-    print(json.dumps(out), flush=True)
-    if world > 1:
+    print(json.dumps(out), file=_BENCH_OUT or sys.stdout, flush=True)
+    if multi:
         dist.destroy_process_group()
 
 
 # --------------------------------------------------------------------------- stereo (c5)
 def main_c5(args, wl):
     torch, dist, world, rank, local = dist_setup(args)
+    multi = dist.is_initialized()  # N ranks, or the one-rank RCCL rehearsal
     import orbx
     from orbx import synth
     from orbx.dist import BoundaryExchange
@@ -860,13 +912,13 @@ def main_c5(args, wl):
     mb, mbf = KITTI_BF / KITTI_FX, KITTI_BF
 
     def step():
-        if world == 1:
+        if not multi:
             kps[0].copy_(kps[B])
             desc[0].copy_(desc[B])
             counts[0:1].copy_(counts[B:B + 1])
         pl.extract(fl, out=(kps[1:], desc[1:], counts[1:]))
         pr.extract(fr)
-        if world > 1:
+        if multi:
             xch.ring_step(dist, rank, (kps[B], desc[B], counts[B:B + 1]),
                           (kps[0], desc[0], counts[0:1]))
         sp.match(pl, pr, fl, fr, mb, mbf, left_out=(kps[1:], desc[1:], counts[1:]))
@@ -882,6 +934,7 @@ def main_c5(args, wl):
                 (torch.zeros_like(kps), torch.zeros_like(desc), torch.zeros_like(counts))]
         ev_x = [torch.cuda.Event(), torch.cuda.Event()]
         ev_m = [torch.cuda.Event(), torch.cuda.Event()]
+        sxch = torch.cuda.Stream(device=dev, priority=xp) if multi and args.xch_stream == "own" else None
         it = [0]
         # --split S (main_mono): sub-batch j's left + right extraction and its
         # ComputeStereoMatches (own plans, own stereo plan) on stream sx[j];
@@ -919,7 +972,7 @@ def main_c5(args, wl):
             (k_i, d_i, c_i), (k_j, d_j, c_j) = bufs[i], bufs[1 - i]
             with torch.cuda.stream(sa):
                 sa.wait_event(ev_m[i])
-                if world == 1:
+                if not multi:
                     k_i[0].copy_(k_j[B])
                     d_i[0].copy_(d_j[B])
                     c_i[0:1].copy_(c_j[B:B + 1])
@@ -934,12 +987,18 @@ def main_c5(args, wl):
                     sp_j.match(pl_j, pr_j, fl_j, fr_j, mb, mbf, left_out=(k_i[lo:hi], d_i[lo:hi], c_i[lo:hi]),
                                stream=sx[j])
                     ev_s[j].record(sx[j])
+            # the boundary exchange on the stream --xch-stream names (main_mono)
+            xs = sb if multi and args.xch_stream == "match" else sxch if sxch is not None else sa
             with torch.cuda.stream(sa):
                 for j in range(1, S):
                     sa.wait_event(ev_s[j])
-                if world > 1:
+            with torch.cuda.stream(xs):
+                if xs is not sa:
+                    xs.wait_event(ev_s[S - 1])
+                    xs.wait_event(ev_m[i])
+                if multi:
                     xch.ring_step(dist, rank, (k_i[B], d_i[B], c_i[B:B + 1]), (k_i[0], d_i[0], c_i[0:1]))
-                ev_x[i].record(sa)
+                ev_x[i].record(xs)
             with torch.cuda.stream(sb):
                 if S == 1 or args.match_whole:
                     sb.wait_event(ev_x[i])
@@ -947,7 +1006,7 @@ def main_c5(args, wl):
                 else:
                     for j in range(S):
                         lo, hi = 1 + j * sub, 1 + (j + 1) * sub
-                        sb.wait_event(ev_x[i] if (j == 0 and world > 1) else ev_s[j])
+                        sb.wait_event(ev_x[i] if (j == 0 and multi) else ev_s[j])
                         if j:
                             sb.wait_event(ev_s[j - 1])
                         mp.match(sub, k_i[lo:hi], d_i[lo:hi], c_i[lo:hi], k_i[lo - 1:hi - 1],
@@ -963,14 +1022,14 @@ def main_c5(args, wl):
     torch.cuda.synchronize()
     for o in (pl, pr, sp, mp):
         o.set_timing(True)
-    if world > 1:
+    if multi:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
     torch.cuda.synchronize()
-    if world > 1:
+    if multi:
         dist.barrier()
     el = time.perf_counter() - t0
     sp.check()
@@ -992,14 +1051,14 @@ def main_c5(args, wl):
         for _ in range(args.warmup):
             pipe()
         torch.cuda.synchronize()
-        if world > 1:
+        if multi:
             dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(args.steps):
             pipe()
         torch.cuda.synchronize()
-        if world > 1:
+        if multi:
             dist.barrier()
         el = finish_time(torch, dist, world, dev, time.perf_counter() - t0)
         for _, _, sp_j in subs:
@@ -1008,7 +1067,7 @@ def main_c5(args, wl):
             raise SystemExit("bench.py: pipelined matches differ from the serial step")
     drec = dist_record(torch, dist, world, local)  # collective: every rank
     if rank != 0:
-        if world > 1:
+        if multi:
             dist.destroy_process_group()
         return
     by = stage_bytes(pl.geo, 2 * B, kps_total, B, wl["topn"], level_blur=st.get("blur", (0, 0))[1] > 0)
@@ -1057,8 +1116,8 @@ def main_c5(args, wl):
     out["distributed"] = drec
     if world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline_c5(args, wl)
-    print(json.dumps(out), flush=True)
-    if world > 1:
+    print(json.dumps(out), file=_BENCH_OUT or sys.stdout, flush=True)
+    if multi:
         dist.destroy_process_group()
 
 

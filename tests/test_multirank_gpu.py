@@ -71,13 +71,16 @@ def _two_gpus():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("backend", ["gloo", "nccl"])
-def test_two_ranks_match_single_process(gpu, backend):
+@pytest.mark.parametrize("backend,world", [("gloo", 2), ("nccl", 2), ("nccl", 1)])
+def test_two_ranks_match_single_process(gpu, backend, world):
+    """("nccl", 1): a one-rank RCCL process group on cuda:0 -- the boundary
+    record goes through RCCL's all-gather from HBM on a one-GPU box (the
+    two-rank case needs two GPUs), and rank 0 takes its own previous step's
+    last frame from the gathered buffer."""
     import torch
     import torch.multiprocessing as mp
-    if backend == "nccl" and not _two_gpus():
+    if backend == "nccl" and world > 1 and not _two_gpus():
         pytest.skip("RCCL rehearsal needs 2 visible GPUs")
-    world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
