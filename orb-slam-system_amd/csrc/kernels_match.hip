@@ -17,6 +17,8 @@
 #include <limits.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "../../include/orbx.h"
 #include "match_internal.h"
 #include "wave_ops.h"
@@ -552,6 +554,7 @@ template __global__ void k_match_cand_rows<6>(const MProblem*, const MNodePair*,
 // accumulator is exact.  ORBM_FP4 0: +-1 bytes on v_mfma_i32_32x32x32_i8.
 // ---------------------------------------------------------------------------
 typedef int v4i_ __attribute__((ext_vector_type(4)));
+typedef int v3i_ __attribute__((ext_vector_type(3)));
 typedef int v16i_ __attribute__((ext_vector_type(16)));
 
 // 4 bits -> 4 bytes of 0 / 1 (bit t -> byte t; the shifted copies never overlap)
@@ -1081,6 +1084,19 @@ __global__ __launch_bounds__(256) void k_match_resolve(
 #ifndef RS_NB
 #define RS_NB 2
 #endif
+// RS_EVB: a chunk's accepted rows are stored once per lane after its rounds
+// (each lane owns its row), so no store sits between the look-ahead loads
+#ifndef RS_EVB
+#define RS_EVB 1
+#endif
+#ifndef RS_RU  // rescan batch (list positions per lane)
+#define RS_RU 8
+#endif
+#if RS_EVB
+#define RS_EV_COMMIT(id) (evl = (id))
+#else
+#define RS_EV_COMMIT(id) (ev[r] = make_int2((id), 0))
+#endif
 __global__ __launch_bounds__(64) void k_match_resolve_spec(
     const MProblem* __restrict__ probs, const MNodePair* __restrict__ nps, int nunits,
     const uint2* __restrict__ cand, const int4* __restrict__ rowinfo, int2* __restrict__ ev,
@@ -1104,9 +1120,11 @@ __global__ __launch_bounds__(64) void k_match_resolve_spec(
   // bound by the latency of these loads)
   // (unconditional loads at a clamped row: a load under a divergent branch
   // would be waited for at the branch join; rows past n1 are masked in chunk)
-  auto fetch = [&](int4& inf_n, uint4 (&cv_n)[ORBM_T / 2], int base) {
+  // (the row info as a 3-vector: with an int4 the unused w register was
+  // taken for a temporary, whose write then waited for the load in flight)
+  auto fetch = [&](v3i_& inf_n, uint4 (&cv_n)[ORBM_T / 2], int base) {
     const int r = NP.row_base + min(base + lane, NP.n1 - 1);
-    inf_n = rowinfo[r];
+    inf_n = *reinterpret_cast<const v3i_*>(rowinfo + r);
     const uint4* src = reinterpret_cast<const uint4*>(cand + (size_t)r * ORBM_T);
 #pragma unroll
     for (int t = 0; t < ORBM_T / 2; ++t) cv_n[t] = src[t];
@@ -1114,7 +1132,7 @@ __global__ __launch_bounds__(64) void k_match_resolve_spec(
 #ifdef RS_STATS
   int st_feas = 0, st_chunks = 0, st_rounds = 0, st_hard = 0;
 #endif
-  auto chunk = [&](int4& inf_n, uint4 (&cv_n)[ORBM_T / 2], int base) {
+  auto chunk = [&](v3i_& inf_n, uint4 (&cv_n)[ORBM_T / 2], int base) {
     const int r = NP.row_base + base + lane;
     // nothing of the row info stays live across the refill below, so the
     // refill reuses the buffer's registers (with a buffer live across the
@@ -1122,9 +1140,9 @@ __global__ __launch_bounds__(64) void k_match_resolve_spec(
     // back, waiting on every load in flight): the rounds need only the
     // wave-uniform "list longer than the candidates" mask, and the rare
     // rescan re-reads its row's idx1
-    const int4 inf = inf_n;
-    const bool feas = base + lane < NP.n1 && inf.x != 0 && inf.z < P.th_low;
-    const uint64_t longl = __ballot(inf.y > ORBM_T);
+    const v3i_ inf = inf_n;
+    const bool feas = base + lane < NP.n1 && inf[0] != 0 && inf[2] < P.th_low;
+    const uint64_t longl = __ballot(inf[1] > ORBM_T);
     uint2 c[ORBM_T];
 #pragma unroll
     for (int t = 0; t < ORBM_T / 2; ++t) {
@@ -1141,6 +1159,9 @@ __global__ __launch_bounds__(64) void k_match_resolve_spec(
     fetch(inf_n, cv_n, base + 64 * RS_NB);  // unconditional (clamped rows)
     uint64_t pend = __ballot(feas);
     if (!pend) return;
+#if RS_EVB
+    int evl = -1;  // the lane's accepted KF2 feature, stored once after the rounds
+#endif
 #ifdef RS_STATS
     st_feas += __popcll(pend); st_chunks++;
 #endif
@@ -1195,7 +1216,7 @@ __global__ __launch_bounds__(64) void k_match_resolve_spec(
       if (acc) claim[id1] = 64;
       if (mine && lane < bnd && acc) {  // rotation bin: k_match_finalize
         atomicOr(&bm[id1 >> 5], 1u << (id1 & 31));
-        ev[r] = make_int2(id1, 0);
+        RS_EV_COMMIT(id1);
       }
       __builtin_amdgcn_wave_barrier();
       pend &= (bnd >= 64) ? 0ull : ~((1ull << bnd) - 1ull);
@@ -1211,13 +1232,42 @@ __global__ __launch_bounds__(64) void k_match_resolve_spec(
         for (int k = 0; k < 8; ++k) d1[k] = q1[k];
         uint32_t kb = 0xFFFFFFFFu;
         int d2 = INT_MAX;
-        for (int jj = lane; jj < NP.n2; jj += 64) {
-          const int i2 = (int)gf2[jj];
-          if (P.valid2 && !((gu8_t)P.valid2)[i2]) continue;
-          if ((bm[i2 >> 5] >> (i2 & 31)) & 1u) continue;
-          const int d = hamming_g(d1, (gu32_t)(P.desc2 + (size_t)i2 * 32));
-          best_merge(kb, d2, ((uint32_t)d << 16) | (uint32_t)jj, INT_MAX);
-        }
+        // RS_RU list positions per lane at a time: every index, then every
+        // descriptor (and validity byte) load of the batch issued before the
+        // first use, unconditionally at clamped positions -- one loop step
+        // per position, with its two dependent loads and a divergent
+        // continue, made a rescan ~60 us (n2 = 2000), longer than the walk
+        const gu8_t gv2 = (gu8_t)P.valid2;
+        // validity bytes only when the problem has them (one uniform branch
+        // per rescan, not a branch and a wait per position)
+        auto scan = [&](auto hv) {
+          constexpr bool HV = decltype(hv)::value;
+          for (int j0 = 0; j0 < NP.n2; j0 += 64 * RS_RU) {
+            int i2[RS_RU];
+#pragma unroll
+            for (int u = 0; u < RS_RU; ++u) i2[u] = (int)gf2[min(j0 + 64 * u + lane, NP.n2 - 1)];
+            v4u_ da[RS_RU], db[RS_RU];
+            uint8_t vv[RS_RU];
+#pragma unroll
+            for (int u = 0; u < RS_RU; ++u) {
+              typedef const v4u_ __attribute__((address_space(1)))* gv4u_t;
+              const gv4u_t q = (gv4u_t)(P.desc2 + (size_t)i2[u] * 32);
+              da[u] = q[0];
+              db[u] = q[1];
+              vv[u] = HV ? gv2[i2[u]] : (uint8_t)1;
+            }
+#pragma unroll
+            for (int u = 0; u < RS_RU; ++u) {
+              const int jj = j0 + 64 * u + lane;
+              const int d = (int)ham256v(make_uint4(d1[0], d1[1], d1[2], d1[3]),
+                                         make_uint4(d1[4], d1[5], d1[6], d1[7]), da[u], db[u]);
+              const bool ok = jj < NP.n2 && vv[u] && !((bm[i2[u] >> 5] >> (i2[u] & 31)) & 1u);
+              if (ok) best_merge(kb, d2, ((uint32_t)d << 16) | (uint32_t)jj, INT_MAX);
+            }
+          }
+        };
+        if (gv2) scan(std::true_type{});
+        else scan(std::false_type{});
 #pragma unroll
         for (int s = 32; s >= 1; s >>= 1) {
           const uint32_t ok = __shfl_xor(kb, s, 64);
@@ -1228,36 +1278,42 @@ __global__ __launch_bounds__(64) void k_match_resolve_spec(
           const int b1 = (int)(kb >> 16), bi = (int)gf2[kb & 0xFFFFu];
           if (b1 < P.th_low && (float)b1 < P.nnratio * (float)d2 && lane == bnd) {
             atomicOr(&bm[bi >> 5], 1u << (bi & 31));
-            ev[r] = make_int2(bi, 0);
+            RS_EV_COMMIT(bi);
           }
         }
         __builtin_amdgcn_wave_barrier();
+        // nothing of the rescan left in flight: its last loads would otherwise
+        // make the waitcnt pass wait for every load at the next round's first
+        // register reuse -- the look-ahead loads included
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0), rare path
         pend &= ~(1ull << bnd);
       }
     }
+#if RS_EVB
+    if (evl >= 0) ev[r] = make_int2(evl, 0);
+#endif
   };
-  int4 inf[RS_NB];
+  v3i_ inf[RS_NB];
   uint4 cv[RS_NB][ORBM_T / 2];
   if (NP.n1 <= 0) return;
 #pragma unroll
-  for (int b = 0; b < RS_NB; ++b) fetch(inf[b], cv[b], 64 * b);
-  // every buffer is refilled exactly once per iteration and the loop leaves
-  // through the breaks, so no buffer is a merge of old and refilled values
-  // at the latch (a merge there made the allocator copy the buffers back,
-  // waiting on every load in flight)
-  for (int base = 0;; base += 64 * RS_NB) {
-    bool done = false;
+  for (int b = 0; b < RS_NB; ++b) {
+    fetch(inf[b], cv[b], 64 * b);
+    __builtin_amdgcn_sched_barrier(0);  // issue order = use order (the loop's waits count on it)
+  }
+  // every buffer is refilled exactly once per iteration and the loop has one
+  // exit, at the latch: a chunk past n1 only refills its buffer (clamped
+  // rows) and finds no pending row.  With an exit after each chunk the CFG
+  // structurizer merged the exits into one flow block that also reaches the
+  // header, on a path where the other buffer was never refilled, and the
+  // waitcnt pass then waited for every load in flight at the header (the
+  // look-ahead was one chunk, not RS_NB)
+  for (int base = 0; base < NP.n1; base += 64 * RS_NB) {
 #pragma unroll
-    for (int b = 0; b < RS_NB; ++b) {
-      if (!done) {
-        chunk(inf[b], cv[b], base + 64 * b);
-        done = base + 64 * (b + 1) >= NP.n1;
-      }
-    }
-    if (done) break;
+    for (int b = 0; b < RS_NB; ++b) chunk(inf[b], cv[b], base + 64 * b);
   }
 #ifdef RS_STATS
-  if (lane == 0 && unit < 4)
+  if (lane == 0)
     printf("RS unit %d n1 %d n2 %d feas %d chunks %d rounds %d hard %d\n", unit, NP.n1, NP.n2,
            st_feas, st_chunks, st_rounds, st_hard);
 #endif
