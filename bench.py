@@ -101,6 +101,9 @@ def parse():
     ap.add_argument("--match-whole", action="store_true",
                     help="with --split: match the whole batch after every sub-batch is extracted "
                          "(default: sub-batch j is matched as soon as it and its predecessor frame exist)")
+    ap.add_argument("--match-cus", type=int, default=0,
+                    help="pipelined step: run the matcher's stream on this many CUs only (HIP CU mask, "
+                         "every k-th CU; 0 = all CUs)")
     ap.add_argument("--traffic", default="", help="PMC traffic summary (default profiles/traffic_<workload>.json)")
     a = ap.parse_args()
     wl = dict(WORKLOADS[a.workload])
@@ -638,6 +641,30 @@ def finish_time(torch, dist, world, dev, el):
 
 
 # --------------------------------------------------------------------------- mono workloads
+def match_stream(torch, dev, args, priority):
+    """The pipelined step's matcher stream: a plain stream at `priority`, or
+    (--match-cus K) a stream whose kernels run on K of the device's CUs only
+    (hipExtStreamCreateWithCUMask, every k-th CU so the subset spans every
+    XCD), wrapped for torch as an external stream."""
+    if args.match_cus <= 0:
+        return torch.cuda.Stream(device=dev, priority=priority)
+    import ctypes
+    ncu = torch.cuda.get_device_properties(dev).multi_processor_count
+    k = max(1, ncu // args.match_cus)
+    words = (ncu + 31) // 32
+    mask = (ctypes.c_uint32 * words)()
+    for i in range(0, ncu, k):
+        if sum(bin(w).count("1") for w in mask) >= args.match_cus:
+            break
+        mask[i // 32] |= 1 << (i % 32)
+    hip = ctypes.CDLL("libamdhip64.so")
+    st = ctypes.c_void_p()
+    rc = hip.hipExtStreamCreateWithCUMask(ctypes.byref(st), ctypes.c_uint32(words), mask)
+    if rc != 0:
+        raise RuntimeError(f"hipExtStreamCreateWithCUMask failed: {rc}")
+    return torch.cuda.ExternalStream(st.value, device=dev)
+
+
 def main_mono(args, wl):
     torch, dist, world, rank, local = dist_setup(args)
     multi = dist.is_initialized()  # N ranks, or the one-rank RCCL rehearsal
@@ -701,7 +728,7 @@ def main_mono(args, wl):
         # streams on one queue serialise
         xp, mpri = (0, -1) if args.match_priority == "high" else (-1, 0)
         sa = torch.cuda.Stream(device=dev, priority=xp)
-        sb = torch.cuda.Stream(device=dev, priority=mpri)
+        sb = match_stream(torch, dev, args, mpri)
         sx = [sa] + [torch.cuda.Stream(device=dev, priority=xp) for _ in range(S - 1)]
         ev_s = [torch.cuda.Event() for _ in range(S)]
         bufs = [(kps, desc, counts),
@@ -956,7 +983,7 @@ def main_c5(args, wl):
                 subs.append((a_, b_, orbx.StereoPlan(a_, device=local)))
         xp, mpri = (0, -1) if args.match_priority == "high" else (-1, 0)
         sa = torch.cuda.Stream(device=dev, priority=xp)  # back to back, after every plan (main_mono)
-        sb = torch.cuda.Stream(device=dev, priority=mpri)
+        sb = match_stream(torch, dev, args, mpri)
         sx = [sa] + [torch.cuda.Stream(device=dev, priority=xp) for _ in range(S - 1)]
         ev_s = [torch.cuda.Event() for _ in range(S)]
 
