@@ -2112,10 +2112,16 @@ __device__ __forceinline__ void ob_body(OB_KERNEL_ARGS, const uint8_t* __restric
     }
     words[rr] = __ballot(t[0] < t[1]);
   }
+#ifdef OB_PROBE_NOSTORE  // profiling only: the outputs' stores never issue (wrong results)
+  if (dbg == 0x5EED)
+#endif
   if (lane < 4) {
     const uint64_t w = lane == 0 ? words[0] : lane == 1 ? words[1] : lane == 2 ? words[2] : words[3];
     reinterpret_cast<uint64_t*>(descf + (uint32_t)me.oi * 32u)[lane] = w;
   }
+#ifdef OB_PROBE_NOSTORE
+  if (dbg == 0x5EED)
+#endif
   if (lane == 0) {
     orbx_keypoint kp;
     kp.x = (float)x;
