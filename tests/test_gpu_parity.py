@@ -453,6 +453,36 @@ def test_search_by_bow_heavy_contention(gpu, oracle, seed):
         assert nm == rnm and np.array_equal(m, rm), ratio
 
 
+@pytest.mark.parametrize("nfill", [151, 152, 153, 1140, 2680])
+@pytest.mark.parametrize("valid", [False, True])
+def test_search_by_bow_rescan_long_lists(gpu, oracle, nfill, valid):
+    """Exhausted candidate lists over long KF2 lists: 360 KF2 features near 12
+    patterns (~30 each, so a row's whole top-8 lies within its pattern) and
+    nfill unrelated ones, 700 KF1 rows near the patterns: once a row's eight
+    candidates are claimed by earlier rows of its pattern, it rescans the
+    whole list (180-321 rescans per case at ratio 1.0, none at 0.75: RS_STATS
+    build, tools/r05_rsl.sh).  The resolver's
+    rescan takes 64 x RS_RU (512) positions per batch: 511 / 512 / 513
+    positions around one batch, several batches, with and without validity
+    bytes."""
+    rng = np.random.default_rng(7 + nfill + (1 << 20) * valid)
+    base = rng.integers(0, 256, (12, 32), dtype=np.uint8)
+    n1 = 700
+    d1 = _correlated(rng, base[rng.integers(0, 12, n1)], rng.integers(0, 20, n1))
+    near = _correlated(rng, base[rng.integers(0, 12, 360)], rng.integers(0, 20, 360))
+    d2 = np.concatenate([near, rng.integers(0, 256, (nfill, 32), dtype=np.uint8)])
+    d2 = d2[rng.permutation(len(d2))]
+    one = lambda d: dict(desc=d, angle=rng.uniform(0, 360, len(d)).astype(np.float32),
+                         valid=(rng.uniform(size=len(d)) > 0.05).astype(np.uint8) if valid else None,
+                         node_id=np.array([3], np.uint32), off=np.array([0, len(d)], np.uint32),
+                         feat=np.arange(len(d), dtype=np.uint32))
+    kf1, kf2 = one(d1), one(d2)
+    for ratio in (0.75, 1.0):
+        m, nm = gpu.search_by_bow(kf1, kf2, ratio, True)
+        rm, rnm = oracle.search_by_bow(kf1, kf2, ratio, True)
+        assert nm == rnm and np.array_equal(m, rm), ratio
+
+
 @pytest.mark.parametrize("n1,n2", [(1, 5), (63, 64), (64, 63), (65, 200), (128, 2), (129, 1), (130, 130)])
 def test_search_by_bow_chunk_edges(gpu, oracle, n1, n2):
     """Node lists around the resolver's 64-row chunk and two-chunk prefetch
