@@ -737,6 +737,7 @@ def main_mono(args, wl):
         ev_m = [torch.cuda.Event(), torch.cuda.Event()]
         sxch = torch.cuda.Stream(device=dev, priority=xp) if multi and args.xch_stream == "own" else None
         it = [0]
+        pend = [None]  # the buffer whose matching the next pipe() call enqueues
 
         def pipe():
             if it[0] == 0:  # continue from the serial loop's state: buffer 0 = its last batch
@@ -747,6 +748,16 @@ def main_mono(args, wl):
                 it[0] = 1
             i = it[0] & 1
             it[0] += 1
+            # step k = the matching of batch k-1 (extracted by the previous
+            # call) + the extraction of batch k: both are enqueued here, the
+            # matching first; on the GPU it still starts as soon as batch k-1's
+            # sub-batches exist and overlaps batch k's extraction, exactly as
+            # when it was enqueued at the end of the previous call.  A timed
+            # window of K steps then holds K matchings and K extractions
+            # without a pipeline fill or drain (the last batch's matching runs
+            # after the window, by pipe_drain, untimed and checked)
+            if pend[0] is not None:
+                match_buf(pend[0])
             (k_i, d_i, c_i), (k_j, d_j, c_j) = bufs[i], bufs[1 - i]
             with torch.cuda.stream(sa):
                 sa.wait_event(ev_m[i])  # the matcher of two steps ago read buffer i
@@ -781,6 +792,10 @@ def main_mono(args, wl):
                 if multi:
                     xch.ring_step(dist, rank, (k_i[B], d_i[B], c_i[B:B + 1]), (k_i[0], d_i[0], c_i[0:1]))
                 ev_x[i].record(xs)
+            pend[0] = i
+
+        def match_buf(i):
+            k_i, d_i, c_i = bufs[i]
             with torch.cuda.stream(sb):
                 if S == 1 or args.match_whole:
                     sb.wait_event(ev_x[i])
@@ -798,6 +813,11 @@ def main_mono(args, wl):
                                  d_i[lo - 1:hi - 1], c_i[lo - 1:hi - 1], args.nnratio, True, stream=sb,
                                  out_offset=lo - 1)
                 ev_m[i].record(sb)
+
+        def pipe_drain():  # the last extracted batch's matching (after the timed window)
+            if pend[0] is not None:
+                match_buf(pend[0])
+                pend[0] = None
 
     for _ in range(args.warmup):
         step()
@@ -844,6 +864,10 @@ def main_mono(args, wl):
         if multi:
             dist.barrier()
         el = finish_time(torch, dist, world, dev, time.perf_counter() - t0)
+        t1 = time.perf_counter()
+        pipe_drain()  # the last batch's matching: after the window (its work is not in it)
+        torch.cuda.synchronize()
+        drain_ms = (time.perf_counter() - t1) * 1e3
         for p_ in subplans:
             p_.check()
         # the frames are the same every step: the pipelined matches must equal
@@ -885,8 +909,9 @@ def main_mono(args, wl):
         "roofline_pyr_fast": pf,
     }
     if pipe is not None:
-        out["step_mode"] = ("pipelined: step k+1's extraction overlaps step k's matching on a second, "
-                            "high-priority stream (same work per step, matches equal the serial step's)")
+        out["step_mode"] = ("pipelined: step k = batch k-1's matching on a second, high-priority stream "
+                            "+ batch k's extraction, overlapping (same work per step, matches equal the "
+                            "serial step's); the window holds K matchings and K extractions, no fill or drain")
         if len(subplans) > 1:
             out["step_mode"] += ("; extraction as %d sub-batches of %d frames on %d streams, %s"
                                  % (len(subplans), B // len(subplans), len(subplans),
@@ -896,6 +921,7 @@ def main_mono(args, wl):
                          "ms_per_step": round(el_serial / args.steps * 1e3, 3),
                          "note": "stage times and roofline entries come from this serial timed loop "
                                  "(kernels alone on the GPU)"}
+        out["pipeline_drain_ms"] = round(drain_ms, 3)  # untimed: the last batch's matching, after the window
     if world == 1 and not args.no_latency and args.workload == "c4":
         out["host_fed"] = host_fed_leg(torch, orbx, plan, mp, wl, args, dev, counts[1:])
         out["latency"] = latency_leg()
@@ -963,6 +989,7 @@ def main_c5(args, wl):
         ev_m = [torch.cuda.Event(), torch.cuda.Event()]
         sxch = torch.cuda.Stream(device=dev, priority=xp) if multi and args.xch_stream == "own" else None
         it = [0]
+        pend = [None]  # the buffer whose matching the next pipe() call enqueues
         # --split S (main_mono): sub-batch j's left + right extraction and its
         # ComputeStereoMatches (own plans, own stereo plan) on stream sx[j];
         # its SearchByBoW pairs start as soon as it and the frame before it exist
@@ -996,6 +1023,16 @@ def main_c5(args, wl):
                 it[0] = 1
             i = it[0] & 1
             it[0] += 1
+            # step k = the matching of batch k-1 (extracted by the previous
+            # call) + the extraction of batch k: both are enqueued here, the
+            # matching first; on the GPU it still starts as soon as batch k-1's
+            # sub-batches exist and overlaps batch k's extraction, exactly as
+            # when it was enqueued at the end of the previous call.  A timed
+            # window of K steps then holds K matchings and K extractions
+            # without a pipeline fill or drain (the last batch's matching runs
+            # after the window, by pipe_drain, untimed and checked)
+            if pend[0] is not None:
+                match_buf(pend[0])
             (k_i, d_i, c_i), (k_j, d_j, c_j) = bufs[i], bufs[1 - i]
             with torch.cuda.stream(sa):
                 sa.wait_event(ev_m[i])
@@ -1026,6 +1063,10 @@ def main_c5(args, wl):
                 if multi:
                     xch.ring_step(dist, rank, (k_i[B], d_i[B], c_i[B:B + 1]), (k_i[0], d_i[0], c_i[0:1]))
                 ev_x[i].record(xs)
+            pend[0] = i
+
+        def match_buf(i):
+            k_i, d_i, c_i = bufs[i]
             with torch.cuda.stream(sb):
                 if S == 1 or args.match_whole:
                     sb.wait_event(ev_x[i])
@@ -1040,6 +1081,11 @@ def main_c5(args, wl):
                                  d_i[lo - 1:hi - 1], c_i[lo - 1:hi - 1], args.nnratio, True, stream=sb,
                                  out_offset=lo - 1)
                 ev_m[i].record(sb)
+
+        def pipe_drain():  # the last extracted batch's matching (after the timed window)
+            if pend[0] is not None:
+                match_buf(pend[0])
+                pend[0] = None
 
     for _ in range(args.warmup):
         step()
@@ -1088,6 +1134,10 @@ def main_c5(args, wl):
         if multi:
             dist.barrier()
         el = finish_time(torch, dist, world, dev, time.perf_counter() - t0)
+        t1 = time.perf_counter()
+        pipe_drain()  # the last batch's matching: after the window (its work is not in it)
+        torch.cuda.synchronize()
+        drain_ms = (time.perf_counter() - t1) * 1e3
         for _, _, sp_j in subs:
             sp_j.check()
         if not torch.equal(mp.match12[:B], ref12):
@@ -1128,9 +1178,10 @@ def main_c5(args, wl):
         "roofline_pyr_fast": pf,
     }
     if pipe is not None:
-        out["step_mode"] = ("pipelined: step k+1's extraction + stereo matching overlap step k's "
-                            "SearchByBoW on a second, high-priority stream (same work per step, "
-                            "matches equal the serial step's)")
+        out["step_mode"] = ("pipelined: step k = batch k-1's SearchByBoW on a second, high-priority "
+                            "stream + batch k's extraction and stereo matching, overlapping (same work per "
+                            "step, matches equal the serial step's); the window holds K of each, no fill or "
+                            "drain")
         if len(subs) > 1:
             out["step_mode"] += ("; extraction + stereo as %d sub-batches of %d pairs on %d streams, %s"
                                  % (len(subs), sub, len(subs),
@@ -1140,6 +1191,7 @@ def main_c5(args, wl):
                          "ms_per_step": round(el_serial / args.steps * 1e3, 3),
                          "note": "stage times and roofline entries come from this serial timed loop "
                                  "(kernels alone on the GPU)"}
+        out["pipeline_drain_ms"] = round(drain_ms, 3)  # untimed: the last batch's matching, after the window
     out["distributed"] = drec
     if world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline_c5(args, wl)
