@@ -1,3 +1,4 @@
+# (historical: --match-streams was removed after this A/B)
 # the sub-batches' matches on two streams (--match-streams 2) vs one stream
 # vs one whole-batch match (--match-whole), pipelined, driver step counts
 set -o pipefail
