@@ -22,7 +22,7 @@ __global__ void k_match_gather2(const MProblem*, const MNodePair*, uint4*, uint3
 typedef int v4i_ __attribute__((ext_vector_type(4)));
 template <int NK>
 __global__ void k_match_expand2(const MProblem*, const MNodePair*, v4i_*);
-template <int NK, int RT, bool PK>
+template <int NK, int RT, bool PK, int CS>
 __global__ void k_match_cand_mfma(const MProblem*, const MNodePair*, const v4i_*, uint2*, int4*,
                                   int2*);
 
@@ -93,26 +93,39 @@ void launch_match(const MProblem* d_probs, int nprob, const MNodePair* d_nps, in
         // distances on the matrix cores (no validity masks on this path):
         // list2 gathered straight into +-1 bytes
         v4i_* gx2 = reinterpret_cast<v4i_*>(d_gx2);
+        // a launch of fewer workgroups than CUs (one long node pair, e.g. a
+        // drop-in call) splits each row tile's list 4 ways over a
+        // workgroup's waves (MC_CSPLIT_WGS: below this many 128-row
+        // workgroups; lists of 8+ tiles)
+        const bool csplit = (size_t)nnp * (size_t)((max_n1 + 128 * MC_RT - 1) / (128 * MC_RT)) < (size_t)MC_CSPLIT_WGS &&
+                            max_n2 >= 256;
+        const dim3 g1((max_n1 + 128 * MC_RT - 1) / (128 * MC_RT), nnp), g4((max_n1 + 31) / 32, nnp);
+#define MC_LAUNCH(NK, PK)                                                                               \
+  do {                                                                                                  \
+    if (csplit)                                                                                         \
+      hipLaunchKernelGGL((k_match_cand_mfma<NK, 1, PK, 4>), g4, dim3(256), 0, s, d_probs, d_nps, gx2,   \
+                         d_cand, d_rowinfo, d_ev);                                                      \
+    else                                                                                                \
+      hipLaunchKernelGGL((k_match_cand_mfma<NK, MC_RT, PK, 1>), g1, dim3(256), 0, s, d_probs, d_nps,    \
+                         gx2, d_cand, d_rowinfo, d_ev);                                                 \
+  } while (0)
         if (six_words) {
           hipLaunchKernelGGL(k_match_expand2<6>, dim3((max_n2 * ORBM_EXPAND_PER_POS(6) + 255) / 256, nnp), dim3(256), 0, s,
                              d_probs, d_nps, gx2);
           // positions in the accumulator while they fit its 2^MC_PB(6) slots
           if (ORBM_FP4 && MC_PK && max_n2 <= (1 << 14))
-            hipLaunchKernelGGL((k_match_cand_mfma<6, MC_RT, ORBM_FP4 != 0>), dim3((max_n1 + 128 * MC_RT - 1) / (128 * MC_RT), nnp), dim3(256), 0, s,
-                               d_probs, d_nps, gx2, d_cand, d_rowinfo, d_ev);
+            MC_LAUNCH(6, ORBM_FP4 != 0);
           else
-            hipLaunchKernelGGL((k_match_cand_mfma<6, MC_RT, false>), dim3((max_n1 + 128 * MC_RT - 1) / (128 * MC_RT), nnp), dim3(256), 0, s,
-                               d_probs, d_nps, gx2, d_cand, d_rowinfo, d_ev);
+            MC_LAUNCH(6, false);
         } else {
           hipLaunchKernelGGL(k_match_expand2<8>, dim3((max_n2 * ORBM_EXPAND_PER_POS(8) + 255) / 256, nnp), dim3(256), 0, s,
                              d_probs, d_nps, gx2);
           if (ORBM_FP4 && MC_PK && max_n2 <= (1 << 13))
-            hipLaunchKernelGGL((k_match_cand_mfma<8, MC_RT, ORBM_FP4 != 0>), dim3((max_n1 + 128 * MC_RT - 1) / (128 * MC_RT), nnp), dim3(256), 0, s,
-                               d_probs, d_nps, gx2, d_cand, d_rowinfo, d_ev);
+            MC_LAUNCH(8, ORBM_FP4 != 0);
           else
-            hipLaunchKernelGGL((k_match_cand_mfma<8, MC_RT, false>), dim3((max_n1 + 128 * MC_RT - 1) / (128 * MC_RT), nnp), dim3(256), 0, s,
-                               d_probs, d_nps, gx2, d_cand, d_rowinfo, d_ev);
+            MC_LAUNCH(8, false);
         }
+#undef MC_LAUNCH
       } else {
         // list2 descriptors gathered into node order, then two rows per lane,
         // the 4 waves splitting the positions; descriptors stream through LDS

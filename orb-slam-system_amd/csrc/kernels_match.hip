@@ -802,19 +802,25 @@ __device__ __forceinline__ void mfma_tile_pk(const v4i_ (&af)[NS], const v4i_ (&
 // Validity arrays are not supported (k_match_cand_rows).
 // PK (fp4 form, max n2 <= 2^MC_PB(NK)): positions in the accumulator
 // (mfma_tile_pk); otherwise keys built per element (mfma_tile)
-template <int NK, int RT, bool PK>
+// CS > 1 (launches with fewer workgroups than CUs, e.g. one node pair of a
+// drop-in call): the workgroup's CS waves take the same 32 rows and split
+// the list's tiles CS ways; their top-T lists merge through LDS at the end
+// (the exact top-T of the union: each part's top-T holds the union's members
+// from that part).
+template <int NK, int RT, bool PK, int CS>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MC_WPE))) void k_match_cand_mfma(
     const MProblem* __restrict__ probs, const MNodePair* __restrict__ nps,
     const v4i_* __restrict__ gx2, uint2* __restrict__ cand, int4* __restrict__ rowinfo,
     int2* __restrict__ ev) {
   static_assert(NK == 6 || NK == 8, "6 or 8 live descriptor dwords");
+  static_assert(CS == 1 || (CS == 4 && RT == 1), "column split: 4 waves on one row tile");
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int h = lane >> 5, c = lane & 31;
   int bx, np;
   frame_unit(bx, np);  // a node pair's row chunks share one L2 (its list2)
   const MNodePair NP = nps[np];
-  const int a0 = bx * 128 * RT;
+  const int a0 = bx * (CS == 1 ? 128 * RT : 32);
   if (a0 >= NP.n1) return;  // workgroup-uniform
   const MProblem P = probs[NP.prob];
   const uint32_t* f2 = P.feat2 + NP.off2;
@@ -833,7 +839,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MC_WPE))) v
 #endif
 #pragma unroll
   for (int t = 0; t < RT; ++t) {
-    a[t] = a0 + 32 * (RT * wave + t) + c;
+    a[t] = a0 + 32 * (RT * (CS == 1 ? wave : 0) + t) + c;
     act[t] = a[t] < NP.n1;
     idx1[t] = 0;
     v1[t] = false;
@@ -873,9 +879,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MC_WPE))) v
   const v16f_ ci = {};
 #define MC_TILE(F, T0) mfma_tile<NS>(F, bf[t], (uint32_t)(T0), n2, hoff, L[t], ci)
 #endif
+  // this wave's positions [tb, te): the whole list, or its tiles split CS ways
+  int tb = 0, te = n2;
+  if constexpr (CS > 1) {
+    const int ntile = (n2 + 31) >> 5, tpw = (ntile + CS - 1) / CS;
+    tb = 32 * min(ntile, wave * tpw);
+    te = 32 * min(ntile, (wave + 1) * tpw);
+  }
 #pragma unroll
-  for (int s = 0; s < NS; ++s) af[s] = n2 > 0 ? gx[(size_t)min(c, n2 - 1) * NS * 2 + 2 * s] : v4i_{0, 0, 0, 0};
+  for (int s = 0; s < NS; ++s) af[s] = n2 > 0 ? gx[(size_t)min(tb + c, n2 - 1) * NS * 2 + 2 * s] : v4i_{0, 0, 0, 0};
 #ifdef MC_NO_PINGPONG  // profiling variant: one fragment set copied forward per tile
+  static_assert(CS == 1, "profiling variant: whole lists only");
   for (int t0 = 0; t0 < n2; t0 += 32) {  // wave-uniform
     const int pn = min(t0 + 32 + c, n2 - 1);
 #pragma unroll
@@ -888,13 +902,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MC_WPE))) v
 #else
   // two fragment sets in turn (tile t0 from af while an loads t0 + 32, then
   // the reverse): no register copies per tile
-  for (int t0 = 0; t0 < n2; t0 += 64) {  // wave-uniform
+  for (int t0 = tb; t0 < te; t0 += 64) {  // wave-uniform
     const int pn = min(t0 + 32 + c, n2 - 1);
 #pragma unroll
     for (int s = 0; s < NS; ++s) an[s] = gx[(size_t)pn * NS * 2 + 2 * s];
 #pragma unroll
     for (int t = 0; t < RT; ++t) MC_TILE(af, t0);
-    if (t0 + 32 >= n2) break;  // wave-uniform
+    if (t0 + 32 >= te) break;  // wave-uniform
     const int pf = min(t0 + 64 + c, n2 - 1);
 #pragma unroll
     for (int s = 0; s < NS; ++s) af[s] = gx[(size_t)pf * NS * 2 + 2 * s];
@@ -912,14 +926,40 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MC_WPE))) v
   for (int t = 0; t < RT; ++t)
 #pragma unroll
     for (int u = 0; u < ORBM_T; ++u) up[t][u] = (uint32_t)__shfl_down((int)L[t][u], 32, 64);
-  if (h) return;
+  if constexpr (CS > 1) {
+    // halves first (lanes 32-63 insert no-op keys), then waves 1.. hand
+    // their lists to wave 0 through LDS
+    __shared__ uint32_t xl[CS - 1][32][ORBM_T + 1];
+#pragma unroll
+    for (int u = 0; u < ORBM_T; ++u) {
+      const uint32_t kk = h ? 0xFFFFFFFFu : up[0][u];
+      if (__ballot(kk < L[0][ORBM_T - 1])) topk_insert(L[0], kk);
+    }
+    if (wave > 0 && !h) {
+#pragma unroll
+      for (int u = 0; u < ORBM_T; ++u) xl[wave - 1][c][u] = L[0][u];
+    }
+    __syncthreads();
+    if (wave > 0 || h) return;
+    for (int w = 0; w < CS - 1; ++w) {
+#pragma unroll
+      for (int u = 0; u < ORBM_T; ++u) {
+        const uint32_t kk = xl[w][c][u];
+        if (__ballot(kk < L[0][ORBM_T - 1])) topk_insert(L[0], kk);
+      }
+    }
+  } else {
+    if (h) return;
+  }
 #pragma unroll
   for (int t = 0; t < RT; ++t) {
     uint32_t (&Lt)[ORBM_T] = L[t];
+    if constexpr (CS == 1) {
 #pragma unroll
-    for (int u = 0; u < ORBM_T; ++u) {
-      const uint32_t kk = up[t][u];
-      if (__ballot(kk < Lt[ORBM_T - 1])) topk_insert(Lt, kk);
+      for (int u = 0; u < ORBM_T; ++u) {
+        const uint32_t kk = up[t][u];
+        if (__ballot(kk < Lt[ORBM_T - 1])) topk_insert(Lt, kk);
+      }
     }
     const bool full = Lt[ORBM_T - 1] < sent;
 #pragma unroll
@@ -949,16 +989,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MC_WPE))) v
     }
   }
 }
-template __global__ void k_match_cand_mfma<6, MC_RT, false>(const MProblem*, const MNodePair*, const v4i_*,
-                                                            uint2*, int4*, int2*);
-template __global__ void k_match_cand_mfma<8, MC_RT, false>(const MProblem*, const MNodePair*, const v4i_*,
-                                                            uint2*, int4*, int2*);
+#define MC_INST(NK, RT, PK, CS) \
+  template __global__ void k_match_cand_mfma<NK, RT, PK, CS>(const MProblem*, const MNodePair*, const v4i_*, uint2*, int4*, int2*);
+MC_INST(6, MC_RT, false, 1)
+MC_INST(8, MC_RT, false, 1)
+MC_INST(6, 1, false, 4)
+MC_INST(8, 1, false, 4)
 #if ORBM_FP4
-template __global__ void k_match_cand_mfma<6, MC_RT, true>(const MProblem*, const MNodePair*, const v4i_*,
-                                                           uint2*, int4*, int2*);
-template __global__ void k_match_cand_mfma<8, MC_RT, true>(const MProblem*, const MNodePair*, const v4i_*,
-                                                           uint2*, int4*, int2*);
+MC_INST(6, MC_RT, true, 1)
+MC_INST(8, MC_RT, true, 1)
+MC_INST(6, 1, true, 4)
+MC_INST(8, 1, true, 4)
 #endif
+#undef MC_INST
 
 // ---------------------------------------------------------------------------
 // k_match_resolve: greedy, in list order.  unit = node pair (parallel mode)

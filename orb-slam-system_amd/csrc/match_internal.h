@@ -29,6 +29,11 @@
 #ifndef MC_RT
 #define MC_RT 1
 #endif
+/* k_match_cand_mfma column split (CS = 4 waves per row tile) below this many
+   128-row workgroups in a launch (api_match.hip launch_match; 0 = never) */
+#ifndef MC_CSPLIT_WGS
+#define MC_CSPLIT_WGS 256
+#endif
 #ifndef MC_WPE
 #define MC_WPE 5
 #endif
