@@ -1365,6 +1365,29 @@ __global__ __launch_bounds__(64) void k_match_resolve_spec(
 // ---------------------------------------------------------------------------
 // k_match_finalize: one workgroup per problem.
 // ---------------------------------------------------------------------------
+// ComputeThreeMaxima (ORBmatcher.cc:469-502), one thread
+__device__ __forceinline__ void three_maxima(const int* hist, int* ind) {
+  int ti[3] = {-1, -1, -1}, tv[3] = {0, 0, 0};
+  int hv[ORBM_HISTO];  // every bin read up front (independent LDS reads)
+#pragma unroll
+  for (int i = 0; i < ORBM_HISTO; ++i) hv[i] = hist[i];
+#pragma unroll
+  for (int i = 0; i < ORBM_HISTO; ++i) {
+    const int v = hv[i];
+    for (int jj = 0; jj < 3; ++jj) {
+      if (v > tv[jj]) {
+        for (int k = 2; k > jj; --k) { tv[k] = tv[k - 1]; ti[k] = ti[k - 1]; }
+        tv[jj] = v;
+        ti[jj] = i;
+        break;
+      }
+    }
+  }
+  if (tv[1] < 0.1f * tv[0]) { ti[1] = -1; ti[2] = -1; }
+  else if (tv[2] < 0.1f * tv[0]) { ti[2] = -1; }
+  ind[0] = ti[0]; ind[1] = ti[1]; ind[2] = ti[2];
+}
+
 __global__ __launch_bounds__(256) void k_match_finalize(const MProblem* __restrict__ probs,
                                                         const MNodePair* __restrict__ nps,
                                                         const int4* __restrict__ rowinfo,
@@ -1383,6 +1406,27 @@ __global__ __launch_bounds__(256) void k_match_finalize(const MProblem* __restri
   typedef int __attribute__((address_space(1)))* gi32_t;
   typedef const float __attribute__((address_space(1)))* gf32_t;
   const gi32_t m12 = (gi32_t)P.match12;
+  // the problem's rows are one contiguous range: node pairs are laid out in
+  // order from np_begin (api_match.hip: the merge-join assigns row_base
+  // sequentially; a batched plan has one node pair per problem)
+  const int rb = P.np_end > P.np_begin ? nps[P.np_begin].row_base : 0;
+  const int re = P.np_end > P.np_begin ? nps[P.np_end - 1].row_base + nps[P.np_end - 1].n1 : 0;
+  constexpr int FZ_U = 8;
+  // every row in one batch per thread (a problem of <= 2048 rows: the
+  // bench's, a drop-in call's): the rows' matches, KF1 indices and bins
+  // stay in registers for the three passes instead of being re-read, and
+  // their loads are issued ahead of the initialisation below
+  const bool one = re > rb && re - rb <= 256 * FZ_U;
+  int2 e1[FZ_U];
+  int i1r[FZ_U];
+  if (one) {
+#pragma unroll
+    for (int u = 0; u < FZ_U; ++u) {
+      const int r = min(rb + tid + 256 * u, re - 1);
+      e1[u] = ev[r];
+      i1r[u] = rowinfo[r].w;
+    }
+  }
   for (int i = tid; i < P.n1; i += 256) {
     m12[i] = -1;
     last[i] = -1;
@@ -1390,16 +1434,72 @@ __global__ __launch_bounds__(256) void k_match_finalize(const MProblem* __restri
   if (tid < ORBM_HISTO) hist[tid] = 0;
   if (tid == 0) { s_nev = 0; s_nfilt = 0; }
   __syncthreads();
-  // the problem's rows are one contiguous range: node pairs are laid out in
-  // order from np_begin (api_match.hip: the merge-join assigns row_base
-  // sequentially; a batched plan has one node pair per problem).  Each
-  // thread walks its rows FZ_U at a time: every load of a batch is issued
-  // before the first use (clamped rows, masked below), instead of three
-  // dependent round trips per row
-  const int rb = P.np_end > P.np_begin ? nps[P.np_begin].row_base : 0;
-  const int re = P.np_end > P.np_begin ? nps[P.np_end - 1].row_base + nps[P.np_end - 1].n1 : 0;
-  constexpr int FZ_U = 8;
+  // Otherwise each thread walks its rows FZ_U at a time: every load of a
+  // batch is issued before the first use (clamped rows, masked below),
+  // instead of three dependent round trips per row
   int nev = 0;
+  if (one) {
+    int2 e[FZ_U];
+    int i1[FZ_U], bin[FZ_U];
+#pragma unroll
+    for (int u = 0; u < FZ_U; ++u) {
+      e[u] = e1[u];
+      i1[u] = i1r[u];
+      bin[u] = 0;
+    }
+    if (P.check_ori) {
+      float rot[FZ_U];
+#pragma unroll
+      for (int u = 0; u < FZ_U; ++u)
+        rot[u] = e[u].x >= 0 ? ((gf32_t)P.ang1)[(size_t)i1[u] * P.ang_stride] -
+                                   ((gf32_t)P.ang2)[(size_t)e[u].x * P.ang_stride]
+                             : 0.0f;
+#pragma unroll
+      for (int u = 0; u < FZ_U; ++u) {
+        float ro = rot[u];
+        if (ro < 0.0f) ro += 360.0f;
+        bin[u] = (int)roundf(ro * factor);  // rotation histogram bin (ORBmatcher.cc:332-340)
+        if (bin[u] == ORBM_HISTO) bin[u] = 0;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < FZ_U; ++u) {
+      const int r = rb + tid + 256 * u;
+      if (r >= re || e[u].x < 0) continue;
+      atomicMax(&last[i1[u]], r);
+      atomicAdd(&hist[bin[u]], 1);
+      ++nev;
+    }
+    atomicAdd(&s_nev, nev);
+    __syncthreads();
+    if (tid == 0) three_maxima(hist, ind);
+    __syncthreads();
+    int l[FZ_U];
+#pragma unroll
+    for (int u = 0; u < FZ_U; ++u) l[u] = last[i1[u]];
+#pragma unroll
+    for (int u = 0; u < FZ_U; ++u) {
+      const int r = rb + tid + 256 * u;
+      if (r < re && e[u].x >= 0 && l[u] == r) m12[i1[u]] = e[u].x;
+    }
+    __syncthreads();
+    int nf = 0;
+    if (P.check_ori) {
+      const int b0 = ind[0], b1 = ind[1], b2 = ind[2];
+#pragma unroll
+      for (int u = 0; u < FZ_U; ++u) {
+        const int r = rb + tid + 256 * u;
+        if (r >= re || e[u].x < 0) continue;
+        if (bin[u] == b0 || bin[u] == b1 || bin[u] == b2) continue;
+        m12[i1[u]] = -2;  // set to nullptr by the rotation check (:359)
+        ++nf;
+      }
+    }
+    atomicAdd(&s_nfilt, nf);
+    __syncthreads();
+    if (tid == 0) *P.nmatches = s_nev - s_nfilt;
+    return;
+  }
   for (int r0 = rb + tid; r0 < re; r0 += 256 * FZ_U) {
     int2 e[FZ_U];
     int i1[FZ_U];
@@ -1436,27 +1536,7 @@ __global__ __launch_bounds__(256) void k_match_finalize(const MProblem* __restri
   }
   atomicAdd(&s_nev, nev);
   __syncthreads();
-  if (tid == 0) {  // ComputeThreeMaxima (ORBmatcher.cc:469-502)
-    int ti[3] = {-1, -1, -1}, tv[3] = {0, 0, 0};
-    int hv[ORBM_HISTO];  // every bin read up front (independent LDS reads)
-#pragma unroll
-    for (int i = 0; i < ORBM_HISTO; ++i) hv[i] = hist[i];
-#pragma unroll
-    for (int i = 0; i < ORBM_HISTO; ++i) {
-      const int v = hv[i];
-      for (int jj = 0; jj < 3; ++jj) {
-        if (v > tv[jj]) {
-          for (int k = 2; k > jj; --k) { tv[k] = tv[k - 1]; ti[k] = ti[k - 1]; }
-          tv[jj] = v;
-          ti[jj] = i;
-          break;
-        }
-      }
-    }
-    if (tv[1] < 0.1f * tv[0]) { ti[1] = -1; ti[2] = -1; }
-    else if (tv[2] < 0.1f * tv[0]) { ti[2] = -1; }
-    ind[0] = ti[0]; ind[1] = ti[1]; ind[2] = ti[2];
-  }
+  if (tid == 0) three_maxima(hist, ind);
   __syncthreads();
   for (int r0 = rb + tid; r0 < re; r0 += 256 * FZ_U) {
     int2 e[FZ_U];
