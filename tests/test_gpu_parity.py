@@ -483,6 +483,28 @@ def test_search_by_bow_rescan_long_lists(gpu, oracle, nfill, valid):
         assert nm == rnm and np.array_equal(m, rm), ratio
 
 
+@pytest.mark.parametrize("n1,n2", [(2048, 300), (2049, 300), (300, 255), (300, 256), (40, 4100),
+                                   (33, 1000)])
+@pytest.mark.parametrize("check_ori", [True, False])
+def test_search_by_bow_launch_forms(gpu, oracle, n1, n2, check_ori):
+    """The drop-in call's launch forms: the candidates' column split (one
+    node pair of <256 128-row workgroups with lists of >= 256 positions:
+    255 / 256 around it, 4100 = 129 tiles split unevenly) and the finalize's
+    register path (<= 2048 rows: 2048 / 2049 around it)."""
+    rng = np.random.default_rng(n1 * 7919 + n2 + 13 * check_ori)
+    d1 = rng.integers(0, 256, (n1, 32), dtype=np.uint8)
+    d2 = _correlated(rng, d1[rng.integers(0, n1, n2)], rng.integers(0, 40, n2))
+    one = lambda d: dict(desc=d, angle=rng.uniform(0, 360, len(d)).astype(np.float32), valid=None,
+                         node_id=np.array([9], np.uint32), off=np.array([0, len(d)], np.uint32),
+                         feat=np.arange(len(d), dtype=np.uint32))
+    kf1, kf2 = one(d1), one(d2)
+    for ratio in (0.75, 1.0):
+        m, nm = gpu.search_by_bow(kf1, kf2, ratio, check_ori)
+        rm, rnm = oracle.search_by_bow(kf1, kf2, ratio, check_ori)
+        assert nm == rnm and np.array_equal(m, rm), ratio
+        assert nm > 0
+
+
 @pytest.mark.parametrize("n1,n2", [(1, 5), (63, 64), (64, 63), (65, 200), (128, 2), (129, 1), (130, 130)])
 def test_search_by_bow_chunk_edges(gpu, oracle, n1, n2):
     """Node lists around the resolver's 64-row chunk and two-chunk prefetch
