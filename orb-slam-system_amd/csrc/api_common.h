@@ -153,6 +153,12 @@ hipError_t stream_wait(hipStream_t s);
 // concurrent call writing a smaller value could undercut a larger launch).
 int set_max_dynamic_lds(const void* kernel, int device);
 
+// a drop-in call's inputs [0, bytes) from its pinned staging buffer h into
+// its device arena d, on stream s: a kernel (k_stage_in) when
+// ORBM_STAGE_KERNEL, else a DMA copy.  bytes: a multiple of 16 (Carve's
+// 256-byte blocks)
+int stage_in(void* d, const void* h, size_t bytes, hipStream_t s);
+
 }  // namespace orbx
 
 #endif

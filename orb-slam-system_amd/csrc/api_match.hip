@@ -303,7 +303,8 @@ static int bow_search(const orbx_bow_frame* kf1, const orbx_bow_frame* kf2, floa
   memcpy(h + o_prob, &P, sizeof(P));
   if (nnp) memcpy(h + o_nps, nps.data(), nnp * sizeof(MNodePair));
   memset(h + o_loff, 0, sizeof(int));
-  ORBX_TRY(hipMemcpyAsync(d, h, in_end, hipMemcpyHostToDevice, s));
+  rc2 = stage_in(d, h, in_end, s);
+  if (rc2) return rc2;
   launch_match(reinterpret_cast<MProblem*>(d + o_prob), 1, reinterpret_cast<MNodePair*>(d + o_nps),
                (int)nnp, rows, sequential, max_n1, max_n2, kf2->n,
                reinterpret_cast<uint4*>(d + o_g2),
@@ -377,7 +378,8 @@ extern "C" int orbm_descriptor_distance_batch(const uint8_t* a, int na, const ui
   memcpy(h + o_b, b, (size_t)nb * 32);
   memcpy(h + o_ia, ia, (size_t)npairs * 4);
   memcpy(h + o_ib, ib, (size_t)npairs * 4);
-  ORBX_TRY(hipMemcpyAsync(d, h, in_end, hipMemcpyHostToDevice, s));
+  rc = stage_in(d, h, in_end, s);
+  if (rc) return rc;
   hipLaunchKernelGGL(k_hamming_pairs, dim3((npairs + 255) / 256), dim3(256), 0, s, d + o_a, d + o_b,
                      reinterpret_cast<const int32_t*>(d + o_ia),
                      reinterpret_cast<const int32_t*>(d + o_ib), npairs,

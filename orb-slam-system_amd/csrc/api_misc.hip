@@ -47,7 +47,7 @@ extern "C" int orbm_compute_distinctive_descriptors(const uint8_t* desc, const i
   if (rc) return rc;
   if (total) memcpy(w->h + o_desc, desc, (size_t)total * 32);
   memcpy(w->h + o_off, off, (size_t)(nmp + 1) * 4);
-  ORBX_TRY(hipMemcpyAsync(w->d, w->h, in_end, hipMemcpyHostToDevice, w->stream));
+  if (stage_in(w->d, w->h, in_end, w->stream)) return ORBX_ERR_HIP;
   hipLaunchKernelGGL(k_distinctive, dim3((nmp + 3) / 4), dim3(256), 0, w->stream, w->d + o_desc,
                      reinterpret_cast<const int32_t*>(w->d + o_off), nmp,
                      reinterpret_cast<int32_t*>(w->d + o_best));
@@ -89,8 +89,8 @@ extern "C" int orbx_undistort_keypoints(const orbx_keypoint* kps, int n, const f
   rc = w->reserve(C.off, C.off);
   if (rc) return rc;
   memcpy(w->h + o_in, kps, (size_t)n * sizeof(orbx_keypoint));
-  ORBX_TRY(hipMemcpyAsync(w->d + o_in, w->h + o_in, (size_t)n * sizeof(orbx_keypoint),
-                          hipMemcpyHostToDevice, w->stream));
+  if (stage_in(w->d + o_in, w->h + o_in, ((size_t)n * sizeof(orbx_keypoint) + 15) & ~(size_t)15, w->stream))
+    return ORBX_ERR_HIP;
   hipLaunchKernelGGL(k_undistort, dim3((n + 255) / 256), dim3(256), 0, w->stream,
                      reinterpret_cast<const orbx_keypoint*>(w->d + o_in), n, A,
                      reinterpret_cast<orbx_keypoint*>(w->d + o_out));

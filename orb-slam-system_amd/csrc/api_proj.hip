@@ -123,7 +123,7 @@ extern "C" int orbm_search_by_projection(int mode, const orbx_proj_frame* F,
   hp->cell_feat = reinterpret_cast<int*>(d + o_feat);
   hp->cand = reinterpret_cast<uint32_t*>(d + o_cand);
   hp->ncand = reinterpret_cast<int*>(d + o_nc);
-  ORBX_TRY(hipMemcpyAsync(d, h, in_end, hipMemcpyHostToDevice, s));
+  if (stage_in(d, h, in_end, s)) return ORBX_ERR_HIP;
   launch_proj(dp, 1, n, nq, mode, nnratio, th_dist, check_ori, s);
   if (hipGetLastError() != hipSuccess) return ORBX_ERR_HIP;
   ORBX_TRY(hipMemcpyAsync(h + in_end, d + in_end, out_end - in_end, hipMemcpyDeviceToHost, s));

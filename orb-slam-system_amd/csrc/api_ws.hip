@@ -2,6 +2,7 @@
 // for the synchronous drop-in entry points (api_common.h).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <chrono>
 #include <thread>
 #include <map>
@@ -10,6 +11,7 @@
 #include <vector>
 
 #include "api_common.h"
+#include "match_internal.h"
 
 namespace orbx {
 
@@ -106,6 +108,20 @@ hipError_t stream_wait(hipStream_t s) {
     if (now >= t_yield) std::this_thread::yield();
     else __builtin_ia32_pause();
   }
+}
+
+__global__ void k_stage_in(uint4*, const uint4*, size_t);  // kernels_match.hip
+
+int stage_in(void* d, const void* h, size_t bytes, hipStream_t s) {
+#if ORBM_STAGE_KERNEL
+  const size_t n16 = bytes / 16;
+  if (n16 == 0) return ORBX_OK;
+  hipLaunchKernelGGL(k_stage_in, dim3((unsigned)std::min<size_t>((n16 + 255) / 256, 1024)), dim3(256), 0, s,
+                     reinterpret_cast<uint4*>(d), reinterpret_cast<const uint4*>(h), n16);
+  return hipGetLastError() == hipSuccess ? ORBX_OK : ORBX_ERR_HIP;
+#else
+  return hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, s) == hipSuccess ? ORBX_OK : ORBX_ERR_HIP;
+#endif
 }
 
 int set_max_dynamic_lds(const void* kernel, int device) {

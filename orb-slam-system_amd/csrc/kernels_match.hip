@@ -1682,6 +1682,18 @@ __global__ __launch_bounds__(256) void k_match_select(
 }
 
 // DescriptorDistance over index pairs
+// ---------------------------------------------------------------------------
+// k_stage_in: a call's inputs from the pinned staging buffer (host memory the
+// GPU reads over PCIe) into its device arena, as a kernel on the call's
+// stream: the kernels after it start without the copy engine -> compute
+// queue handover a DMA copy needs (~8 us between the copy's end and the first
+// kernel in the drop-in SearchByBoW trace).  bytes: a multiple of 16.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_stage_in(uint4* __restrict__ d, const uint4* __restrict__ h,
+                                                  size_t n16) {
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n16; i += (size_t)gridDim.x * 256) d[i] = h[i];
+}
+
 __global__ void k_hamming_pairs(const uint8_t* __restrict__ a, const uint8_t* __restrict__ b,
                                 const int32_t* __restrict__ ia, const int32_t* __restrict__ ib,
                                 int npairs, int32_t* __restrict__ dist) {

@@ -31,6 +31,11 @@
 #endif
 /* k_match_cand_mfma column split (CS = 4 waves per row tile) below this many
    128-row workgroups in a launch (api_match.hip launch_match; 0 = never) */
+/* drop-in calls stage their inputs with a kernel reading the pinned buffer
+   (k_stage_in) instead of a DMA copy (A/B: 0) */
+#ifndef ORBM_STAGE_KERNEL
+#define ORBM_STAGE_KERNEL 1
+#endif
 #ifndef MC_CSPLIT_WGS
 #define MC_CSPLIT_WGS 256
 #endif

@@ -1,8 +1,11 @@
+# drop-in SearchByBoW: inputs staged by a kernel (base) vs a DMA copy (stg0)
 set -o pipefail
 cd $GRAFT_REPO_ROOT
-for wl in c4 c1 c2; do
-for st in none pyramid fast quadtree none pyramid fast; do
-timeout -k 10 300 python bench.py --workload $wl --steps 40 --warmup 5 --no-cpu-baseline --no-latency --stagger $st > gpurun_out/stg.json 2> gpurun_out/stg.err || { tail -5 gpurun_out/stg.err; exit 1; }
-python3 -c "import json,sys;d=json.load(open(sys.argv[1]));print(sys.argv[2], sys.argv[3], d['value'], d['ms_per_step'])" gpurun_out/stg.json $wl $st
-done
+TAG=r05stg bash tools/gpu_tests.sh tests/test_gpu_parity.py -k "bow or kf_frame" || { tail -30 gpurun_out/gtests_r05stg.log; exit 1; }
+tail -1 gpurun_out/gtests_r05stg.log
+for r in 1 2 3; do
+  for v in base stg0; do
+    vv=""; [ $v != base ] && vv=$v
+    echo -n "$v "; ORBX_VARIANT=$vv timeout -k 10 120 python tools/bow_latency_probe.py 300 || exit 1
+  done
 done
