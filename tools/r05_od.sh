@@ -1,3 +1,4 @@
+# (historical: the variant this measured was reverted)
 # drop-in SearchByBoW outputs written straight to the pinned buffer (base)
 # vs the device arena + a copy back (od0)
 set -o pipefail

@@ -1,3 +1,4 @@
+# (historical: the variant this measured was reverted)
 # quadtree child / node counts aggregated per wave (QT_AGG_MAXS: base 64,
 # qa0 = off, qa256, qa4k = every pass): extraction parity, serial-loop
 # stage times per workload, the drop-in extraction latency

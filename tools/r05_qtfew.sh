@@ -1,3 +1,4 @@
+# (historical: the variant this measured was reverted)
 # k_quadtree_few for small launches (drop-in extraction): full GPU suite,
 # the extraction latency probe + trace, and the c4 line's latency leg
 set -o pipefail
