@@ -1,11 +1,7 @@
-# pipelined step: matcher stream priority A/B (c4, c1, c2), two runs each
+# (historical: RS_PRIO was removed after this A/B)
+# resolver wave priority (s_setprio) in the pipelined step: base (0) vs 1 / 3
 set -o pipefail
 cd $GRAFT_REPO_ROOT
-mkdir -p gpurun_out/r05d
-for wl in c4 c1 c2; do
-  for pr in high low high low; do
-    timeout -k 10 300 python bench.py --workload $wl --match-priority $pr --steps 20 --warmup 5 --no-cpu-baseline --no-latency \
-      > gpurun_out/r05d/bench_${wl}_$pr.json 2> gpurun_out/r05d/bench_${wl}_$pr.err || exit $?
-    python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[1], d['value'], d['ms_per_step'], d['serial']['value'])" gpurun_out/r05d/bench_${wl}_$pr.json
-  done
+for wl in c4 c1 c2 c5; do
+  WL=$wl BATCH=0 STEPS=20 VARS="base rp3 rp1 base rp3 rp1" bash tools/variant_probe.sh | cut -d' ' -f1,2 | sed "s/^/$wl /" || exit 1
 done
