@@ -223,6 +223,11 @@ extern "C" int orbx_plan_create(const orbx_params* prm, int width, int height, i
     p->largs.pitch[l] = u.pitch;
   }
   p->largs.key_xs = P.levels[0].key_xs;
+  // plans with a pyramid run its waves and FAST's at a raised issue
+  // priority (ORBX_EX_PRIO): measured in the pipelined step, c4 +1.4-2.3 %,
+  // c1 +0.5-0.7 %, c5 neutral; a single level (c2) lost 2.3 %, the matcher
+  // then being a larger share of its step
+  p->largs.prio = (ORBX_EX_PRIO && P.params.nlevels > 1) ? 1 : 0;
   p->bargs.key_xs = P.levels[0].key_xs;
   p->bargs.nlevels = P.params.nlevels;
   p->bargs.kcap = P.kcap;
@@ -446,9 +451,11 @@ static int extract_pass(orbx_plan* p, const uint8_t* frames, int n, size_t fstri
                          dim3(256), 0, s, frames, fstride, rstride, d_pyr, p->pyr_stride, g);
       continue;
     }
+    PyrSeg gp = g;
+    gp.prio = p->largs.prio;
     hipLaunchKernelGGL(k_pyramid, dim3(g.ntx * g.nty, n), dim3(256),
                        g.lds_a + g.lds_b + g.lds_yl + p->pad_pyr, s, frames, fstride, rstride,
-                       d_pyr, p->pyr_stride, g, reinterpret_cast<const int4*>(p->d_pyr_xs),
+                       d_pyr, p->pyr_stride, gp, reinterpret_cast<const int4*>(p->d_pyr_xs),
                        reinterpret_cast<const int4*>(p->d_pyr_ys),
                        reinterpret_cast<const uint4*>(p->d_pyr_blob), p->d_pyr_bo, p->dbg);
   }

@@ -340,7 +340,7 @@ static int plan_pyramid(Plan& P) {
   size_t i = 1;
   while (i < uniq.size()) {
     if (P.area2[uniq[i]]) {  /* exact 2x: its own launch of k_pyr_area2 */
-      PyrSeg g;
+      PyrSeg g{};
       memset(&g, 0, sizeof(g));
       g.nl = 1;
       g.area = 1;
@@ -363,7 +363,7 @@ static int plan_pyramid(Plan& P) {
       std::vector<int> lev(uniq.begin() + (i - 1), uniq.begin() + j);
       const int ntile = (j == i + 1) ? 9 : 6;
       for (int k = std::min(k0, ntile - 1); k < ntile && !done; ++k) {
-        PyrSeg g;
+        PyrSeg g{};
         std::vector<Iv> xs, ys;
         if (!try_segment(P, lev, tiles[k][0], tiles[k][1], g, xs, ys)) continue;
         g.xs_off = (int)(P.pyr_xs.size() / 4);

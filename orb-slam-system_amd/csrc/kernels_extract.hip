@@ -188,6 +188,9 @@ __global__ __launch_bounds__(256) void k_pyramid(const uint8_t* __restrict__ fra
                                                  const uint4* __restrict__ blob,
                                                  const int* __restrict__ bo, int dbg) {
   extern __shared__ __align__(16) uint8_t plds[];
+#if ORBX_EX_PRIO
+  if (S.prio) __builtin_amdgcn_s_setprio(ORBX_EX_PRIO);  // ahead of a co-resident matcher's waves
+#endif
   const int tid = threadIdx.x;
   int bx, f;
   frame_unit(bx, f);
@@ -951,6 +954,9 @@ __device__ __forceinline__ void fs_kernel(
   // | per-cell counts; the NMS row masks reuse the tile, which is dead after
   // pass 1 (fs_lds in api_extract.hip mirrors this layout)
   extern __shared__ __align__(16) uint32_t sm[];
+#if ORBX_EX_PRIO
+  if (LA.prio) __builtin_amdgcn_s_setprio(ORBX_EX_PRIO);  // ahead of a co-resident matcher's waves
+#endif
   uint8_t* tile = reinterpret_cast<uint8_t*>(sm);                    // tpitch * tmax_h
   uint8_t* amap_mem = tile + tpitch * tmax_h;                         // tpitch * (tmax_h - 6)
   int* cnt = reinterpret_cast<int*>(amap_mem + tpitch * (tmax_h - 6));  // mcells

@@ -82,10 +82,18 @@ struct StripInfo {
 
 /* per-level storage of the pyramid, passed by value to kernels that only
  * need to locate a level (no dependent LevelInfo loads) */
+/* s_setprio of the pyramid and FAST waves when a plan sets prio: in the
+ * pipelined step they then win their SIMDs' issue arbitration over the
+ * matcher's co-resident waves (the matcher fills the slots they leave).
+ * Plans with a pyramid set it (orbx_plan_create); 0 disables */
+#ifndef ORBX_EX_PRIO
+#define ORBX_EX_PRIO 2
+#endif
 struct LevelArgs {
   long long pyr_off[ORBX_MAX_LEVELS];
   int pitch[ORBX_MAX_LEVELS];
   int key_xs; /* orbx_pack_key shift */
+  int prio;   /* 1: FAST waves at ORBX_EX_PRIO */
 };
 #define ORBX_STRIP_MAXCELLS 64 /* cells per FAST strip (>= 256 / min cell width) */
 
@@ -177,6 +185,7 @@ struct PyrSeg {
   int lev[ORBX_MAX_LEVELS], w[ORBX_MAX_LEVELS], h[ORBX_MAX_LEVELS], pitch[ORBX_MAX_LEVELS];
   int lut_x[ORBX_MAX_LEVELS], lut_y[ORBX_MAX_LEVELS];
   long long off[ORBX_MAX_LEVELS]; /* pyr offset; -1 = the caller's frame (level 0) */
+  int prio;                       /* 1: pyramid waves at ORBX_EX_PRIO (set at launch) */
 };
 
 
