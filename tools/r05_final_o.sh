@@ -1,0 +1,8 @@
+# round-5 evidence after the extraction issue priority: full GPU suite, smoke,
+# then kernel stats / traffic / SQ / bench lines per workload (round_final)
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+TAG=r05o bash tools/gpu_tests.sh tests || { tail -40 gpurun_out/gtests_r05o.log; exit 1; }
+tail -2 gpurun_out/gtests_r05o.log
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" || exit 1
+R=r05o bash tools/round_final.sh || exit $?
