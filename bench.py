@@ -613,13 +613,16 @@ def dist_setup(args):
     return torch, dist, world, rank, local
 
 
-def dist_record(torch, dist, world, local):
+def dist_record(torch, dist, world, local, **extra):
     """What the process group actually formed, for the bench line: backend,
     world size and every rank's device (gathered), so a multi-GPU record
-    shows by itself that RCCL saw N ranks on N distinct GPUs."""
+    shows by itself that RCCL saw N ranks on N distinct GPUs; `extra` (per
+    rank: its last batch's keypoints and matches, whether its pipelined
+    matches equal its serial loop's) is gathered with it."""
     props = torch.cuda.get_device_properties(local)
     me = {"local_rank": local, "device": props.name,
           "uuid": str(getattr(props, "uuid", "")), "pci_bus": getattr(props, "pci_bus_id", None)}
+    me.update(extra)
     if not dist.is_initialized():
         return {"backend": "none (single process)", "world_size": 1, "ranks": [me]}
     ranks = [None] * dist.get_world_size()
@@ -630,6 +633,28 @@ def dist_record(torch, dist, world, local):
 def xch_device(torch, dev):
     """Where the boundary exchange buffers live: HBM for RCCL, host for gloo."""
     return torch.device("cpu") if _share_gpu() else dev
+
+
+def test_fault(rank):
+    """Test-only fault injection (tests/test_bench_cli.py): ORBX_BENCH_TEST_FAULT
+    = "exit:R" ends rank R with status 7 after its warm-up steps, "hang:R"
+    parks it there, so the siblings block in the next collective; the job
+    must then end non-zero (launch_ranks stops the others once one rank has
+    failed; a parked rank trips the others' collective timeout)."""
+    f = os.environ.get("ORBX_BENCH_TEST_FAULT", "")
+    if not f:
+        return
+    kind, _, r = f.partition(":")
+    if int(r) != rank:
+        return
+    sys.stderr.write("bench.py: test fault %s on rank %d\n" % (kind, rank))
+    sys.stderr.flush()
+    if kind == "exit":
+        os._exit(7)
+    if kind == "hang":
+        while True:
+            time.sleep(1)
+    raise SystemExit("bench.py: unknown ORBX_BENCH_TEST_FAULT %r" % f)
 
 
 def finish_time(torch, dist, world, dev, el):
@@ -823,6 +848,7 @@ def main_mono(args, wl):
         step()
     plan.check()
     torch.cuda.synchronize()
+    test_fault(rank)
     plan.set_timing(True)
     if mp:
         mp.set_timing(True)
@@ -875,7 +901,8 @@ def main_mono(args, wl):
         same = bool(torch.equal(mp.match12[:B], ref12))
         if not same:
             raise SystemExit("bench.py: pipelined matches differ from the serial step")
-    drec = dist_record(torch, dist, world, local)  # collective: every rank
+    drec = dist_record(torch, dist, world, local, keypoints_last_batch=kps_total, matches_last_batch=nmatch,
+                       pipelined_equals_serial=same)  # collective: every rank
     if rank != 0:
         if multi:
             dist.destroy_process_group()
@@ -1093,6 +1120,7 @@ def main_c5(args, wl):
     pr.check()
     sp.check()
     torch.cuda.synchronize()
+    test_fault(rank)
     for o in (pl, pr, sp, mp):
         o.set_timing(True)
     if multi:
@@ -1117,6 +1145,7 @@ def main_c5(args, wl):
     nstereo = int(sp.nmatches[:B].sum().item())
     nmatch = int(mp.nmatches[:B].sum().item())
     el_serial = el
+    same = None
     if pipe is not None:
         for o in (pl, pr, sp, mp):
             o.set_timing(False)
@@ -1140,9 +1169,11 @@ def main_c5(args, wl):
         drain_ms = (time.perf_counter() - t1) * 1e3
         for _, _, sp_j in subs:
             sp_j.check()
-        if not torch.equal(mp.match12[:B], ref12):
+        same = bool(torch.equal(mp.match12[:B], ref12))
+        if not same:
             raise SystemExit("bench.py: pipelined matches differ from the serial step")
-    drec = dist_record(torch, dist, world, local)  # collective: every rank
+    drec = dist_record(torch, dist, world, local, keypoints_last_batch=kps_total, matches_last_batch=nmatch,
+                       stereo_matches_last_batch=nstereo, pipelined_equals_serial=same)  # collective: every rank
     if rank != 0:
         if multi:
             dist.destroy_process_group()

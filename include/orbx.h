@@ -22,7 +22,10 @@
 extern "C" {
 #endif
 
-#define ORBX_ABI_VERSION 1
+/* 2 (round 6): plan option flags 2 and 4 retired (ORBX_ERR_ARG), flags 8 / 16,
+ * orbx_proj_problem and the orbm_proj_plan_* / orbm_search_by_bow_kf_frame
+ * entry points added (round 5) */
+#define ORBX_ABI_VERSION 2
 
 /* status codes */
 enum {
@@ -176,9 +179,13 @@ int orbx_plan_extract(orbx_plan* plan, const uint8_t* d_frames, int nframes, siz
 int orbx_plan_check(orbx_plan* plan, void* stream);
 /* Debug counters since the last call (then reset; synchronises the plan's
  * stream): FAST strips whose corner list overflowed into the strength-map
- * scan.  Testing aid: ORBX_DEBUG_CCAP=<n> at plan creation lowers the list
- * capacity so the scan runs on ordinary frames. */
+ * scan (see orbx_debug_set_fast_ccap). */
 int orbx_plan_debug_counters(orbx_plan* plan, int* fast_overflow_strips);
+/* Testing only: plans created after this call give the FAST kernels a
+ * corner list of `ccap` entries (<= 1024) in one launch group, so the
+ * strength-map overflow path runs on ordinary frames; ccap < 0 restores the
+ * planner's own length.  Process-global; results are unchanged either way. */
+int orbx_debug_set_fast_ccap(int ccap);
 
 /* Kernel-path options of a plan (default 0 = automatic; persistent).  Every
  * path gives bit-identical results; they differ in speed only.
@@ -441,9 +448,12 @@ int orbm_search_by_projection(int mode, const orbx_proj_frame* frame, const orbx
  * / uright / occupied, q, qdesc; outputs match[frame.n] and *nmatches);
  * asynchronous on `stream`.  Same results as orbm_search_by_projection on
  * each problem.  A plan holds the scratch for max_problems problems of at
- * most max_n features (<= 8192) and max_nq queries; one call at a time per
- * plan (the problem table is staged in pinned memory; a call waits for the
- * previous call's table upload, not for its kernels). */
+ * most max_n features (<= 8192) and max_nq queries; one host thread calls a
+ * plan at a time (the problem table is staged in pinned memory; a call
+ * waits on the host for the previous call's table upload, not for its
+ * kernels).  Calls may use different streams: each call's stream waits on
+ * the device for the previous call's kernels before it reuses the plan's
+ * scratch. */
 typedef struct {
   orbx_proj_frame frame;
   const orbx_query_proj* q;

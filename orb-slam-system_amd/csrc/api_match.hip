@@ -340,6 +340,17 @@ extern "C" int orbm_search_by_bow_kf_frame(const orbx_bow_frame* kf, const orbx_
   /* the sentinel scheme assumes a second-best of 256 (upstream's initial
    * bestDist2) passes the ratio test for every acceptable best */
   if (orbm_dcap(nnratio, ORBM_TH_LOW + 1) > 256) return ORBX_ERR_UNSUPPORTED;
+  /* a KF feature listed under two nodes (never in a DBoW2 FeatureVector) would
+   * leave one row per KF index in the row -> candidate result while nmatches
+   * counts both: rejected */
+  if (kf && kf->n > 0 && kf->nnodes > 0 && kf->node_off && kf->feat) {
+    std::vector<unsigned char> seen((size_t)kf->n, 0);
+    for (uint32_t j = 0; j < kf->node_off[kf->nnodes]; ++j) {
+      const uint32_t i = kf->feat[j];
+      if (i >= (uint32_t)kf->n || seen[i]) return ORBX_ERR_ARG;
+      seen[i] = 1;
+    }
+  }
   orbx_bow_frame fr = *frame;
   fr.valid = nullptr;  /* every Frame feature is a candidate */
   std::vector<int32_t> m(kf && kf->n > 0 ? (size_t)kf->n : 1, -1);

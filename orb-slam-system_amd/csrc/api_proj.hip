@@ -142,6 +142,7 @@ struct orbm_proj_plan {
   ProjProblem* d_probs = nullptr;
   ProjProblem* h_probs = nullptr;  // pinned staging of the problem table
   hipEvent_t ev = nullptr;         // the last table upload (h_probs reusable after it)
+  hipEvent_t ev_done = nullptr;    // the last call's kernels (its grid / candidate scratch free after it)
   int* d_cell_off = nullptr;
   int* d_cell_feat = nullptr;
   uint32_t* d_cand = nullptr;
@@ -152,6 +153,7 @@ static void proj_plan_free(orbm_proj_plan* p) {
   if (!p) return;
   hipSetDevice(p->device);
   if (p->ev) hipEventDestroy(p->ev);
+  if (p->ev_done) hipEventDestroy(p->ev_done);
   if (p->h_probs) hipHostFree(p->h_probs);
   void* bufs[] = {p->d_probs, p->d_cell_off, p->d_cell_feat, p->d_cand, p->d_ncand};
   for (void* b : bufs)
@@ -175,6 +177,7 @@ extern "C" int orbm_proj_plan_create(int max_problems, int max_n, int max_nq, in
   if (hipMalloc((void**)&p->d_probs, B * sizeof(ProjProblem)) != hipSuccess ||
       hipHostMalloc((void**)&p->h_probs, B * sizeof(ProjProblem), hipHostMallocDefault) != hipSuccess ||
       hipEventCreateWithFlags(&p->ev, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&p->ev_done, hipEventDisableTiming) != hipSuccess ||
       hipMalloc((void**)&p->d_cell_off, B * (PG_CELLS + 1) * sizeof(int)) != hipSuccess ||
       hipMalloc((void**)&p->d_cell_feat, B * (size_t)max_n * sizeof(int)) != hipSuccess ||
       hipMalloc((void**)&p->d_cand, B * (size_t)std::max(max_nq, 1) * PJ_T * sizeof(uint32_t)) != hipSuccess ||
@@ -214,6 +217,11 @@ extern "C" int orbm_proj_plan_search(orbm_proj_plan* p, int mode, int nprob, con
   ORBX_TRY(hipSetDevice(p->device));
   hipStream_t s = (hipStream_t)stream;
   ORBX_TRY(hipEventSynchronize(p->ev));  // the previous call's table has left the staging buffer
+  // every call reuses the plan's device scratch (problem table, grids,
+  // candidates): a call on another stream than the previous one's must not
+  // overwrite them under the previous call's kernels -- the
+  // stream waits for them on the device; no host block
+  ORBX_TRY(hipStreamWaitEvent(s, p->ev_done, 0));
   for (int i = 0; i < nprob; ++i) {
     const orbx_proj_problem& q = probs[i];
     ProjProblem& P = p->h_probs[i];
@@ -236,5 +244,6 @@ extern "C" int orbm_proj_plan_search(orbm_proj_plan* p, int mode, int nprob, con
   ORBX_TRY(hipEventRecord(p->ev, s));
   launch_proj(p->d_probs, nprob, max_n, max_nq, mode, nnratio, th_dist, check_ori, s);
   if (hipGetLastError() != hipSuccess) return ORBX_ERR_HIP;
+  ORBX_TRY(hipEventRecord(p->ev_done, s));
   return ORBX_OK;
 }

@@ -58,6 +58,11 @@ namespace orbx {
 
 __device__ __forceinline__ int lane_id() { return __lane_id(); }
 
+// LDS byte address of a __shared__ pointer (an operand of hand-written ds_*)
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
+}
+
 
 // 16-B chunk as a native LLVM vector: HIP's uint4 class defeats SROA when it
 // is held in a local array (stage_region's loads would bounce through scratch).
@@ -497,7 +502,7 @@ __device__ __forceinline__ int wave_excl_scan(int n, int lane, int* total) {
 // ---------------------------------------------------------------------------
 // TP: the tile pitch as a compile-time constant (every LDS offset of stage A
 // an immediate of one address register), 0 = runtime pitch
-template <int TP>
+template <int TP, bool PF = false>
 __device__ __forceinline__ void fs_strip_body(
     uint8_t* __restrict__ tile, uint8_t* __restrict__ amap_mem, int* __restrict__ cnt,
     unsigned long long* __restrict__ mask, unsigned long long* __restrict__ mask2,
@@ -531,13 +536,21 @@ __device__ __forceinline__ void fs_strip_body(
   // nothing of the staging is in flight any more: an explicit vmcnt(0) here
   // lets the waitcnt pass drop the (run-time no-op) vmcnt waits it otherwise
   // re-inserts every stage-A iteration for registers the staging loads used
-  __builtin_amdgcn_s_waitcnt(0x0F70);
+  // (PF, the persistent kernel: the next unit's tile loads stay in flight)
+  if (!PF) __builtin_amdgcn_s_waitcnt(0x0F70);
   const int g0 = c0 >> 2, g1 = (c1 + 3) >> 2, ng = g1 - g0;
   const int ntask = ng * bh;
   uint16_t* L1 = wlist1[wave];
   uint16_t* L2 = wlist2[wave];
   int n2 = 0;  // wave-uniform list length of L2
   int n1 = 0;  // wave-uniform L1 length
+#ifndef FS_APPEND_CC
+  // L1's end as an LDS byte address (SGPR): stage A's appends advance it in
+  // scalar code, n1 is derived from it only where the list is consumed
+  const uint32_t l1base = lds_addr(L1);
+  uint32_t l1a = l1base;
+  const unsigned long long exec_all = __builtin_amdgcn_read_exec();
+#endif
 #ifdef FS_PROBE_NOAPP
   uint32_t probe_sink = 0;
 #endif
@@ -635,7 +648,12 @@ __device__ __forceinline__ void fs_strip_body(
       if (zf) *reinterpret_cast<uint32_t*>(zp) = 0u;
     };
     auto l1_flush = [&]() {
+#ifndef FS_APPEND_CC
+      if (l1a >= l1base + 2u * FS_L1FLUSH) {  // wave-uniform
+        n1 = (int)((l1a - l1base) >> 1);
+#else
       if (n1 >= FS_L1FLUSH) {  // wave-uniform
+#endif
         wave_sync_lds();
         while (n1 >= 64) {
           n1 -= 64;
@@ -644,6 +662,9 @@ __device__ __forceinline__ void fs_strip_body(
 #endif
         }
         wave_sync_lds();
+#ifndef FS_APPEND_CC
+        l1a = l1base + 2u * (uint32_t)n1;
+#endif
       }
     };
     auto gtest = [&](const GroupWords& q, uint8_t* zp, uint32_t ebase, uint32_t ttl, bool zf) {
@@ -657,7 +678,53 @@ __device__ __forceinline__ void fs_strip_body(
       probe_sink |= clo | chi;
       return;
 #endif
-#ifndef FS_N1_VGPR
+#ifndef FS_APPEND_CC
+      // Branch-free appends (round 6).  The CU's one scalar unit issues about
+      // one instruction per cycle (tools/probe/issue_rates.hip: 0.93-0.96
+      // SALU per CU-cycle at 4-8 waves per SIMD), and the compiler's form of
+      // `if (k) L1[n1 + mbcnt] = e; n1 += popcount` spent 7 scalar
+      // instructions per append (s_and_saveexec, s_cbranch_execz, s_lshl,
+      // s_add, s_or exec, s_bcnt1, s_add).  Here exec is set straight from
+      // each compare's ballot around its store and the list end advances by
+      // one s_lshl1_add per append: 13 scalar instructions per group of 4
+      // pixels instead of 28 (a store with no active lane writes nothing).
+      {
+        const unsigned long long b0 = __ballot((uint16_t)clo != 0), b1 = __ballot((uint16_t)chi != 0),
+                                 b2 = __ballot(clo > 0xFFFFu), b3 = __ballot(chi > 0xFFFFu);
+        const uint32_t p0 = (uint32_t)lanes_below(b0), p1 = (uint32_t)lanes_below(b1),
+                       p2 = (uint32_t)lanes_below(b2), p3 = (uint32_t)lanes_below(b3);
+        const uint32_t e0 = ebase, e1 = ebase + 1u, e2 = ebase + 2u, e3 = ebase + 3u;
+        uint32_t a0, a1, a2, a3, t;
+        asm volatile(
+            "s_bcnt1_i32_b64 %[t], %[b0]\n\t"
+            "v_lshl_add_u32 %[a0], %[p0], 1, %[la]\n\t"
+            "s_lshl1_add_u32 %[la], %[t], %[la]\n\t"
+            "s_bcnt1_i32_b64 %[t], %[b1]\n\t"
+            "v_lshl_add_u32 %[a1], %[p1], 1, %[la]\n\t"
+            "s_lshl1_add_u32 %[la], %[t], %[la]\n\t"
+            "s_bcnt1_i32_b64 %[t], %[b2]\n\t"
+            "v_lshl_add_u32 %[a2], %[p2], 1, %[la]\n\t"
+            "s_lshl1_add_u32 %[la], %[t], %[la]\n\t"
+            "s_bcnt1_i32_b64 %[t], %[b3]\n\t"
+            "v_lshl_add_u32 %[a3], %[p3], 1, %[la]\n\t"
+            "s_lshl1_add_u32 %[la], %[t], %[la]\n\t"
+            "s_mov_b64 exec, %[b0]\n\t"
+            "ds_write_b16 %[a0], %[e0]\n\t"
+            "s_mov_b64 exec, %[b1]\n\t"
+            "ds_write_b16 %[a1], %[e1]\n\t"
+            "s_mov_b64 exec, %[b2]\n\t"
+            "ds_write_b16 %[a2], %[e2]\n\t"
+            "s_mov_b64 exec, %[b3]\n\t"
+            "ds_write_b16 %[a3], %[e3]\n\t"
+            "s_mov_b64 exec, %[ex]"
+            : [la] "+s"(l1a), [t] "=&s"(t), [a0] "=&v"(a0), [a1] "=&v"(a1), [a2] "=&v"(a2), [a3] "=&v"(a3)
+            : [b0] "s"(b0), [b1] "s"(b1), [b2] "s"(b2), [b3] "s"(b3), [p0] "v"(p0), [p1] "v"(p1),
+              [p2] "v"(p2), [p3] "v"(p3), [e0] "v"(e0), [e1] "v"(e1), [e2] "v"(e2), [e3] "v"(e3),
+              [ex] "s"(exec_all)
+            : "memory", "scc");
+      }
+#else
+      // profiling variant: the compiler's branchy appends (rounds 1-5)
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const uint32_t x = (j & 1) ? chi : clo;
@@ -669,24 +736,6 @@ __device__ __forceinline__ void fs_strip_body(
         if (k) L1n[pos] = (uint16_t)(ebase + (uint32_t)j);
         n1 += __popcll(bal);
       }
-#else
-      // profiling variant: the list length in a VGPR (same value in every
-      // lane): slot = mbcnt(ballot) with n1 as its addend, n1 += v_bcnt of
-      // both ballot halves -- 7 VALU + 2 SALU per append instead of 5 + 7.
-      // Measured slower (c4 FAST 1.248 vs 1.202 ms, round 4): the CU-shared
-      // scalar unit is not what binds this kernel, VALU issue is
-      uint32_t n1v = (uint32_t)n1;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const uint32_t x = (j & 1) ? chi : clo;
-        const bool k = ((j & 2) ? (x >> 16) : (x & 0xFFFFu)) != 0;
-        const unsigned long long bal = __ballot(k);
-        const uint32_t blo = (uint32_t)bal, bhi = (uint32_t)(bal >> 32);
-        const int pos = (int)__builtin_amdgcn_mbcnt_hi(bhi, __builtin_amdgcn_mbcnt_lo(blo, n1v));
-        if (k) L1[pos] = (uint16_t)(ebase + (uint32_t)j);
-        asm("v_bcnt_u32_b32 %0, %1, %0\n\tv_bcnt_u32_b32 %0, %2, %0" : "+v"(n1v) : "s"(blo), "s"(bhi));
-      }
-      n1 = __builtin_amdgcn_readfirstlane((int)n1v);
 #endif
 #ifdef FS_PROBE_SALU  // profiling only: FS_PROBE_SALU extra scalar instructions per group
       {
@@ -800,6 +849,9 @@ __device__ __forceinline__ void fs_strip_body(
       }
     }
     wave_sync_lds();
+#ifndef FS_APPEND_CC
+    n1 = (int)((l1a - l1base) >> 1);
+#endif
     while (n1 >= 64) {  // leftovers above one batch (FS_L1FLUSH > 64)
       n1 -= 64;
       even_batch(L1[n1 + lane], true);
@@ -1040,6 +1092,165 @@ __global__ __launch_bounds__(FS_NT) FS_ATTR void k_fast_strips(FS_KERNEL_ARGS) {
 // the plan's tile pitch is 288 for every strip width in 224..264 (all the
 // bench workloads): immediates instead of per-iteration address adds
 __global__ __launch_bounds__(FS_NT) FS_ATTR void k_fast_strips_p288(FS_KERNEL_ARGS) { fs_kernel<288>(FS_KERNEL_PASS); }
+
+// ---------------------------------------------------------------------------
+// k_fast_pf: the same strip body in a persistent loop whose next unit's tile
+// is loaded into registers while the current unit is processed (round 6).
+// Per-phase SQ counters of k_fast_strips (tools/phase_sq.sh, c4) put a third
+// of a wave's 18.4 K cycles before its first pixel test: the tile's row loads
+// (6.0 K cycles, 49 % of them parked on vmcnt).  A grid of G resident
+// workgroups walks the (strip, frame) units u = blockIdx.x + i * G; unit
+// u + G's tile (<= FS_PF_DW dwords per thread) is requested right after unit
+// u's tile went to LDS and lands during unit u's passes, so only the first
+// unit of a workgroup waits for memory.  Every unit runs fs_strip_body's
+// block-staged form (stage A from the LDS tile; no column walk, whose rows
+// live in the registers the prefetch needs).  Units keep the plain grid's
+// XCD of unit u (G is a multiple of 8).
+// ---------------------------------------------------------------------------
+// where a unit's tile comes from: recomputed from (strip, frame) wherever it
+// is needed instead of carried across the strip body in scalar registers.
+// The launcher takes this kernel only when every level's rows are 16-B
+// aligned (the caller's frames and row stride; the pyramid buffer always is),
+// so the tile moves in 16-B chunks: one load form, nothing for the compiler
+// to hoist across a mode test (with a dword form beside it, the chunk loads
+// waited for hoisted dword loads)
+struct FsSrc {
+  int nper, total, xal;
+  uint32_t pitch;
+  const uint8_t* s0;
+};
+__device__ __forceinline__ FsSrc fs_pf_src(const StripInfo& st, int f, const uint8_t* __restrict__ frames,
+                                           size_t fstride, size_t rstride, const uint8_t* __restrict__ pyr,
+                                           size_t pstride, const LevelArgs& LA) {
+  FsSrc g;
+  const int pitch = st.level == 0 ? (int)rstride : LA.pitch[st.level];
+  const uint8_t* base = st.level == 0 ? frames + (size_t)f * fstride : pyr + (size_t)f * pstride + LA.pyr_off[st.level];
+  g.xal = st.x & ~15;
+  g.nper = (st.x - g.xal + st.w + 15) >> 4;
+  g.total = st.h * g.nper;
+  g.pitch = (uint32_t)pitch;
+  g.s0 = base + (size_t)st.y * pitch + g.xal;
+  return g;
+}
+
+// issue the tile loads of unit (sx, f) into R (chunk e = tid + FS_NT k:
+// (row, chunk) stepped without divisions; loads past the tile repeat its
+// last row: unconditional, so nothing waits for them here) and its cells'
+// slot offsets
+__device__ __forceinline__ void fs_pf_fetch(uint32_t (&R)[FS_PF_DW], int& slot_pref, const uint8_t* __restrict__ frames,
+                                            size_t fstride, size_t rstride, const uint8_t* __restrict__ pyr,
+                                            size_t pstride, const LevelArgs& LA, const CellInfo* __restrict__ cells,
+                                            const StripInfo* __restrict__ strips, int sx, int f) {
+  const int tid = threadIdx.x;
+  const StripInfo st = strips[sx];
+  const FsSrc g = fs_pf_src(st, f, frames, fstride, rstride, pyr, pstride, LA);
+  const int nper = g.nper, dr = FS_NT / nper, dc = FS_NT - dr * nper;
+  int r = tid / nper, c = tid - r * nper;
+#pragma unroll
+  for (int k = 0; k < FS_PF_DW / 4; ++k) {
+    const v4u v = *reinterpret_cast<const v4u*>(g.s0 + (__umul24((uint32_t)min(r, st.h - 1), g.pitch) + 16u * (uint32_t)c));
+    R[4 * k] = v.x;
+    R[4 * k + 1] = v.y;
+    R[4 * k + 2] = v.z;
+    R[4 * k + 3] = v.w;
+    r += dr;
+    c += dc;
+    if (c >= nper) { c -= nper; ++r; }
+  }
+  // last, at a clamped index: a load under `tid < ncells` would be waited for
+  // at the branch's join (lanes past ncells never use the value)
+  slot_pref = cells[st.cell_begin + min(tid, max(st.ncells - 1, 0))].slot_off;
+}
+
+__device__ __forceinline__ void fs_pf_commit(const uint32_t (&R)[FS_PF_DW], const FsSrc& g, uint8_t* __restrict__ tile,
+                                             int tpitch) {
+  const int tid = threadIdx.x;
+  const int nper = g.nper, dr = FS_NT / nper, dc = FS_NT - dr * nper;
+  int r = tid / nper, c = tid - r * nper;
+#pragma unroll
+  for (int k = 0; k < FS_PF_DW / 4; ++k) {
+    if (tid + FS_NT * k < g.total) {
+      v4u v;
+      v.x = R[4 * k];
+      v.y = R[4 * k + 1];
+      v.z = R[4 * k + 2];
+      v.w = R[4 * k + 3];
+      reinterpret_cast<v4u*>(tile + __mul24(r, tpitch))[c] = v;
+    }
+    r += dr;
+    c += dc;
+    if (c >= nper) { c -= nper; ++r; }
+  }
+}
+
+template <int TP>
+__device__ __forceinline__ void fs_pf_kernel(
+    const uint8_t* __restrict__ frames, size_t fstride, size_t rstride,
+    const uint8_t* __restrict__ pyr, size_t pstride, const LevelArgs& LA,
+    const CellInfo* __restrict__ cells, const StripInfo* __restrict__ strips,
+    uint32_t* __restrict__ slots, size_t slot_stride, uint32_t* __restrict__ ccount, int ncells,
+    int ini_th, int min_th, int tpitch_rt, int tmax_h, int mcells, int ccap, int* __restrict__ ovf,
+    int strip0, int dbg, int nstrips, int nunits) {
+  const int tpitch = TP ? TP : tpitch_rt;
+  extern __shared__ __align__(16) uint32_t sm[];  // layout as fs_kernel
+#if ORBX_EX_PRIO
+  if (LA.prio) __builtin_amdgcn_s_setprio(ORBX_EX_PRIO);
+#endif
+  uint8_t* tile = reinterpret_cast<uint8_t*>(sm);
+  uint8_t* amap_mem = tile + tpitch * tmax_h;
+  int* cnt = reinterpret_cast<int*>(amap_mem + tpitch * (tmax_h - 6));
+  int* cslot = cnt + ((mcells + 3) & ~3);
+  uint16_t* clist = reinterpret_cast<uint16_t*>(cslot + ((mcells + 3) & ~3));
+  const bool masks_in_tile = 16 * mcells * (tmax_h - 6) <= tpitch * tmax_h;
+  unsigned long long* mask = masks_in_tile ? reinterpret_cast<unsigned long long*>(tile)
+                                           : reinterpret_cast<unsigned long long*>(clist + ((ccap + 3) & ~3));
+  unsigned long long* mask2 = mask + mcells * (tmax_h - 6);
+  __shared__ uint16_t wlist1[FS_NW][FS_L1CAP];
+  __shared__ uint16_t wlist2[FS_NW][FS_L2CAP];
+  __shared__ int ncorner;
+  const int G = (int)gridDim.x;
+  int u = (int)blockIdx.x;
+  if (u >= nunits) return;
+  // units u, u + G, ...: (strip s, frame f) stepped without divisions
+  int s = u % nstrips, f = u / nstrips;
+  const int gs = G % nstrips, gf = G / nstrips;
+  uint32_t R[FS_PF_DW];
+  int slot_cur, slot_next = 0;
+  fs_pf_fetch(R, slot_cur, frames, fstride, rstride, pyr, pstride, LA, cells, strips, strip0 + s, f);
+  for (;;) {
+    __syncthreads();  // the previous unit's passes are done with the tile, map and lists
+    const StripInfo st = strips[strip0 + s];
+    const int fc = f;
+    {
+      const FsSrc g = fs_pf_src(st, fc, frames, fstride, rstride, pyr, pstride, LA);
+      fs_pf_commit(R, g, tile, tpitch);
+    }
+    const int xal = st.x & ~15;
+    u += G;
+    s += gs;
+    f += gf;
+    if (s >= nstrips) {
+      s -= nstrips;
+      ++f;
+    }
+    const bool more = u < nunits;  // workgroup-uniform
+    if (more) fs_pf_fetch(R, slot_next, frames, fstride, rstride, pyr, pstride, LA, cells, strips, strip0 + s, f);
+    fs_strip_body<TP, true>(tile, amap_mem, cnt, mask, mask2, wlist1, wlist2, clist, cslot, ncorner, st, fc,
+                            st.x - xal, xal, slot_cur, slots, slot_stride, ccount, ncells, ini_th, min_th, tpitch, ccap,
+                            ovf, dbg, nullptr, 0, false, LA.key_xs);
+    if (!more) break;
+    slot_cur = slot_next;
+  }
+}
+
+#ifndef FS_PF_WPE
+#define FS_PF_WPE 6 /* 6 workgroups per CU, as LDS allows: <= 80 VGPRs */
+#endif
+#define FS_PF_ATTR __attribute__((amdgpu_waves_per_eu(FS_PF_WPE)))
+#define FS_PF_ARGS FS_KERNEL_ARGS, int nstrips, int nunits
+#define FS_PF_PASS FS_KERNEL_PASS, nstrips, nunits
+__global__ __launch_bounds__(FS_NT) FS_PF_ATTR void k_fast_pf(FS_PF_ARGS) { fs_pf_kernel<0>(FS_PF_PASS); }
+__global__ __launch_bounds__(FS_NT) FS_PF_ATTR void k_fast_pf_p288(FS_PF_ARGS) { fs_pf_kernel<288>(FS_PF_PASS); }
 
 // ---------------------------------------------------------------------------
 // Block-wide exclusive scan of an LDS int array (256 threads), returns total.

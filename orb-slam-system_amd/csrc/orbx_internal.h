@@ -107,6 +107,9 @@ struct StereoArgs {
   float scale[ORBX_MAX_LEVELS], inv_scale[ORBX_MAX_LEVELS];
   float mb, mbf;
 };
+#ifndef FS_PF_DW
+#define FS_PF_DW 12 /* k_fast_pf: prefetched tile dwords per thread (tiles up to FS_NT * 48 B; 16 spills at 80 VGPRs) */
+#endif
 #ifndef FS_NT
 #define FS_NT 256 /* threads per k_fast_strips workgroup (one strip) */
 #endif

@@ -51,7 +51,7 @@ EXPORTED = [
     "orbx_extractor_set_options", "orbx_extractor_level_host", "orbx_extractor_stats",
     "orbx_boundary_record_bytes", "orbx_boundary_pack", "orbx_boundary_unpack",
     "orbx_plan_create", "orbx_plan_destroy", "orbx_plan_geometry", "orbx_plan_extract",
-    "orbx_plan_check", "orbx_plan_debug_counters", "orbx_plan_set_options", "orbx_plan_level", "orbx_stage_count", "orbx_stage_name", "orbx_plan_set_timing",
+    "orbx_plan_check", "orbx_plan_debug_counters", "orbx_debug_set_fast_ccap", "orbx_plan_set_options", "orbx_plan_level", "orbx_stage_count", "orbx_stage_name", "orbx_plan_set_timing",
     "orbx_plan_stage_times", "orbx_synth_frames", "orbm_search_by_bow", "orbm_search_by_bow_kf_frame",
     "orbm_descriptor_distance_batch", "orbm_plan_create", "orbm_plan_destroy",
     "orbm_plan_match_frames", "orbm_plan_set_timing", "orbm_plan_stage_times", "orbm_plan_set_options",
@@ -139,6 +139,7 @@ _sig = {
     "orbx_plan_extract": (I, [P, P, I, SZ, SZ, P, P, P, P]),
     "orbx_plan_check": (I, [P, P]),
     "orbx_plan_debug_counters": (I, [P, P]),
+    "orbx_debug_set_fast_ccap": (I, [I]),
     "orbx_plan_set_options": (I, [P, I]),
     "orbx_plan_level": (I, [P, I, I, P, SZ, P, P, P]),
     "orbx_stage_count": (I, []),

@@ -106,3 +106,62 @@ def test_bench_c4_host_fed_and_latency_legs():
     co = lat["compat_operator_1920x1080"]
     assert co["operator_with_mvImagePyramid"]["checksum"] != 0
     assert co["operator_with_mvImagePyramid"]["keypoints"] == co["operator_no_pyramid"]["keypoints"]
+
+
+def _bench(args, extra_env=None, timeout=600):
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(extra_env or {})
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args + ["--no-cpu-baseline", "--no-latency"],
+                          env=env, capture_output=True, text=True, timeout=timeout)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("wl,batch", [("c4", 8), ("c5", 8), ("c5", 1)])
+def test_bench_four_ranks_on_one_gpu(wl, batch):
+    # rehearsal of the N-GPU path with 4 ranks (the ring wrap: rank 0 takes
+    # rank 3's previous-step record); c5 at --batch 1 is configs[4]'s literal
+    # shape, one frame pair in flight per rank.  Every rank's pipelined
+    # matches must equal its serial loop's (bench.py aborts otherwise) and
+    # the line must name all 4 ranks.
+    r = _bench(["--gpus", "4", "--workload", wl, "--batch", str(batch), "--steps", "3", "--warmup", "1"],
+               {"ORBX_BENCH_SHARE_GPU": "1"})
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    dr = d["distributed"]
+    assert d["n_gpus"] == 4 and dr["world_size"] == 4 and len(dr["ranks"]) == 4
+    assert all(x["pipelined_equals_serial"] in (True, None) for x in dr["ranks"])
+    assert all(x["matches_last_batch"] > 0 for x in dr["ranks"])
+
+
+@pytest.mark.gpu
+def test_bench_sharded_matches_equal_one_rank():
+    # frame sharding changes who matches which pair, not the pairs: 4 ranks
+    # x 2 frames match (0,7) (rank 0, across the ring wrap), (1,0), (2,1) ..
+    # (7,6), the same pairs one rank x 8 frames matches, so the summed
+    # keypoints and matches must be equal
+    one = _bench(["--workload", "c1", "--batch", "8", "--steps", "2", "--warmup", "2"])
+    assert one.returncode == 0, one.stderr[-3000:]
+    d1 = json.loads(one.stdout.strip().splitlines()[-1])
+    four = _bench(["--gpus", "4", "--workload", "c1", "--batch", "2", "--steps", "2", "--warmup", "2"],
+                  {"ORBX_BENCH_SHARE_GPU": "1"})
+    assert four.returncode == 0, four.stderr[-3000:]
+    d4 = json.loads(four.stdout.strip().splitlines()[-1])
+    rk = d4["distributed"]["ranks"]
+    assert sum(x["keypoints_last_batch"] for x in rk) == d1["config"]["keypoints_last_batch"]
+    assert sum(x["matches_last_batch"] for x in rk) == d1["config"]["matches_last_batch"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fault", ["exit:1", "hang:1"])
+def test_bench_failed_rank_ends_job(fault):
+    # a rank that dies, or stops answering, must end the whole job non-zero
+    # (no hang): launch_ranks stops the siblings of a failed rank, and a
+    # parked rank trips the others' collective timeout
+    import time
+    t0 = time.time()
+    r = _bench(["--gpus", "2", "--workload", "c1", "--batch", "4", "--steps", "2", "--warmup", "1"],
+               {"ORBX_BENCH_SHARE_GPU": "1", "ORBX_BENCH_TEST_FAULT": fault, "ORBX_COLLECTIVE_TIMEOUT_S": "20"},
+               timeout=300)
+    assert r.returncode != 0
+    assert "test fault" in r.stderr
+    assert time.time() - t0 < 240

@@ -1,5 +1,6 @@
-"""Multi-process (gloo, world size 2) checks of the frame-sharded exchange
-used by bench.py on N GPUs (RCCL there, gloo here)."""
+"""Multi-process (gloo, world sizes 2, 4 and 8) checks of the frame-sharded
+exchange used by bench.py on N GPUs (RCCL there, gloo here): SURVEY §8(e),
+BASELINE.json configs[4] (8 frames in flight over 8 GPUs)."""
 import os
 import socket
 
@@ -46,7 +47,7 @@ def _worker(rank, world, port, kcap, q):
         # ring_step over two steps: rank r > 0 gets rank r-1's frame of the same
         # step; rank 0 gets rank W-1's frame of the previous step (zeros first)
         y = BoundaryExchange(kcap, world, torch.device("cpu"))
-        for st in range(2):
+        for st in range(4):  # steps 2, 3 reuse the alternating gather buffers
             last = (torch.full((kcap, 28), 10 * st + rank, dtype=torch.uint8),
                     torch.full((kcap, 32), 10 * st + rank, dtype=torch.uint8),
                     torch.tensor([10 * st + rank], dtype=torch.int32))
@@ -63,7 +64,7 @@ def _worker(rank, world, port, kcap, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2])
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_boundary_exchange_gloo(world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()

@@ -235,14 +235,17 @@ def test_plan_argument_checks(gpu, oracle):
                                                 (1241, 376, 2000, "strict", 96)])
 def test_fast_corner_list_overflow_path(gpu, oracle, monkeypatch, W, H, nf, guard, ccap):
     """k_fast_strips' per-strip corner list overflow: with the list capacity
-    lowered (ORBX_DEBUG_CCAP, read at plan creation) the NMS walks the
-    strength map instead of the list.  The debug counter proves the branch
-    ran; every keypoint field and descriptor byte must still equal the oracle."""
+    lowered (orbx_debug_set_fast_ccap, read at plan creation) the NMS walks
+    the strength map instead of the list.  The debug counter proves the
+    branch ran; every keypoint field and descriptor byte must still equal the
+    oracle."""
     import torch
     B = 3
-    monkeypatch.setenv("ORBX_DEBUG_CCAP", str(ccap))
-    plan = gpu.Plan(gpu.params(nf, 1.2, 8, 20, 7, guard), W, H, B)
-    monkeypatch.delenv("ORBX_DEBUG_CCAP")
+    assert gpu.lib().orbx_debug_set_fast_ccap(ccap) == gpu.OK
+    try:
+        plan = gpu.Plan(gpu.params(nf, 1.2, 8, 20, 7, guard), W, H, B)
+    finally:
+        gpu.lib().orbx_debug_set_fast_ccap(-1)
     kinds = ("noise", "rects", "pan")
     frames = np.stack([synth.frame(W, H, 60 + f, kinds[f]) for f in range(B)])
     plan.extract(torch.from_numpy(frames).cuda())
@@ -360,6 +363,24 @@ def test_search_by_bow_single_node_bruteforce(gpu, oracle):
         assert nm == rnm and np.array_equal(m, rm)
 
 
+def test_search_by_bow_kf_frame_rejects_repeated_kf_features(gpu, oracle):
+    """A KF feature listed under two nodes (no DBoW2 FeatureVector does that)
+    would make the KF-Frame form's row -> Frame-feature inversion lose a
+    match that nmatches still counts: the entry point rejects such a KF
+    (ORBX_ERR_ARG); a repeated Frame feature stays allowed."""
+    rng = np.random.default_rng(13)
+    d = rng.integers(0, 256, (200, 32), dtype=np.uint8)
+    kf_dup = _random_bow(rng, 200, 5, 20, d, dup=True)
+    assert len(np.unique(kf_dup["feat"])) < len(kf_dup["feat"])
+    fr = _random_bow(rng, 200, 5, 20, _correlated(rng, d, rng.integers(0, 30, 200)))
+    with pytest.raises(gpu.OrbxError):
+        gpu.search_by_bow_kf_frame(kf_dup, fr, 0.75, True)
+    kf = _random_bow(rng, 200, 5, 20, d)
+    m, nm = gpu.search_by_bow_kf_frame(kf, fr, 0.75, True)
+    rm, rnm = oracle.search_by_bow_kf_frame(kf, fr, 0.75, True)
+    assert nm == rnm and np.array_equal(m, rm)
+
+
 def test_search_by_bow_duplicate_features_sequential(gpu, oracle):
     rng = np.random.default_rng(11)
     d = rng.integers(0, 256, (300, 32), dtype=np.uint8)
@@ -461,7 +482,7 @@ def test_search_by_bow_rescan_long_lists(gpu, oracle, nfill, valid):
     nfill unrelated ones, 700 KF1 rows near the patterns: once a row's eight
     candidates are claimed by earlier rows of its pattern, it rescans the
     whole list (180-321 rescans per case at ratio 1.0, none at 0.75: RS_STATS
-    build, tools/r05_rsl.sh).  The resolver's
+    build, tools/probes/r05_rsl.sh).  The resolver's
     rescan takes 64 x RS_RU (512) positions per batch: 511 / 512 / 513
     positions around one batch, several batches, with and without validity
     bytes."""

@@ -22,7 +22,7 @@ def test_library_exports_every_header_function(orbx_mod):
     missing = [n for n in decl if not hasattr(orbx_mod.lib(), n)]
     assert not missing, missing
     assert set(orbx_mod.EXPORTED) == decl
-    assert orbx_mod.lib().orbx_abi_version() == 1
+    assert orbx_mod.lib().orbx_abi_version() == 2  # include/orbx.h ORBX_ABI_VERSION (flags 2 / 4 retired)
 
 
 @pytest.mark.parametrize("nf,L", [(1000, 8), (2000, 8), (1200, 8), (1000, 1), (1500, 6)])
@@ -112,13 +112,15 @@ def test_release_library_reads_no_profiling_knobs():
     """The ORBX_DEBUG_* / ORBX_CHUNK environment knobs (phase early exits, grid
     divisors, chunked passes) exist only in profiling builds (-DORBX_PROFILING,
     tools/variant.sh): the release liborbx.so does not contain their names, so
-    an inherited environment cannot change its results.  ORBX_DEBUG_CCAP stays
-    (a test hook that moves the FAST corner-list overflow path, results equal)."""
+    an inherited environment cannot change its results.  The FAST corner-list
+    test hook is a C entry point (orbx_debug_set_fast_ccap), not a variable
+    (ADVICE r5)."""
     blob = open(os.path.join(PKG, "liborbx.so"), "rb").read()
     for knob in (b"ORBX_DEBUG_STOP", b"ORBX_DEBUG_OBDIV", b"ORBX_CHUNK", b"ORBX_DEBUG_OVERLAP",
-                 b"ORBX_DEBUG_SMDIV", b"ORBX_DEBUG_PYR_TILE", b"ORBX_DEBUG_PYR_MAXSEG"):
+                 b"ORBX_DEBUG_SMDIV", b"ORBX_DEBUG_PYR_TILE", b"ORBX_DEBUG_PYR_MAXSEG", b"ORBX_DEBUG_CCAP",
+                 b"ORBX_DEBUG_FSPF"):
         assert knob not in blob, knob
-    assert b"ORBX_DEBUG_CCAP" in blob
+    assert b"orbx_debug_set_fast_ccap" in blob
 
 
 def test_no_device_fails_loudly(orbx_mod):

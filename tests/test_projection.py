@@ -195,6 +195,25 @@ def test_projection_plan_batched_matches_oracle(gpu, oracle, mode, ratio, thd, o
     for pb, (rm, rn) in zip(probs, refs):
         n = pb["keys"].shape[0]
         assert np.array_equal(pb["match"].cpu().numpy()[:n], rm)
+    # back-to-back calls on two different streams: the second
+    # call's table upload and grid / candidate writes must wait for the first
+    # call's kernels on the device (no host synchronisation between them)
+    half = [dict(pb, match=torch.full_like(pb["match"], 7), nmatches=torch.full_like(pb["nmatches"], -5))
+            for pb in probs[::-1]]
+    for pb in probs:
+        pb["match"].fill_(7)
+        pb["nmatches"].fill_(-5)
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    s1.wait_stream(torch.cuda.current_stream())
+    s2.wait_stream(torch.cuda.current_stream())
+    plan.search(mode, probs, ratio, thd, ori, stream=s1)
+    plan.search(mode, half, ratio, thd, ori, stream=s2)
+    torch.cuda.synchronize()
+    for pbs, rs in ((probs, refs), (half, refs[::-1])):
+        for pb, (rm, rn) in zip(pbs, rs):
+            n = pb["keys"].shape[0]
+            assert int(pb["nmatches"].cpu()[0]) == rn
+            assert np.array_equal(pb["match"].cpu().numpy()[:n], rm)
 
 
 def test_projection_plan_argument_checks_cpu():

@@ -1,6 +1,6 @@
 """Drop-in orbm_search_by_bow 2000 x 2000 (the bench latency leg's call),
 repeated: run under rocprofv3 --kernel-trace --memory-copy-trace to split a
-call's ~117 us into copies, kernels and gaps (tools/r05_bowlat.sh)."""
+call's ~117 us into copies, kernels and gaps (tools/probes/r05_bowlat.sh)."""
 import ctypes
 import os
 import sys

@@ -1,6 +1,6 @@
 """Drop-in orbx_extract at 1080p (the bench latency leg's call), repeated:
 run under rocprofv3 --kernel-trace --memory-copy-trace to split a call into
-copies, kernels and gaps (tools/r05_exlat.sh)."""
+copies, kernels and gaps (tools/probes/r05_exlat.sh)."""
 import os
 import sys
 import time
