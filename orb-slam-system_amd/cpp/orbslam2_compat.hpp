@@ -417,4 +417,94 @@ class ORBmatcher {
 
 }  // namespace ORB_SLAM2
 
+// ---------------------------------------------------------------------------
+// SURVEY.md §8(f), the callers either side of the path, with the reference's
+// own shapes:
+//   * DBoW2::BowVector / FeatureVector (Thirdparty/DBoW2/DBoW2/BowVector.h,
+//     FeatureVector.h: std::maps keyed by word / node id) and
+//     ORB_SLAM2::ORBVocabulary (DBoW2::TemplatedVocabulary<FORB::TDescriptor,
+//     FORB>, include/ORBVocabulary.h) with loadFromTextFile / empty /
+//     transform(features, BowVector&, FeatureVector&, levelsup), as
+//     Frame::ComputeBoW (src/Frame.cc:373-382) and System's loader call them;
+//   * Frame::ComputeStereoMatches (src/Frame.cc:446-620) as a template over
+//     the caller's Frame, reading and writing exactly the members the
+//     reference's member function does.
+// ---------------------------------------------------------------------------
+#ifndef ORBX_COMPAT_NO_DBOW2
+namespace DBoW2 {
+typedef unsigned int WordId;
+typedef double WordValue;
+typedef unsigned int NodeId;
+class BowVector : public std::map<WordId, WordValue> {};
+class FeatureVector : public std::map<NodeId, std::vector<unsigned int> > {};
+}  // namespace DBoW2
+#endif
+
+namespace ORB_SLAM2 {
+
+class ORBVocabulary {
+ public:
+  ORBVocabulary() {}
+  ~ORBVocabulary() { orbv_vocab_destroy(v_); }
+  ORBVocabulary(const ORBVocabulary&) = delete;
+  ORBVocabulary& operator=(const ORBVocabulary&) = delete;
+
+  // TemplatedVocabulary::loadFromTextFile (TemplatedVocabulary.h:1126-1259)
+  bool loadFromTextFile(const std::string& filename) {
+    orbv_vocab* v = nullptr;
+    if (orbv_vocab_load_text(filename.c_str(), 0, &v) != ORBX_OK) return false;
+    orbv_vocab_destroy(v_);
+    v_ = v;
+    return true;
+  }
+  bool empty() const {
+    int nwords = 0;
+    return !v_ || orbv_vocab_info(v_, nullptr, nullptr, nullptr, nullptr, nullptr, &nwords) || nwords == 0;
+  }
+  // transform(features, v, fv, levelsup) (TemplatedVocabulary.h:1338-1424):
+  // features = Converter::toDescriptorVector(mDescriptors), one 1 x 32 row each
+  void transform(const std::vector<cv::Mat>& features, DBoW2::BowVector& v, DBoW2::FeatureVector& fv,
+                 int levelsup) const {
+    v.clear();
+    fv.clear();
+    const int n = (int)features.size();
+    if (n == 0) return;
+    std::vector<uint8_t> desc((size_t)n * 32);
+    for (int i = 0; i < n; ++i) memcpy(desc.data() + (size_t)i * 32, features[i].ptr(0), 32);
+    std::vector<uint32_t> word(n), node(n), off(n + 1), feat(n);
+    std::vector<double> value(n);
+    int nb = 0, nf = 0;
+    orbx_throw(orbv_transform(v_, desc.data(), n, levelsup, word.data(), value.data(), &nb, node.data(),
+                              off.data(), feat.data(), &nf),
+               "ORBVocabulary::transform");
+    for (int i = 0; i < nb; ++i) v.insert(v.end(), std::make_pair(word[i], value[i]));
+    for (int j = 0; j < nf; ++j)
+      fv.insert(fv.end(), std::make_pair(node[j], std::vector<unsigned int>(feat.begin() + off[j],
+                                                                              feat.begin() + off[j + 1])));
+  }
+
+ private:
+  orbv_vocab* v_ = nullptr;
+};
+
+// Frame::ComputeStereoMatches (src/Frame.cc:446-620) for a stereo Frame whose
+// two extractors just ran on its images (their pyramids stay on the device
+// for the search).  FR: the reference's Frame -- reads N, mvKeys, mvKeysRight,
+// mDescriptors, mDescriptorsRight, mb, mbf, mpORBextractorLeft / Right;
+// writes mvuRight / mvDepth (-1 where no match survives, :448-449).
+template <class FR>
+void ComputeStereoMatches(FR& F) {
+  F.mvuRight = std::vector<float>(F.N, -1.0f);
+  F.mvDepth = std::vector<float>(F.N, -1.0f);
+  int kept = 0;
+  orbx_throw(orbx_stereo_match(F.mpORBextractorLeft->Orbx(), F.mpORBextractorRight->Orbx(),
+                               reinterpret_cast<const orbx_keypoint*>(F.mvKeys.data()), F.mDescriptors.data,
+                               (int)F.mvKeys.size(), reinterpret_cast<const orbx_keypoint*>(F.mvKeysRight.data()),
+                               F.mDescriptorsRight.data, (int)F.mvKeysRight.size(), F.mb, F.mbf,
+                               F.mvuRight.data(), F.mvDepth.data(), &kept),
+             "ComputeStereoMatches");
+}
+
+}  // namespace ORB_SLAM2
+
 #endif

@@ -1,5 +1,7 @@
-"""The C++ host mirror (cpp/orbx.hpp) compiled against liborbx.so and driven
-like the reference's call sites; outputs checked against the oracle."""
+"""The reference-shaped C++ surface (cpp/orbslam2_compat.hpp: ORB_SLAM2::
+ORBextractor / ORBmatcher / ORBVocabulary, DBoW2 vectors, Frame's stereo
+search) compiled against liborbx.so and driven like the reference's call
+sites; outputs checked against the oracle."""
 import os
 import subprocess
 
@@ -10,49 +12,6 @@ from orbx import synth
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(ROOT, "orb-slam-system_amd")
-
-
-def _build(tmp_path):
-    exe = tmp_path / "adapter_main"
-    subprocess.check_call(["g++", "-O2", "-std=c++17", "-I", os.path.join(PKG, "cpp"),
-                           os.path.join(ROOT, "tests", "cpp", "adapter_main.cpp"), "-o", str(exe),
-                           "-L", PKG, "-lorbx", "-Wl,-rpath," + PKG])
-    return exe
-
-
-def test_cpp_adapter_compiles(tmp_path):
-    assert _build(tmp_path).exists()
-
-
-@pytest.mark.gpu
-def test_cpp_adapter_matches_oracle(gpu, oracle, tmp_path):
-    exe = _build(tmp_path)
-    W, H, nf, L = 752, 480, 1200, 8
-    a, b = synth.frame(W, H, 50, "rects"), synth.frame(W, H, 51, "rects")
-    (tmp_path / "a.raw").write_bytes(a.tobytes())
-    (tmp_path / "b.raw").write_bytes(b.tobytes())
-    out = tmp_path / "out.bin"
-    subprocess.check_call([str(exe), str(tmp_path / "a.raw"), str(tmp_path / "b.raw"), str(W), str(H),
-                           str(nf), str(L), "0", str(out)])
-    raw = out.read_bytes()
-    hdr = np.frombuffer(raw[:24], np.int32)
-    n1, n2, nm, d01, lw, lh = hdr.tolist()
-    off = 24
-    k1 = np.frombuffer(raw[off:off + 28 * n1], oracle.KEYPOINT_DTYPE); off += 28 * n1
-    d1 = np.frombuffer(raw[off:off + 32 * n1], np.uint8).reshape(n1, 32); off += 32 * n1
-    m12 = np.frombuffer(raw[off:off + 4 * n1], np.int32); off += 4 * n1
-    lvl = np.frombuffer(raw[off:off + lw * lh], np.uint8).reshape(lh, lw)
-    e = oracle.Extractor(nf, 1.2, L, 20, 7)
-    rk1, rd1 = e.extract(a)
-    assert np.array_equal(lvl, e.level(L - 1))
-    rk2, rd2 = e.extract(b)
-    assert np.array_equal(k1.view(np.uint8), rk1.view(np.uint8)) and np.array_equal(d1, rd1)
-    assert n2 == len(rk2)
-    one = lambda k, d: dict(desc=d, angle=k["angle"], valid=None, node_id=np.array([7], np.uint32),
-                            off=np.array([0, len(k)], np.uint32), feat=np.arange(len(k), dtype=np.uint32))
-    rm, rnm = oracle.search_by_bow(one(rk1, rd1), one(rk2, rd2), 0.75, True)
-    assert nm == rnm and np.array_equal(m12, rm)
-    assert d01 == oracle.descriptor_distance(rd1[0], rd2[0])
 
 
 def _build_stereo(tmp_path):
@@ -140,7 +99,9 @@ def test_cpp_vocab_adapter_matches_oracle(gpu, oracle, tmp_path):
     kf1 = dict(desc=d1, angle=k1["angle"], valid=None, **rfv1)
     kf2 = dict(desc=d2, angle=k2["angle"], valid=None, **rfv2)
     rm, rnm = oracle.search_by_bow(kf1, kf2, 0.75, True)
-    assert nm == rnm and np.array_equal(m12, rm)
+    # vpMatches12 as pointers: matched entries name kf2's MapPoint, the rest
+    # (never written, or reset by the rotation check) are null
+    assert nm == rnm and np.array_equal(m12, np.where(rm >= 0, rm, -1))
 
 
 def _build_compat(tmp_path):
