@@ -25,12 +25,6 @@ __global__ void k_fast_strips(const uint8_t*, size_t, size_t, const uint8_t*, si
 __global__ void k_fast_strips_p288(const uint8_t*, size_t, size_t, const uint8_t*, size_t,
                               const LevelArgs, const CellInfo*, const StripInfo*, uint32_t*,
                               size_t, uint32_t*, int, int, int, int, int, int, int, int*, int, int);
-__global__ void k_fast_pf(const uint8_t*, size_t, size_t, const uint8_t*, size_t,
-                          const LevelArgs, const CellInfo*, const StripInfo*, uint32_t*,
-                          size_t, uint32_t*, int, int, int, int, int, int, int, int*, int, int, int, int);
-__global__ void k_fast_pf_p288(const uint8_t*, size_t, size_t, const uint8_t*, size_t,
-                               const LevelArgs, const CellInfo*, const StripInfo*, uint32_t*,
-                               size_t, uint32_t*, int, int, int, int, int, int, int, int*, int, int, int, int);
 __global__ void k_quadtree(const LevelInfo*, const CellInfo*, const uint32_t*, size_t,
                            const uint32_t*, int, uint32_t*, int32_t*, size_t, uint32_t*, size_t,
                            int*, int, int, int, int*, uint32_t*);
@@ -194,7 +188,6 @@ extern "C" int orbx_plan_create(const orbx_params* prm, int width, int height, i
   if (const char* e = getenv("ORBX_DEBUG_LDSPAD")) sscanf(e, "%d,%d,%d", &p->pad_pyr, &p->pad_fast, &p->pad_brief);
   if (const char* e = getenv("ORBX_CHUNK")) p->chunk = atoi(e);
   if (const char* e = getenv("ORBX_DEBUG_OVERLAP")) p->overlap = atoi(e); /* FAST level 0 beside the pyramid */
-  if (const char* e = getenv("ORBX_DEBUG_FSPF")) p->fs_pf = atoi(e); /* 0: k_fast_strips grid (A/B) */
 #endif
   p->fs_ccap = FS_CCAP;
   /* testing only: a smaller FAST corner list, so the overflow path runs
@@ -211,10 +204,6 @@ extern "C" int orbx_plan_create(const orbx_params* prm, int width, int height, i
   p->device = device;
   p->max_batch = max_batch;
   ORBX_TRY(hipSetDevice(device));
-  if (hipDeviceGetAttribute(&p->ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || p->ncu < 1) {
-    plan_free(p);
-    return ORBX_ERR_HIP;
-  }
   // quadtree LDS: cell offsets, then (reusing them) 11 int arrays of qt_smax
   p->qt_lds = sizeof(int) * std::max((size_t)P.qt_max_cells + 1, 11 * (size_t)P.qt_smax);
   if (p->qt_lds > 150 * 1024) { plan_free(p); return ORBX_ERR_UNSUPPORTED; }
@@ -222,8 +211,6 @@ extern "C" int orbx_plan_create(const orbx_params* prm, int width, int height, i
       set_max_dynamic_lds((const void*)k_quadtree_j6, device) ||
       set_max_dynamic_lds((const void*)k_fast_strips, device) ||
       set_max_dynamic_lds((const void*)k_fast_strips_p288, device) ||
-      set_max_dynamic_lds((const void*)k_fast_pf, device) ||
-      set_max_dynamic_lds((const void*)k_fast_pf_p288, device) ||
       set_max_dynamic_lds((const void*)k_pyramid, device)) { plan_free(p); return ORBX_ERR_HIP; }
   if (p->overlap && (hipStreamCreateWithFlags(&p->s_aux, hipStreamNonBlocking) != hipSuccess ||
                      hipEventCreateWithFlags(&p->ev_aux0, hipEventDisableTiming) != hipSuccess ||
@@ -247,6 +234,13 @@ extern "C" int orbx_plan_create(const orbx_params* prm, int width, int height, i
     p->largs.pitch[l] = u.pitch;
   }
   p->largs.key_xs = P.levels[0].key_xs;
+  // each FAST strip carries its level's pitch and pyramid offset: the kernel
+  // reads them with the strip record instead of indexing the by-value level
+  // tables (two dependent scalar loads per workgroup)
+  for (StripInfo& si : p->P.strips) {
+    si.pitch = si.level == 0 ? 0 : p->largs.pitch[si.level];
+    si.off = si.level == 0 ? 0 : p->largs.pyr_off[si.level];
+  }
   // plans with a pyramid run its waves and FAST's at a raised issue
   // priority (ORBX_EX_PRIO): measured in the pipelined step, c4 +1.4-2.3 %,
   // c1 +0.5-0.7 %, c5 neutral; a single level (c2) lost 2.3 %, the matcher
@@ -367,21 +361,6 @@ extern "C" int orbx_plan_create(const orbx_params* prm, int width, int height, i
       G.lds += FS_LDS_PAD;
 #endif
       if (G.lds > 150 * 1024) { plan_free(p); return ORBX_ERR_UNSUPPORTED; }
-      /* persistent form: every strip's tile within FS_PF_DW dwords per thread
-       * in 16-B chunks from the 16-B aligned column at or left of st.x */
-      G.pf = p->fs_pf != 0;
-      for (int k = G.begin; k < G.end && G.pf; ++k) {
-        const StripInfo& si = PM.strips[k];
-        if ((size_t)si.h * (size_t)((si.w + 15 + 15) / 16) > (size_t)FS_NT * (FS_PF_DW / 4)) G.pf = false;
-      }
-      if (G.pf) {
-        int nb = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)(p->fs_tpitch == 288 ? k_fast_pf_p288 : k_fast_pf),
-                                                         FS_NT, G.lds + p->pad_fast) != hipSuccess || nb < 1)
-          G.pf = false;
-        else
-          G.pf_wgs = std::min(nb, 8);
-      }
     }
   }
   hipStream_t us = p->stream;
@@ -465,21 +444,6 @@ static int extract_pass(orbx_plan* p, const uint8_t* frames, int n, size_t fstri
   auto fast_launch = [&](int g, int strip0, int strip1, hipStream_t st) {
     if (strip1 <= strip0) return;
     const orbx_plan::FsGroup& G = p->fs_grp[g];
-    // persistent form when level 0's rows (the caller's frames) are 16-B
-    // aligned, as the pyramid's always are
-    const bool al16 = ((reinterpret_cast<uintptr_t>(frames) | (uintptr_t)fstride | (uintptr_t)rstride) & 15) == 0;
-    if (G.pf && al16) {
-      // persistent: G resident workgroups walk the (strip, frame) units
-      const int nstrips = strip1 - strip0, nunits = nstrips * n;
-      int grid = std::min(nunits, p->ncu * G.pf_wgs);
-      if (grid > 8) grid &= ~7;  // a multiple of 8: unit u keeps the plain grid's XCD
-      hipLaunchKernelGGL(p->fs_tpitch == 288 ? k_fast_pf_p288 : k_fast_pf, dim3((unsigned)grid), dim3(FS_NT),
-                         G.lds + p->pad_fast, st, frames, fstride, rstride, d_pyr, p->pyr_stride, p->largs,
-                         p->d_cells, p->d_strips, d_slots, p->slot_stride, d_ccount, P.ncells, P.ini_th,
-                         P.min_th, p->fs_tpitch, G.tmaxh, G.mcells, G.ccap, p->d_err + ORBX_ERRW_FAST_OVF,
-                         strip0, p->dbg, nstrips, nunits);
-      return;
-    }
     hipLaunchKernelGGL(p->fs_tpitch == 288 ? k_fast_strips_p288 : k_fast_strips, dim3((unsigned)(strip1 - strip0), n), dim3(FS_NT), G.lds + p->pad_fast, st,
                        frames, fstride, rstride, d_pyr, p->pyr_stride, p->largs, p->d_cells,
                        p->d_strips, d_slots, p->slot_stride, d_ccount, P.ncells, P.ini_th,

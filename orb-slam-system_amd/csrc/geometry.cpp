@@ -528,6 +528,8 @@ int plan_geometry(const orbx_params& p, int width, int height, Plan& P) {
         st.level = l; st.x = a.x; st.y = a.y; st.w = b.x + b.w - a.x; st.h = a.h;
         st.cell_begin = row_first + j0; st.ncells = j1 - j0; st.wcell = wCell;
         st.colwalk = lv.w >= cw_minw;
+        st.pitch = 0;  /* set by the plan (api_extract.hip) */
+        st.off = 0;
         P.strips.push_back(st);
         P.strip_max_w = std::max(P.strip_max_w, st.w);
         P.strip_max_h = std::max(P.strip_max_h, st.h);

@@ -502,7 +502,7 @@ __device__ __forceinline__ int wave_excl_scan(int n, int lane, int* total) {
 // ---------------------------------------------------------------------------
 // TP: the tile pitch as a compile-time constant (every LDS offset of stage A
 // an immediate of one address register), 0 = runtime pitch
-template <int TP, bool PF = false>
+template <int TP>
 __device__ __forceinline__ void fs_strip_body(
     uint8_t* __restrict__ tile, uint8_t* __restrict__ amap_mem, int* __restrict__ cnt,
     unsigned long long* __restrict__ mask, unsigned long long* __restrict__ mask2,
@@ -536,8 +536,7 @@ __device__ __forceinline__ void fs_strip_body(
   // nothing of the staging is in flight any more: an explicit vmcnt(0) here
   // lets the waitcnt pass drop the (run-time no-op) vmcnt waits it otherwise
   // re-inserts every stage-A iteration for registers the staging loads used
-  // (PF, the persistent kernel: the next unit's tile loads stay in flight)
-  if (!PF) __builtin_amdgcn_s_waitcnt(0x0F70);
+  __builtin_amdgcn_s_waitcnt(0x0F70);
   const int g0 = c0 >> 2, g1 = (c1 + 3) >> 2, ng = g1 - g0;
   const int ntask = ng * bh;
   uint16_t* L1 = wlist1[wave];
@@ -775,21 +774,44 @@ __device__ __forceinline__ void fs_strip_body(
       const uint32_t tl = lact ? tt : 0xFF00FF00u;
       if (rb < re) {  // wave-uniform
         uint32_t V[FS_CW_RMAX + 6];
-        const uint8_t* src = gsrc + 4 * gl;
+        // the wave's rows through a buffer resource over [row rb, the tile's
+        // last row]: one scalar offset add per row, no 64-bit address math,
+        // and rows past the tile read 0 from the range check instead of a
+        // clamped address (those rows are never stored or tested; round 6)
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<uint8_t*>(gsrc) + __umul24((uint32_t)rb, (uint32_t)gpitch), 0, (st.h - rb) * gpitch, 0x00020000);
+        const int voff = 4 * gl;
 #pragma unroll
-        for (int k = 0; k < FS_CW_RMAX + 6; ++k)  // unconditional: rows past the tile repeat its last
-          V[k] = *reinterpret_cast<const uint32_t*>(src + __umul24((uint32_t)min(rb + k, st.h - 1), (uint32_t)gpitch));
+        for (int k = 0; k < FS_CW_RMAX + 6; ++k) V[k] = __builtin_amdgcn_raw_buffer_load_b32(rs, voff, k * gpitch, 0);
         uint8_t* trow = tile + __mul24(rb, tpitch) + 4 * gl;
         const int nr = re - rb;
+#ifdef FS_CW_STORE_FIRST  // profiling variant: every row to the tile before the first test (rounds 3-5)
+        if (true) {
+#else
+        if (dbg == 5) {  // profiling only: loads and tile stores
+#endif
 #pragma unroll
-        for (int k = 0; k < FS_CW_RMAX + 6; ++k)
-          if (k < nr + 6) *reinterpret_cast<uint32_t*>(trow + k * tpitch) = V[k];
-        if (dbg == 5) return;  // profiling only: loads and tile stores
+          for (int k = 0; k < FS_CW_RMAX + 6; ++k)
+            if (k < nr + 6) *reinterpret_cast<uint32_t*>(trow + k * tpitch) = V[k];
+          if (dbg == 5) return;
+        }
+        // rows 0..5 to the tile now, row k + 6 just before band row k's test
+        // (round 6): the rows arrive in load order and each store waits only
+        // for its own row, so the first tests run while later rows are still
+        // in flight (stages B / C read rows up to r + 3 of an entry at row
+        // r <= k, already stored)
+#ifndef FS_CW_STORE_FIRST
+#pragma unroll
+        for (int k = 0; k < 6; ++k) *reinterpret_cast<uint32_t*>(trow + k * tpitch) = V[k];
+#endif
         uint8_t* zrow = amap + __mul24(3 + rb, tpitch) + 4 * gl;
         uint32_t er = ((uint32_t)(3 + rb) << 9) | (uint32_t)(4 * gl);
 #pragma unroll
         for (int k = 0; k < FS_CW_RMAX; ++k) {
           if (k < nr) {  // wave-uniform
+#ifndef FS_CW_STORE_FIRST
+            *reinterpret_cast<uint32_t*>(trow + (k + 6) * tpitch) = V[k + 6];
+#endif
             GroupWords q;
             q.up = V[k];
             q.w1 = V[k + 3];
@@ -1036,14 +1058,13 @@ __device__ __forceinline__ void fs_kernel(
   const int sx = blockIdx.x + strip0, f = blockIdx.y;
 #endif
   const StripInfo st = strips[sx];
-  const int pitch = st.level == 0 ? (int)rstride : LA.pitch[st.level];
+  const int pitch = st.pitch ? st.pitch : (int)rstride;
 #ifdef FS_PROBE_SAMESRC  // profiling only: every frame's strips read frame 0 (cache-resident source)
   const int fsrc = 0;
 #else
   const int fsrc = f;
 #endif
-  const uint8_t* base = st.level == 0 ? frames + (size_t)fsrc * fstride
-                                      : pyr + (size_t)fsrc * pstride + LA.pyr_off[st.level];
+  const uint8_t* base = st.level == 0 ? frames + (size_t)fsrc * fstride : pyr + (size_t)fsrc * pstride + st.off;
   const int slot_pref = tid < st.ncells ? cells[st.cell_begin + tid].slot_off : 0;  // in flight
   const uintptr_t alb = reinterpret_cast<uintptr_t>(base) | (uintptr_t)pitch;
   const bool aligned = (alb & 3) == 0;
@@ -1069,9 +1090,9 @@ __device__ __forceinline__ void fs_kernel(
     else if (aligned) stage_region<uint32_t, 12, FS_NT>(tile, tpitch, s0, pitch, st.h, (tw + 3) >> 2, tid);
     else stage_rows_u32<12, FS_NT>(tile, tpitch, s0, pitch, st.h, tw, tid);
   }
-  fs_strip_body<TP>(tile, amap_mem, cnt, mask, mask2, wlist1, wlist2, clist, cslot, ncorner, st, f,
-                    lead, xal, slot_pref, slots, slot_stride, ccount, ncells, ini_th, min_th, tpitch,
-                    ccap, ovf, dbg, s0, pitch, cw, LA.key_xs);
+  fs_strip_body<TP>(tile, amap_mem, cnt, mask, mask2, wlist1, wlist2, clist, cslot, ncorner, st, f, lead,
+                             xal, slot_pref, slots, slot_stride, ccount, ncells, ini_th, min_th, tpitch, ccap, ovf,
+                             dbg, s0, pitch, cw, LA.key_xs);
 }
 
 #define FS_KERNEL_ARGS                                                                              \
@@ -1092,165 +1113,6 @@ __global__ __launch_bounds__(FS_NT) FS_ATTR void k_fast_strips(FS_KERNEL_ARGS) {
 // the plan's tile pitch is 288 for every strip width in 224..264 (all the
 // bench workloads): immediates instead of per-iteration address adds
 __global__ __launch_bounds__(FS_NT) FS_ATTR void k_fast_strips_p288(FS_KERNEL_ARGS) { fs_kernel<288>(FS_KERNEL_PASS); }
-
-// ---------------------------------------------------------------------------
-// k_fast_pf: the same strip body in a persistent loop whose next unit's tile
-// is loaded into registers while the current unit is processed (round 6).
-// Per-phase SQ counters of k_fast_strips (tools/phase_sq.sh, c4) put a third
-// of a wave's 18.4 K cycles before its first pixel test: the tile's row loads
-// (6.0 K cycles, 49 % of them parked on vmcnt).  A grid of G resident
-// workgroups walks the (strip, frame) units u = blockIdx.x + i * G; unit
-// u + G's tile (<= FS_PF_DW dwords per thread) is requested right after unit
-// u's tile went to LDS and lands during unit u's passes, so only the first
-// unit of a workgroup waits for memory.  Every unit runs fs_strip_body's
-// block-staged form (stage A from the LDS tile; no column walk, whose rows
-// live in the registers the prefetch needs).  Units keep the plain grid's
-// XCD of unit u (G is a multiple of 8).
-// ---------------------------------------------------------------------------
-// where a unit's tile comes from: recomputed from (strip, frame) wherever it
-// is needed instead of carried across the strip body in scalar registers.
-// The launcher takes this kernel only when every level's rows are 16-B
-// aligned (the caller's frames and row stride; the pyramid buffer always is),
-// so the tile moves in 16-B chunks: one load form, nothing for the compiler
-// to hoist across a mode test (with a dword form beside it, the chunk loads
-// waited for hoisted dword loads)
-struct FsSrc {
-  int nper, total, xal;
-  uint32_t pitch;
-  const uint8_t* s0;
-};
-__device__ __forceinline__ FsSrc fs_pf_src(const StripInfo& st, int f, const uint8_t* __restrict__ frames,
-                                           size_t fstride, size_t rstride, const uint8_t* __restrict__ pyr,
-                                           size_t pstride, const LevelArgs& LA) {
-  FsSrc g;
-  const int pitch = st.level == 0 ? (int)rstride : LA.pitch[st.level];
-  const uint8_t* base = st.level == 0 ? frames + (size_t)f * fstride : pyr + (size_t)f * pstride + LA.pyr_off[st.level];
-  g.xal = st.x & ~15;
-  g.nper = (st.x - g.xal + st.w + 15) >> 4;
-  g.total = st.h * g.nper;
-  g.pitch = (uint32_t)pitch;
-  g.s0 = base + (size_t)st.y * pitch + g.xal;
-  return g;
-}
-
-// issue the tile loads of unit (sx, f) into R (chunk e = tid + FS_NT k:
-// (row, chunk) stepped without divisions; loads past the tile repeat its
-// last row: unconditional, so nothing waits for them here) and its cells'
-// slot offsets
-__device__ __forceinline__ void fs_pf_fetch(uint32_t (&R)[FS_PF_DW], int& slot_pref, const uint8_t* __restrict__ frames,
-                                            size_t fstride, size_t rstride, const uint8_t* __restrict__ pyr,
-                                            size_t pstride, const LevelArgs& LA, const CellInfo* __restrict__ cells,
-                                            const StripInfo* __restrict__ strips, int sx, int f) {
-  const int tid = threadIdx.x;
-  const StripInfo st = strips[sx];
-  const FsSrc g = fs_pf_src(st, f, frames, fstride, rstride, pyr, pstride, LA);
-  const int nper = g.nper, dr = FS_NT / nper, dc = FS_NT - dr * nper;
-  int r = tid / nper, c = tid - r * nper;
-#pragma unroll
-  for (int k = 0; k < FS_PF_DW / 4; ++k) {
-    const v4u v = *reinterpret_cast<const v4u*>(g.s0 + (__umul24((uint32_t)min(r, st.h - 1), g.pitch) + 16u * (uint32_t)c));
-    R[4 * k] = v.x;
-    R[4 * k + 1] = v.y;
-    R[4 * k + 2] = v.z;
-    R[4 * k + 3] = v.w;
-    r += dr;
-    c += dc;
-    if (c >= nper) { c -= nper; ++r; }
-  }
-  // last, at a clamped index: a load under `tid < ncells` would be waited for
-  // at the branch's join (lanes past ncells never use the value)
-  slot_pref = cells[st.cell_begin + min(tid, max(st.ncells - 1, 0))].slot_off;
-}
-
-__device__ __forceinline__ void fs_pf_commit(const uint32_t (&R)[FS_PF_DW], const FsSrc& g, uint8_t* __restrict__ tile,
-                                             int tpitch) {
-  const int tid = threadIdx.x;
-  const int nper = g.nper, dr = FS_NT / nper, dc = FS_NT - dr * nper;
-  int r = tid / nper, c = tid - r * nper;
-#pragma unroll
-  for (int k = 0; k < FS_PF_DW / 4; ++k) {
-    if (tid + FS_NT * k < g.total) {
-      v4u v;
-      v.x = R[4 * k];
-      v.y = R[4 * k + 1];
-      v.z = R[4 * k + 2];
-      v.w = R[4 * k + 3];
-      reinterpret_cast<v4u*>(tile + __mul24(r, tpitch))[c] = v;
-    }
-    r += dr;
-    c += dc;
-    if (c >= nper) { c -= nper; ++r; }
-  }
-}
-
-template <int TP>
-__device__ __forceinline__ void fs_pf_kernel(
-    const uint8_t* __restrict__ frames, size_t fstride, size_t rstride,
-    const uint8_t* __restrict__ pyr, size_t pstride, const LevelArgs& LA,
-    const CellInfo* __restrict__ cells, const StripInfo* __restrict__ strips,
-    uint32_t* __restrict__ slots, size_t slot_stride, uint32_t* __restrict__ ccount, int ncells,
-    int ini_th, int min_th, int tpitch_rt, int tmax_h, int mcells, int ccap, int* __restrict__ ovf,
-    int strip0, int dbg, int nstrips, int nunits) {
-  const int tpitch = TP ? TP : tpitch_rt;
-  extern __shared__ __align__(16) uint32_t sm[];  // layout as fs_kernel
-#if ORBX_EX_PRIO
-  if (LA.prio) __builtin_amdgcn_s_setprio(ORBX_EX_PRIO);
-#endif
-  uint8_t* tile = reinterpret_cast<uint8_t*>(sm);
-  uint8_t* amap_mem = tile + tpitch * tmax_h;
-  int* cnt = reinterpret_cast<int*>(amap_mem + tpitch * (tmax_h - 6));
-  int* cslot = cnt + ((mcells + 3) & ~3);
-  uint16_t* clist = reinterpret_cast<uint16_t*>(cslot + ((mcells + 3) & ~3));
-  const bool masks_in_tile = 16 * mcells * (tmax_h - 6) <= tpitch * tmax_h;
-  unsigned long long* mask = masks_in_tile ? reinterpret_cast<unsigned long long*>(tile)
-                                           : reinterpret_cast<unsigned long long*>(clist + ((ccap + 3) & ~3));
-  unsigned long long* mask2 = mask + mcells * (tmax_h - 6);
-  __shared__ uint16_t wlist1[FS_NW][FS_L1CAP];
-  __shared__ uint16_t wlist2[FS_NW][FS_L2CAP];
-  __shared__ int ncorner;
-  const int G = (int)gridDim.x;
-  int u = (int)blockIdx.x;
-  if (u >= nunits) return;
-  // units u, u + G, ...: (strip s, frame f) stepped without divisions
-  int s = u % nstrips, f = u / nstrips;
-  const int gs = G % nstrips, gf = G / nstrips;
-  uint32_t R[FS_PF_DW];
-  int slot_cur, slot_next = 0;
-  fs_pf_fetch(R, slot_cur, frames, fstride, rstride, pyr, pstride, LA, cells, strips, strip0 + s, f);
-  for (;;) {
-    __syncthreads();  // the previous unit's passes are done with the tile, map and lists
-    const StripInfo st = strips[strip0 + s];
-    const int fc = f;
-    {
-      const FsSrc g = fs_pf_src(st, fc, frames, fstride, rstride, pyr, pstride, LA);
-      fs_pf_commit(R, g, tile, tpitch);
-    }
-    const int xal = st.x & ~15;
-    u += G;
-    s += gs;
-    f += gf;
-    if (s >= nstrips) {
-      s -= nstrips;
-      ++f;
-    }
-    const bool more = u < nunits;  // workgroup-uniform
-    if (more) fs_pf_fetch(R, slot_next, frames, fstride, rstride, pyr, pstride, LA, cells, strips, strip0 + s, f);
-    fs_strip_body<TP, true>(tile, amap_mem, cnt, mask, mask2, wlist1, wlist2, clist, cslot, ncorner, st, fc,
-                            st.x - xal, xal, slot_cur, slots, slot_stride, ccount, ncells, ini_th, min_th, tpitch, ccap,
-                            ovf, dbg, nullptr, 0, false, LA.key_xs);
-    if (!more) break;
-    slot_cur = slot_next;
-  }
-}
-
-#ifndef FS_PF_WPE
-#define FS_PF_WPE 6 /* 6 workgroups per CU, as LDS allows: <= 80 VGPRs */
-#endif
-#define FS_PF_ATTR __attribute__((amdgpu_waves_per_eu(FS_PF_WPE)))
-#define FS_PF_ARGS FS_KERNEL_ARGS, int nstrips, int nunits
-#define FS_PF_PASS FS_KERNEL_PASS, nstrips, nunits
-__global__ __launch_bounds__(FS_NT) FS_PF_ATTR void k_fast_pf(FS_PF_ARGS) { fs_pf_kernel<0>(FS_PF_PASS); }
-__global__ __launch_bounds__(FS_NT) FS_PF_ATTR void k_fast_pf_p288(FS_PF_ARGS) { fs_pf_kernel<288>(FS_PF_PASS); }
 
 // ---------------------------------------------------------------------------
 // Block-wide exclusive scan of an LDS int array (256 threads), returns total.
@@ -2466,3 +2328,4 @@ __global__ __launch_bounds__(256) void k_selftest_sincos_range(uint32_t first, i
 }
 
 }  // namespace orbx
+

@@ -78,6 +78,8 @@ struct StripInfo {
   int ncells;
   int wcell;
   int colwalk;    /* planner's choice of k_fast_strips' column walk (when it applies) */
+  int pitch;      /* row pitch of the level's storage; 0 = level 0 (the call's row stride) */
+  long long off;  /* byte offset of the level in the per-frame pyramid buffer (level > 0) */
 };
 
 /* per-level storage of the pyramid, passed by value to kernels that only
@@ -107,9 +109,6 @@ struct StereoArgs {
   float scale[ORBX_MAX_LEVELS], inv_scale[ORBX_MAX_LEVELS];
   float mb, mbf;
 };
-#ifndef FS_PF_DW
-#define FS_PF_DW 12 /* k_fast_pf: prefetched tile dwords per thread (tiles up to FS_NT * 48 B; 16 spills at 80 VGPRs) */
-#endif
 #ifndef FS_NT
 #define FS_NT 256 /* threads per k_fast_strips workgroup (one strip) */
 #endif

@@ -23,11 +23,6 @@ struct orbx_plan {
   struct FsGroup {
     int begin = 0, end = 0, tmaxh = 7, mcells = 1, ccap = 0;
     size_t lds = 0;
-    /* k_fast_pf (persistent, next tile prefetched in registers): every tile
-     * of the group fits its register budget; pf_wgs = resident workgroups
-     * per CU (the grid is CUs x pf_wgs, rounded to a multiple of 8) */
-    bool pf = false;
-    int pf_wgs = 0;
   };
   FsGroup fs_grp[2];
   int fs_ngrp = 1;
@@ -58,8 +53,6 @@ struct orbx_plan {
   int chunk = 0;  /* frames per extraction pass (0 = the whole batch in one pass) */
   hipEvent_t ev_after_pyr = nullptr; /* recorded after the pyramid launch when set (orbx_extract) */
   int overlap = 0; /* FAST on level 0 beside the pyramid on s_aux */
-  int fs_pf = 0;   /* k_fast_pf where the tiles fit (ORBX_DEBUG_FSPF=0: the one-strip-per-workgroup grid) */
-  int ncu = 0;     /* compute units of the device (k_fast_pf's grid) */
   hipStream_t s_aux = nullptr;
   hipEvent_t ev_aux0 = nullptr, ev_aux1 = nullptr;
   int options = 0; /* ORBX_PLAN_* (include/orbx.h) */
