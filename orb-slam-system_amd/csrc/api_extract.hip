@@ -3,6 +3,7 @@
 // timing and synthetic frames.
 #include <hip/hip_runtime.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -31,6 +32,9 @@ __global__ void k_quadtree(const LevelInfo*, const CellInfo*, const uint32_t*, s
 __global__ void k_quadtree_j6(const LevelInfo*, const CellInfo*, const uint32_t*, size_t,
                               const uint32_t*, int, uint32_t*, int32_t*, size_t, uint32_t*, size_t,
                               int*, int, int, int, int*, uint32_t*);
+__global__ void k_quadtree_wide(const LevelInfo*, const CellInfo*, const uint32_t*, size_t,
+                                const uint32_t*, int, uint32_t*, int32_t*, size_t, uint32_t*, size_t,
+                                int*, int, int, int, int*, uint32_t*);
 __global__ void k_orient_brief(const uint8_t*, size_t, size_t, const uint8_t*, size_t,
                                const BriefArgs, const uint32_t*, size_t, const int*,
                                orbx_keypoint*, uint8_t*, int*, const uint32_t*, int);
@@ -204,11 +208,14 @@ extern "C" int orbx_plan_create(const orbx_params* prm, int width, int height, i
   p->device = device;
   p->max_batch = max_batch;
   ORBX_TRY(hipSetDevice(device));
-  // quadtree LDS: cell offsets, then (reusing them) 11 int arrays of qt_smax
-  p->qt_lds = sizeof(int) * std::max((size_t)P.qt_max_cells + 1, 11 * (size_t)P.qt_smax);
+  // quadtree LDS: cell offsets + slot offsets, then (reusing them) 11 int arrays of qt_smax
+  p->qt_lds = sizeof(int) * std::max(2 * (size_t)P.qt_max_cells + 1, 11 * (size_t)P.qt_smax);
   if (p->qt_lds > 150 * 1024) { plan_free(p); return ORBX_ERR_UNSUPPORTED; }
+  // the wide single-frame form adds a second child array (4 smax ints)
+  p->qt_lds_wide = sizeof(int) * std::max(2 * (size_t)P.qt_max_cells + 1, 15 * (size_t)P.qt_smax);
   if (set_max_dynamic_lds((const void*)k_quadtree, device) ||
       set_max_dynamic_lds((const void*)k_quadtree_j6, device) ||
+      set_max_dynamic_lds((const void*)k_quadtree_wide, device) ||
       set_max_dynamic_lds((const void*)k_fast_strips, device) ||
       set_max_dynamic_lds((const void*)k_fast_strips_p288, device) ||
       set_max_dynamic_lds((const void*)k_pyramid, device)) { plan_free(p); return ORBX_ERR_HIP; }
@@ -498,9 +505,16 @@ static int extract_pass(orbx_plan* p, const uint8_t* frames, int n, size_t fstri
   }
   // K3 DistributeOctTree
   p->timer.begin(ORBX_STAGE_QUADTREE, s);
-  // keys per thread in registers: 8 for 1080p-class level 0, else 6 (qt_body)
-  hipLaunchKernelGGL(P.levels[0].w * P.levels[0].h >= (1 << 20) ? k_quadtree : k_quadtree_j6, dim3(n, L),
-                     dim3(256), p->qt_lds, s, p->d_lv, p->d_cells,
+  // keys per thread in registers: 8 for 1080p-class level 0, else 6
+  // (qt_body); a call of a few frames (the drop-in's one frame per
+  // Frame::ExtractORB) leaves the chip mostly idle and the level-0 workgroup
+  // sets the latency: 1024-thread workgroups there
+  bool qt_wide = (long long)n * L <= 64 && p->qt_lds_wide <= 150 * 1024;
+#ifdef ORBX_PROFILING
+  if (const char* e = getenv("ORBX_DEBUG_QT_WIDE")) qt_wide = atoi(e) != 0 && p->qt_lds_wide <= 150 * 1024;  // A/B (profiling only)
+#endif
+  hipLaunchKernelGGL(qt_wide ? k_quadtree_wide : P.levels[0].w * P.levels[0].h >= (1 << 20) ? k_quadtree : k_quadtree_j6,
+                     dim3(n, L), dim3(qt_wide ? 1024 : 256), qt_wide ? p->qt_lds_wide : p->qt_lds, s, p->d_lv, p->d_cells,
                      d_slots, p->slot_stride, d_ccount, P.ncells, d_qkeys, d_qnode,
                      p->qk_stride, d_qout, p->qout_stride, d_lcount, L, P.qt_smax,
                      P.qt_max_cells, p->d_err, p->d_qperm + f0 * p->qout_stride);

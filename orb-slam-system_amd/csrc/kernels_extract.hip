@@ -1115,11 +1115,12 @@ __global__ __launch_bounds__(FS_NT) FS_ATTR void k_fast_strips(FS_KERNEL_ARGS) {
 __global__ __launch_bounds__(FS_NT) FS_ATTR void k_fast_strips_p288(FS_KERNEL_ARGS) { fs_kernel<288>(FS_KERNEL_PASS); }
 
 // ---------------------------------------------------------------------------
-// Block-wide exclusive scan of an LDS int array (256 threads), returns total.
+// Block-wide exclusive scan of an LDS int array (NT threads), returns total.
 // ---------------------------------------------------------------------------
+template <int NT>
 __device__ int block_scan_excl(int* a, int n, int* wtmp) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int chunk = (n + 255) / 256;
+  const int chunk = (n + NT - 1) / NT;
   const int b = tid * chunk, e = min(n, b + chunk);
   int s = 0;
   for (int i = b; i < e; ++i) s += a[i];
@@ -1128,7 +1129,9 @@ __device__ int block_scan_excl(int* a, int n, int* wtmp) {
   __syncthreads();
   int woff = 0;
   for (int w = 0; w < wave; ++w) woff += wtmp[w];
-  const int total = wtmp[0] + wtmp[1] + wtmp[2] + wtmp[3];
+  int total = 0;
+#pragma unroll
+  for (int w = 0; w < NT / 64; ++w) total += wtmp[w];
   int run = woff + incl - s;
   for (int i = b; i < e; ++i) {
     const int v = a[i];
@@ -1184,14 +1187,14 @@ __device__ __forceinline__ int upper_bound_i(const int* a, int n, int v) {
 #define QT_KERNEL_PASS \
   lv, cells, slots, slot_stride, ccount, ncells_total, qkeys, qnode, qk_stride, qout, qout_stride, lcount, nlevels, smax, maxcells, err, qperm
 
-// QJ: keys per thread held in registers (256 QJ per level; more spill to the
+// QJ: keys per thread held in registers (NT QJ per level; more spill to the
 // global keys/node arrays).  Both instantiations are built for 8 waves per
 // SIMD (<= 64 VGPRs, 8 workgroups per CU): the kernel is latency-bound, so
 // occupancy beats a larger register file of keys.  Measured (same-run A/B,
 // ms per step): 12 keys at 95 VGPRs (5 waves) 0.089 / 0.173 / 0.117 (c4 /
 // c1 / c5); 8 keys at 8 waves 0.089 / 0.123 / 0.078; 6 keys at 8 waves
 // 0.092 / 0.115 / 0.075 -- 8 for 1080p-class levels, 6 below.
-template <int QJ>
+template <int QJ, int NT>
 __device__ __forceinline__ void qt_body(QT_KERNEL_ARGS) {
   extern __shared__ __align__(16) int smem[];
   // grid (frames, levels): dispatch is round-robin over the 8 XCDs in
@@ -1205,8 +1208,9 @@ __device__ __forceinline__ void qt_body(QT_KERNEL_ARGS) {
   const LevelInfo L = lv[l];
   const LevelInfo U = lv[L.unique];
   // cell offsets live only through the key gather: the node arrays reuse
-  // their LDS (max(maxcells + 1, 11 smax) ints: one round of workgroups)
+  // their LDS (max(2 maxcells + 1, 11 smax) ints: one round of workgroups)
   int* cell_off = smem;                       // maxcells + 1
+  int* cell_slot = smem + maxcells + 1;        // maxcells (slot_off of each cell)
   int* rx = smem;                             // smax  (rx / ry / cnt and nrx / nry / ncnt
   int* ry = rx + smax;                        // smax   swap roles every pass)
   int* cnt = ry + smax;                       // smax
@@ -1215,8 +1219,12 @@ __device__ __forceinline__ void qt_body(QT_KERNEL_ARGS) {
   int* nry = nrx + smax;                      // smax
   int* ncnt = nry + smax;                     // smax
   int* tmp1 = ncnt + smax;                    // smax
-  __shared__ int wtmp[4];
-  __shared__ int s_flag;
+  // wide form: a second child array (4*smax, qt_lds_wide) so the next pass's
+  // counts are zeroed inside this pass (one barrier less per pass)
+  constexpr bool DB = NT >= 1024;
+  int* const child2 = DB ? tmp1 + smax : child;
+  __shared__ int wtmp[NT / 64];
+  __shared__ int s_flag[2];
 
   uint32_t* keys = qkeys + (size_t)f * qk_stride + L.qk_off;
   int32_t* node = qnode + (size_t)f * qk_stride + L.qk_off;
@@ -1224,13 +1232,18 @@ __device__ __forceinline__ void qt_body(QT_KERNEL_ARGS) {
   // gather vToDistributeKeys (cell-major, raster within cell)
   const int nc = U.ncells;
   const uint32_t* fcc = ccount + (size_t)f * ncells_total + U.cell_begin;
-  for (int i = tid; i < nc; i += 256) cell_off[i] = (int)fcc[i];
+  // the cells' slot offsets are loaded beside their counts (independent
+  // loads), so a key's gather below is one dependent global load, not two
+  for (int i = tid; i < nc; i += NT) {
+    cell_off[i] = (int)fcc[i];
+    cell_slot[i] = cells[U.cell_begin + i].slot_off;
+  }
   __syncthreads();
-  const int C = block_scan_excl(cell_off, nc, wtmp);
+  const int C = block_scan_excl<NT>(cell_off, nc, wtmp);
   if (tid == 0) cell_off[nc] = C;
   __syncthreads();
   const uint32_t* fslots = slots + (size_t)f * slot_stride;
-  // keys k = tid + 256 j (j < QJ) and their node ids live in registers for
+  // keys k = tid + NT j (j < QJ) and their node ids live in registers for
   // the whole distribution (every pass walks all keys twice: from global
   // memory that was a load-latency chain per pass); more keys than that
   // spill to the global scratch.  keys[] in global memory also serves the
@@ -1239,18 +1252,18 @@ __device__ __forceinline__ void qt_body(QT_KERNEL_ARGS) {
   int nr[QJ];
 #pragma unroll
   for (int j = 0; j < QJ; ++j) {
-    const int k = tid + 256 * j;
+    const int k = tid + NT * j;
     kr[j] = 0u;
     nr[j] = -1;
     if (k < C) {
       const int c = upper_bound_i(cell_off, nc, k) - 1;
-      kr[j] = fslots[cells[U.cell_begin + c].slot_off + (k - cell_off[c])];
+      kr[j] = fslots[cell_slot[c] + (k - cell_off[c])];
       keys[k] = kr[j];
     }
   }
-  for (int k = tid + 256 * QJ; k < C; k += 256) {
+  for (int k = tid + NT * QJ; k < C; k += NT) {
     const int c = upper_bound_i(cell_off, nc, k) - 1;
-    keys[k] = fslots[cells[U.cell_begin + c].slot_off + (k - cell_off[c])];
+    keys[k] = fslots[cell_slot[c] + (k - cell_off[c])];
   }
   __syncthreads();  // cell_off is dead: its LDS becomes the node arrays
 #if defined(QT_PROBE_STOP) && QT_PROBE_STOP == 1  // profiling only: the gather alone
@@ -1260,10 +1273,10 @@ __device__ __forceinline__ void qt_body(QT_KERNEL_ARGS) {
   auto for_keys = [&](auto&& body) {  // body(k, key, node&)
 #pragma unroll
     for (int j = 0; j < QJ; ++j) {
-      const int k = tid + 256 * j;
+      const int k = tid + NT * j;
       if (k < C) body(k, kr[j], nr[j]);
     }
-    for (int k = tid + 256 * QJ; k < C; k += 256) {
+    for (int k = tid + NT * QJ; k < C; k += NT) {
       int n = node[k];
       body(k, keys[k], n);
       node[k] = n;
@@ -1272,12 +1285,16 @@ __device__ __forceinline__ void qt_body(QT_KERNEL_ARGS) {
   // initial nodes (:230-252)
   const int nIni = L.nini;
   int S = nIni;
-  for (int i = tid; i < nIni; i += 256) {
+  for (int i = tid; i < nIni; i += NT) {
     rx[i] = (int)(L.hX * (float)i) | ((int)(L.hX * (float)(i + 1)) << 16);
     ry[i] = 0 | (L.Hr << 16);
     cnt[i] = 0;
   }
   __syncthreads();
+  if (DB) {  // the first pass's child counts and flag (the fast pass zeroes the next ones)
+    for (int i = tid; i < 4 * min(nIni, smax); i += NT) child[i] = 0;
+    if (tid == 0) s_flag[0] = 0;
+  }
   for_keys([&](int, uint32_t key, int& n) {
     n = -1;
     if (nIni > 0) {
@@ -1290,6 +1307,29 @@ __device__ __forceinline__ void qt_body(QT_KERNEL_ARGS) {
   __syncthreads();
 
   int newS = 0;
+  int* chc = child;  // this pass's child array (DB: alternates with child2)
+  int* chn = child2;
+  // fast passes: each key's child slot (4 n + quadrant, or 4 n for a
+  // single-key node; -1 none) and whether it counts, from one batch of node
+  // reads (one LDS round trip, not one per key); kept for the reassignment
+  int tq[QJ];
+  uint32_t split = 0;
+  bool pre = false;
+  auto qt_targets = [&]() {
+    split = 0;
+#pragma unroll
+    for (int j = 0; j < QJ; ++j) {
+      tq[j] = -1;
+      if (NT * j >= C) continue;  // wave-uniform: key slots past the level's keys cost nothing
+      const int n = nr[j], ns = max(n, 0);
+      const int c = cnt[ns], x = rx[ns], y = ry[ns];
+      tq[j] = n < 0 ? -1 : c >= 2 ? 4 * n + quadrant(kr[j], x, y, L.key_xs) : 4 * n;
+      split |= (n >= 0 && c >= 2 ? 1u : 0u) << j;
+    }
+#pragma unroll
+    for (int j = 0; j < QJ; ++j)
+      if ((split >> j) & 1u) atomicAdd(&chc[tq[j]], 1);
+  };
   for (int pass = 0;; ++pass) {
 #ifdef QT_PROBE_MAXPASS  // profiling only: stop after this many passes (wrong keypoints)
     if (pass >= QT_PROBE_MAXPASS) break;
@@ -1299,14 +1339,102 @@ __device__ __forceinline__ void qt_body(QT_KERNEL_ARGS) {
       newS = 0;
       break;
     }
-    for (int i = tid; i < 4 * S; i += 256) child[i] = 0;
-    if (tid == 0) s_flag = 0;
+    int& flag = s_flag[DB ? (pass & 1) : 0];
+    if (DB && S <= NT && C <= NT * QJ) {
+      // ---- fast pass (one node per thread, 3 barriers).  The child counts
+      // (chc, zeroed by the previous pass) were issued at the end of the
+      // previous pass (or just below for the first); then per node in
+      // reverse order (thread t = node S-1-t, the scan order of tmp1 in the
+      // general pass) the packed count, its wave scan and the cross-wave
+      // offsets straight from registers: no scan array, no second scan
+      // barrier; then the children; then each key's new node, read from its
+      // kept slot, and the next pass's counts in the same phase.
+      if (!pre) qt_targets();
+      __syncthreads();
+      const int i = S - 1 - tid;
+      int cn = 0, v = 0;
+      if (i >= 0) {
+        cn = cnt[i];
+        int nch = 0;
+        if (cn >= 2) nch = (chc[4 * i] > 0) + (chc[4 * i + 1] > 0) + (chc[4 * i + 2] > 0) + (chc[4 * i + 3] > 0);
+        v = (nch << 16) | (cn == 1);
+      }
+      const int incl = wave_incl_scan(v);
+      const int wave = tid >> 6;
+      if ((tid & 63) == 63) wtmp[wave] = incl;
+      // the next pass's counts (<= 4 children per node) and flag: their last
+      // readers were before this pass's first barrier
+      for (int j = tid; j < 4 * min(4 * S, smax); j += NT) chn[j] = 0;
+      if (tid == 0) s_flag[(pass + 1) & 1] = 0;
+      __syncthreads();
+      int woff = 0, tot = 0;
+#pragma unroll
+      for (int w = 0; w < NT / 64; ++w) {
+        const int x = wtmp[w];
+        woff += w < wave ? x : 0;
+        tot += x;
+      }
+      const int excl = woff + incl - v;
+      const int totC = tot >> 16, totK = tot & 0xFFFF;
+      newS = totC + totK;
+      if (i >= 0) {
+        if (cn >= 2) {
+          int pos = excl >> 16;
+          for (int q = 3; q >= 0; --q) {
+            const int cc = chc[4 * i + q];
+            if (cc > 0) {
+              if (pos < smax) {
+                int crx, cry;
+                child_rect(rx[i], ry[i], q, &crx, &cry);
+                nrx[pos] = crx;
+                nry[pos] = cry;
+                ncnt[pos] = cc;
+              }
+              if (cc >= 2) flag = 1;
+              chc[4 * i + q] = pos++;
+            } else {
+              chc[4 * i + q] = -1;
+            }
+          }
+        } else if (cn == 1) {
+          const int pos = totC + totK - (excl & 0xFFFF) - 1;
+          if (pos < smax) {
+            nrx[pos] = rx[i];
+            nry[pos] = ry[i];
+            ncnt[pos] = 1;
+          }
+          chc[4 * i] = pos;
+        }
+      }
+      __syncthreads();
+#pragma unroll
+      for (int j = 0; j < QJ; ++j)
+        if (NT * j < C) nr[j] = tq[j] >= 0 ? chc[tq[j]] : -1;
+      const bool finish = (newS >= L.N) || (flag == 0);
+      if (finish) {
+        __syncthreads();  // the tail reuses chc's LDS
+        break;
+      }
+      int* t = rx; rx = nrx; nrx = t;
+      t = ry; ry = nry; nry = t;
+      t = cnt; cnt = ncnt; ncnt = t;
+      t = chc; chc = chn; chn = t;
+      S = newS;
+      // the next pass's counts right away (new node arrays written before
+      // the barrier above; chc zeroed in this pass's second phase)
+      pre = S <= NT;
+      if (pre) qt_targets();
+      continue;
+    }
+    int* const child = chc;  // the general pass (any S)
+    for (int i = tid; i < 4 * S; i += NT) child[i] = 0;
+    if (tid == 0) flag = 0;
     __syncthreads();
     for_keys([&](int, uint32_t key, int& n) {
       if (n >= 0 && cnt[n] >= 2) atomicAdd(&child[4 * n + quadrant(key, rx[n], ry[n], L.key_xs)], 1);
     });
     __syncthreads();
-    for (int i = tid; i < S; i += 256) {
+    for (int i = tid; i < S; i += NT) {
       const int cn = cnt[i];
       int nch = 0;
       if (cn >= 2) nch = (child[4 * i] > 0) + (child[4 * i + 1] > 0) + (child[4 * i + 2] > 0) + (child[4 * i + 3] > 0);
@@ -1317,10 +1445,10 @@ __device__ __forceinline__ void qt_body(QT_KERNEL_ARGS) {
       tmp1[S - 1 - i] = (nch << 16) | (cn == 1);
     }
     __syncthreads();
-    const int tot = block_scan_excl(tmp1, S, wtmp);
+    const int tot = block_scan_excl<NT>(tmp1, S, wtmp);
     const int totC = tot >> 16, totK = tot & 0xFFFF;
     newS = totC + totK;
-    for (int i = tid; i < S; i += 256) {
+    for (int i = tid; i < S; i += NT) {
       const int cn = cnt[i];
       if (cn >= 2) {
         int pos = tmp1[S - 1 - i] >> 16;
@@ -1334,7 +1462,7 @@ __device__ __forceinline__ void qt_body(QT_KERNEL_ARGS) {
               nry[pos] = cry;
               ncnt[pos] = cc;
             }
-            if (cc >= 2) s_flag = 1;
+            if (cc >= 2) flag = 1;
             child[4 * i + q] = pos++;
           } else {
             child[4 * i + q] = -1;
@@ -1354,18 +1482,10 @@ __device__ __forceinline__ void qt_body(QT_KERNEL_ARGS) {
     for_keys([&](int, uint32_t key, int& n) {
       if (n >= 0) n = (cnt[n] >= 2) ? child[4 * n + quadrant(key, rx[n], ry[n], L.key_xs)] : child[4 * n];
     });
-    const bool finish = (newS >= L.N) || (s_flag == 0);
+    const bool finish = (newS >= L.N) || (flag == 0);
     __syncthreads();
     if (finish) break;
-#ifdef QT_COPY_NODES  // profiling variant: copy the new node arrays back (one more barrier per pass)
-    for (int i = tid; i < newS; i += 256) {
-      rx[i] = nrx[i];
-      ry[i] = nry[i];
-      cnt[i] = ncnt[i];
-    }
-    S = newS;
-    __syncthreads();
-#else
+
     // ping-pong: the new node arrays become the current ones (every read of
     // the old ones is before the barrier above; the next pass writes the
     // other set only after its first barrier)
@@ -1373,7 +1493,6 @@ __device__ __forceinline__ void qt_body(QT_KERNEL_ARGS) {
     t = ry; ry = nry; nry = t;
     t = cnt; cnt = ncnt; ncnt = t;
     S = newS;
-#endif
   }
 #if defined(QT_PROBE_STOP) && QT_PROBE_STOP == 2  // profiling only: gather + passes
   if (tid == 0) lcount[(size_t)f * nlevels + l] = 0;
@@ -1385,14 +1504,14 @@ __device__ __forceinline__ void qt_body(QT_KERNEL_ARGS) {
     if (tid == 0) atomicOr(err, ORBX_DEVERR_QTCAP);
     newS = 0;
   }
-  for (int i = tid; i < newS; i += 256) best[i] = 0u;
+  for (int i = tid; i < newS; i += NT) best[i] = 0u;
   __syncthreads();
   for_keys([&](int k, uint32_t key, int& n) {
     if (n >= 0 && n < newS) atomicMax(&best[n], ((key & 0xFFu) << 24) | (0xFFFFFFu - (uint32_t)k));
   });
   __syncthreads();
   uint32_t* out = qout + (size_t)f * qout_stride + L.kout_off;
-  for (int i = tid; i < newS; i += 256) {
+  for (int i = tid; i < newS; i += NT) {
     const uint32_t k = 0xFFFFFFu - (best[i] & 0xFFFFFFu);
     out[i] = keys[k];
   }
@@ -1411,28 +1530,33 @@ __device__ __forceinline__ void qt_body(QT_KERNEL_ARGS) {
 #endif
     uint32_t* bm = reinterpret_cast<uint32_t*>(nrx);
     int* pc = rx;
-    for (int w = tid; w < nw; w += 256) bm[w] = 0u;
+    for (int w = tid; w < nw; w += NT) bm[w] = 0u;
     __syncthreads();
-    for (int i = tid; i < newS; i += 256) {
+    for (int i = tid; i < newS; i += NT) {
       const uint32_t k = 0xFFFFFFu - (best[i] & 0xFFFFFFu);
       atomicOr(&bm[k >> 5], 1u << (k & 31));
     }
     __syncthreads();
-    for (int w = tid; w < nw; w += 256) pc[w] = __popc(bm[w]);
+    for (int w = tid; w < nw; w += NT) pc[w] = __popc(bm[w]);
     __syncthreads();
-    block_scan_excl(pc, nw, wtmp);
-    for (int i = tid; i < newS; i += 256) {
+    block_scan_excl<NT>(pc, nw, wtmp);
+    for (int i = tid; i < newS; i += NT) {
       const uint32_t k = 0xFFFFFFu - (best[i] & 0xFFFFFFu);
       perm[pc[k >> 5] + __popc(bm[k >> 5] & ((1u << (k & 31)) - 1u))] = (uint32_t)i;
     }
   } else {
-    for (int i = tid; i < newS; i += 256) perm[i] = (uint32_t)i;
+    for (int i = tid; i < newS; i += NT) perm[i] = (uint32_t)i;
   }
   if (tid == 0) lcount[(size_t)f * nlevels + l] = newS;
 }
 
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k_quadtree(QT_KERNEL_ARGS) {
-  qt_body<8>(QT_KERNEL_PASS);
+  qt_body<8, 256>(QT_KERNEL_PASS);
+}
+// single-frame / small-batch calls (a grid of a few workgroups, the level-0
+// one sets the latency): 1024 threads walk the keys and the node lists
+__global__ __launch_bounds__(1024) void k_quadtree_wide(QT_KERNEL_ARGS) {
+  qt_body<8, 1024>(QT_KERNEL_PASS);
 }
 #ifndef QT_JSMALL
 #define QT_JSMALL 6 /* keys per thread in registers below 1 Mpx levels */
@@ -1441,7 +1565,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
 #define QT_WPE_SMALL 8
 #endif
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(QT_WPE_SMALL))) void k_quadtree_j6(QT_KERNEL_ARGS) {
-  qt_body<QT_JSMALL>(QT_KERNEL_PASS);
+  qt_body<QT_JSMALL, 256>(QT_KERNEL_PASS);
 }
 
 // ---------------------------------------------------------------------------

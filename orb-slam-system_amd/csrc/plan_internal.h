@@ -38,6 +38,7 @@ struct orbx_plan {
   int* h_err = nullptr; /* pinned: orbx_plan_check reads the error word without a blocking copy */
   size_t pyr_stride = 0, blur_stride = 0, slot_stride = 0, qk_stride = 0, qout_stride = 0;
   size_t qt_lds = 0;
+  size_t qt_lds_wide = 0; /* k_quadtree_wide (single-frame calls): + a second child array */
   BriefArgs bargs;
   BlurArgs blargs;  /* level-blur mode: k_blur's tiles */
   int lb_auto = 0;  /* the planner's BRIEF blur choice: 1 = level blur (k_blur + k_orient_brief_lb) */

@@ -117,7 +117,7 @@ def test_release_library_reads_no_profiling_knobs():
     (ADVICE r5)."""
     blob = open(os.path.join(PKG, "liborbx.so"), "rb").read()
     for knob in (b"ORBX_DEBUG_STOP", b"ORBX_DEBUG_OBDIV", b"ORBX_CHUNK", b"ORBX_DEBUG_OVERLAP",
-                 b"ORBX_DEBUG_SMDIV", b"ORBX_DEBUG_PYR_TILE", b"ORBX_DEBUG_PYR_MAXSEG", b"ORBX_DEBUG_CCAP"):
+                 b"ORBX_DEBUG_SMDIV", b"ORBX_DEBUG_PYR_TILE", b"ORBX_DEBUG_PYR_MAXSEG", b"ORBX_DEBUG_CCAP", b"ORBX_DEBUG_QT_WIDE"):
         assert knob not in blob, knob
     assert b"orbx_debug_set_fast_ccap" in blob
 

@@ -20,7 +20,7 @@ int main(int argc, char** argv) {
   }
   for (const PyrSeg& g : P.segs) {
     long long comp = 0, own = 0;
-    printf("segment: %d levels, %d x %d tiles, LDS %d + %d B\n", g.nl, g.ntx, g.nty, g.lds_a, g.lds_b);
+    printf("segment: %d levels, %d x %d tiles, LDS %d + %d + yl %d B\n", g.nl, g.ntx, g.nty, g.lds_a, g.lds_b, g.lds_yl);
     for (int s = 0; s <= g.nl; ++s) {
       long long c = 0, o = 0;
       for (int tx = 0; tx < g.ntx; ++tx)
