@@ -242,6 +242,19 @@ static bool try_segment(Plan& P, const std::vector<int>& lev, int TW, int TH, Py
   }
   if (a + b + 8 * (bx + by) > ORBX_PYR_LDS_MAX) return false;
   memset(&g, 0, sizeof(g));
+  /* one LDS pitch per level for every tile (the widest tile column's): the
+   * row LUT then holds final LDS offsets, shared by all tile columns; the
+   * buffers above were sized with it (max pitch x max rows) */
+  for (int s = 0; s < ns; ++s) {
+    long long m = 0;
+    for (int tx = 0; tx < ntx; ++tx) {
+      const Iv& x = xs[(size_t)s * ntx + tx];
+      if (x.chi <= x.clo) continue;
+      m = std::max(m, s == 0 ? (long long)(((x.chi + 15) & ~15) - (x.clo & ~15))
+                             : (long long)((x.chi - (x.clo & ~3) + 3) >> 2) * 4);
+    }
+    g.lpitch[s] = (int)m;
+  }
   g.nl = ns - 1;
   g.ntx = ntx;
   g.nty = nty;
@@ -299,8 +312,13 @@ static bool build_blobs(Plan& P, const std::vector<int>& lev, PyrSeg& g, const s
           if (cf[0] < 0 || cf[0] > 4095 || cf[1] < 0 || cf[1] > 4095) return false;
           if (isx && ((d - b) & 3) == 0) glo = lo;
           if (isx && hi - glo > 7) return false;
-          if (!isx)
-            P.pyr_blob.push_back((uint32_t)(lo - origin) | ((uint32_t)(hi - origin) << 16));
+          if (!isx) { /* LDS byte offsets of the two source rows (< 64 KiB) */
+            const uint32_t base = ((s - 1) & 1) ? (uint32_t)g.lds_a : 0u;
+            const uint32_t o0 = base + (uint32_t)(lo - origin) * (uint32_t)g.lpitch[s - 1];
+            const uint32_t o1 = base + (uint32_t)(hi - origin) * (uint32_t)g.lpitch[s - 1];
+            if (o0 > 0xFFFF || o1 > 0xFFFF) return false;
+            P.pyr_blob.push_back(o0 | (o1 << 16));
+          }
           else if (((d - b) & 3) == 0) /* group column 0: s0 | (sx1 - s0) << 16 */
             P.pyr_blob.push_back((uint32_t)(lo - origin) | ((uint32_t)(hi - lo) << 16));
           else /* columns 1..3: k_pyramid's v_perm selector, bytes relative to s0 */

@@ -200,24 +200,23 @@ __global__ __launch_bounds__(256) void k_pyramid(const uint8_t* __restrict__ fra
   int bx, f;
   frame_unit(bx, f);
   const int tx = bx % S.ntx, ty = bx / S.ntx;
-  uint8_t* cur = plds;
-  uint8_t* nxt = plds + S.lds_a;
   // the column LUT is read once per level and thread: straight from global
   // memory (L2); the row LUT, read every row iteration, is staged in LDS
   // (keeping the column LUT out of LDS raises occupancy from 5 to 7
-  // workgroups per CU at 1080p)
+  // workgroups per CU at 1080p).  Row entries hold the LDS byte offsets of
+  // their two source rows: every tile lays a level out at the same pitch
+  // (PyrSeg::lpitch), so the planner writes final offsets.
   const uint2* xl = reinterpret_cast<const uint2*>(blob) + bo[S.xbo_off + tx];
-  uint2* yl = reinterpret_cast<uint2*>(plds + S.lds_a + S.lds_b);
   {
+    uint2* yl = reinterpret_cast<uint2*>(plds + S.lds_a + S.lds_b);
     const int y0 = bo[S.ybo_off + ty], ny = (bo[S.ybo_off + ty + 1] - y0) >> 1;
     const uint4* yb = blob + (y0 >> 1);
     for (int i = tid; i < ny; i += 256) reinterpret_cast<uint4*>(yl)[i] = yb[i];
   }
   // ---- stage the source region (level lev[0]) ----
   int4 X = xs[S.xs_off + tx], Y = ys[S.ys_off + ty];
-  int cay = Y.x, cax = X.x & ~15;
-  int cpitch = ((X.y + 15) & ~15) - cax;
   {
+    const int cay = Y.x, cax = X.x & ~15, cpitch = S.lpitch[0];
     const uint8_t* src;
     size_t sp;
 #ifdef PYR_PROBE_SAMESRC  // profiling only: every frame stages frame 0's source region
@@ -235,13 +234,13 @@ __global__ __launch_bounds__(256) void k_pyramid(const uint8_t* __restrict__ fra
     const int nr = Y.y - Y.x;
     const uintptr_t al = reinterpret_cast<uintptr_t>(src) | (uintptr_t)sp;
     const uint8_t* s0 = src + (size_t)cay * sp;
-    if ((al & 15) == 0) {
-      stage_region<v4u, 4, 256>(cur, cpitch, s0 + cax, sp, nr, cpitch >> 4, tid);
+    if ((al & 15) == 0) {  // this tile's own 16-B columns (the pitch may be wider)
+      stage_region<v4u, 4, 256>(plds, cpitch, s0 + cax, sp, nr, (((X.y + 15) & ~15) - cax) >> 4, tid);
     } else if ((al & 3) == 0) {
       const int d0 = (X.x & ~3) - cax, nd = (((X.y + 3) & ~3) - (X.x & ~3)) >> 2;
-      stage_region<uint32_t, 8, 256>(cur + d0, cpitch, s0 + cax + d0, sp, nr, nd, tid);
+      stage_region<uint32_t, 8, 256>(plds + d0, cpitch, s0 + cax + d0, sp, nr, nd, tid);
     } else {
-      stage_rows_u32<8, 256>(cur, cpitch, s0 + cax, sp, nr, X.y - cax, tid);
+      stage_rows_u32<8, 256>(plds, cpitch, s0 + cax, sp, nr, X.y - cax, tid);
     }
   }
   __syncthreads();
@@ -254,29 +253,29 @@ __global__ __launch_bounds__(256) void k_pyramid(const uint8_t* __restrict__ fra
     const int dax = X.x & ~3;
     const int ncg = X.y > X.x ? (X.y - dax + 3) >> 2 : 0;
     const int nrows = max(Y.y - Y.x, 0);
-    const int dpitch = 4 * ncg;
+    const uint32_t dpitch = (uint32_t)S.lpitch[s];
     if (ncg > 0 && nrows > 0) {
       // tid / ncg and 256 / ncg through the float reciprocal: exact for
       // integers <= 256.5 (relative error ~1e-7 against a margin >= 0.5 / ncg)
       const float rcp = __builtin_amdgcn_rcpf((float)ncg);
-      const int R = (int)(256.5f * rcp);
+      const int R = __builtin_amdgcn_readfirstlane((int)(256.5f * rcp));
       if (tid < R * ncg) {
         const int r0 = (int)(((float)tid + 0.5f) * rcp), cg = tid - r0 * ncg;
         // the 4 columns' source bytes lie in an 8-byte window from sx[0]
         // (scale < 2: sx1[3] - sx[0] <= 7, checked by the planner): two
-        // v_alignbyte of three LDS dwords per source row, then one v_perm
-        // (bytes sx, sx1 -> u16 pair) and one v_dot2_u32_u16 with the
-        // (a0, a1) pair per column: D = S[sx]*a0 + S[sx1]*a1
+        // v_alignbyte of three LDS dwords per source row (one unaligned
+        // ds_read_b64 instead: 0.685 -> 1.20 ms, c4), then one v_perm (bytes
+        // sx, sx1 -> u16 pair) and one v_dot2_u32_u16 with the (a0, a1) pair
+        // per column: D = S[sx]*a0 + S[sx1]*a1
         // blob (geometry.cpp build_blobs): column 0 of the group holds
         // s0 | (sx1 - s0) << 16, columns 1..3 their v_perm selectors
         // relative to s0; .y = a0 | a1 << 16, both in [0, 2048]
         uint32_t hsel[4], hcoef[4];
-        int hbase, hsh;
+        uint32_t hbase, hsh;
         {
           const uint2 e0 = xl[xo + 4 * cg];
-          const int s0 = (int)(e0.x & 0xFFFF);
-          hbase = s0 & ~3;
-          hsh = s0 & 3;
+          hbase = (e0.x & 0xFFFCu) + lds_addr(plds);  // LDS byte address of the window's first dword
+          hsh = e0.x & 3u;
           hsel[0] = (e0.x & 0xFFFF0000u) | 0x0C000C00u;
           hcoef[0] = e0.y;
 #pragma unroll
@@ -287,71 +286,82 @@ __global__ __launch_bounds__(256) void k_pyramid(const uint8_t* __restrict__ fra
           }
         }
         const int gx0 = dax + 4 * cg;
-        const bool any_x = gx0 + 4 > X.z && gx0 < X.w;
-        uint8_t* gdst = pyr + (size_t)f * pstride + S.off[s];
+        // HBM stores through a buffer resource over the level: a group
+        // holding no owned column gets an offset past num_records, so its
+        // stores are dropped by the range check (no per-row branch)
+        const bool own = PYR_STORE_ON && gx0 + 4 > X.z && gx0 < X.w;
         const int gp = S.pitch[s];
-        // PYR_U rows per iteration: every LDS read of the group is issued
-        // before the first store (cur/nxt alias as far as the compiler knows)
-        for (int rb = r0; rb < nrows; rb += PYR_U * R) {
-          uint32_t packed[PYR_U];
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            pyr + (size_t)f * pstride + S.off[s], 0, gp * S.h[s], 0x00020000);
+        const uint32_t gbase = own ? (uint32_t)(Y.x * gp + gx0) : 0xC0000000u;
+        const uint32_t lbase = (uint32_t)((s & 1) ? S.lds_a : 0) + 4u * (uint32_t)cg;  // from plds
+        const uint32_t ylb = __builtin_amdgcn_readfirstlane((uint32_t)(S.lds_a + S.lds_b) + 8u * (uint32_t)yo);
+        // wave-uniform trip count (the wave's first active lane has its
+        // smallest row): lanes past the level's last row recompute and
+        // re-store that row (same bytes), so the loop needs no exec masking
+        const int nm1 = nrows - 1;
+        int rv = r0, rw = __builtin_amdgcn_readfirstlane(r0);
+        while (rw < nrows) {
+          const uint32_t r = (uint32_t)min(rv, nm1);
+          rv += R;
+          rw = __builtin_amdgcn_readfirstlane(rw + R);  // a separate scalar trip counter (opaque: not folded into rv)
+          const uint2 e = *reinterpret_cast<const uint2*>(plds + (ylb + 8u * r));
+          // SDWA halves of the entry: hbase + off0 / off1, b0 << 12 / b1 << 12
+          // (the u24 multiply reads the low 24 bits: b0's shift needs no mask)
+          uint32_t a0, a1, bs0, bs1;
+          asm("v_add_u32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_0"
+              : "=v"(a0) : "v"(hbase), "v"(e.x));
+          asm("v_add_u32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1"
+              : "=v"(a1) : "v"(hbase), "v"(e.x));
+          bs0 = e.y << 12;
+          asm("v_lshlrev_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1"
+              : "=v"(bs1) : "v"(12u), "v"(e.y));
+          typedef const __attribute__((address_space(3))) uint32_t* lds_u32p;
+          const lds_u32p R0 = (lds_u32p)(size_t)a0, R1 = (lds_u32p)(size_t)a1;
+          const uint32_t lo0 = __builtin_amdgcn_alignbyte(R0[1], R0[0], hsh);
+          const uint32_t hi0 = __builtin_amdgcn_alignbyte(R0[2], R0[1], hsh);
+          const uint32_t lo1 = __builtin_amdgcn_alignbyte(R1[1], R1[0], hsh);
+          const uint32_t hi1 = __builtin_amdgcn_alignbyte(R1[2], R1[1], hsh);
+          uint32_t v[4];
 #pragma unroll
-          for (int u = 0; u < PYR_U; ++u) {
-            const int r = min(rb + u * R, nrows - 1);
-            const uint2 e = yl[yo + r];
+          for (int k = 0; k < 4; ++k) {
             // vertical: ((b*(D>>4))>>16) == mulhi_u24(b << 12, D & ~15)
             // (b <= 2048, D <= 255*2048: both operands < 2^24, exact)
-            const uint64_t b0s = (uint64_t)((e.y & 0xFFFu) << 12), b1s = (uint64_t)(((e.y >> 16) & 0xFFFu) << 12);
-            const uint32_t* R0 = reinterpret_cast<const uint32_t*>(cur + __mul24((int)(e.x & 0xFFFF), cpitch) + hbase);
-            const uint32_t* R1 = reinterpret_cast<const uint32_t*>(cur + __mul24((int)(e.x >> 16), cpitch) + hbase);
-            const uint32_t lo0 = __builtin_amdgcn_alignbyte(R0[1], R0[0], hsh);
-            const uint32_t hi0 = __builtin_amdgcn_alignbyte(R0[2], R0[1], hsh);
-            const uint32_t lo1 = __builtin_amdgcn_alignbyte(R1[1], R1[0], hsh);
-            const uint32_t hi1 = __builtin_amdgcn_alignbyte(R1[2], R1[1], hsh);
-            uint32_t v[4];
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-              const uint32_t d0 = __builtin_amdgcn_udot2(as_us2(__builtin_amdgcn_perm(hi0, lo0, hsel[k])),
-                                                         as_us2(hcoef[k]), 0u, false);
-              const uint32_t d1 = __builtin_amdgcn_udot2(as_us2(__builtin_amdgcn_perm(hi1, lo1, hsel[k])),
-                                                         as_us2(hcoef[k]), 0u, false);
-              const uint32_t t0 = (uint32_t)((b0s * (uint64_t)(d0 & 0xFFFFF0u)) >> 32);
-              const uint32_t t1 = (uint32_t)((b1s * (uint64_t)(d1 & 0xFFFFF0u)) >> 32);
-              v[k] = (t0 + t1 + 2u) >> 2;
-            }
-            packed[u] = __builtin_amdgcn_perm(v[1], v[0], 0x0C0C0400u) | __builtin_amdgcn_perm(v[3], v[2], 0x04000C0Cu);
+            const uint32_t d0 = __builtin_amdgcn_udot2(as_us2(__builtin_amdgcn_perm(hi0, lo0, hsel[k])),
+                                                       as_us2(hcoef[k]), 0u, false);
+            const uint32_t d1 = __builtin_amdgcn_udot2(as_us2(__builtin_amdgcn_perm(hi1, lo1, hsel[k])),
+                                                       as_us2(hcoef[k]), 0u, false);
+            // (operands from LDS: the 24-bit form is spelled out, the
+            // compiler would emit the quarter-rate v_mul_hi_u32)
+            uint32_t t0, t1;
+            asm("v_mul_hi_u32_u24 %0, %1, %2" : "=v"(t0) : "v"(bs0), "v"(d0 & 0xFFFFF0u));
+            asm("v_mul_hi_u32_u24 %0, %1, %2" : "=v"(t1) : "v"(bs1), "v"(d1 & 0xFFFFF0u));
+            v[k] = t0 + t1 + 2u;  // < 1024
           }
-#pragma unroll
-          for (int u = 0; u < PYR_U; ++u) {
-            const int r = rb + u * R;
-            if (r >= nrows) break;
-            const int y = Y.x + r;
-            *reinterpret_cast<uint32_t*>(nxt + r * dpitch + 4 * cg) = packed[u];
-            // every computed row, also the ones another tile owns: computed
-            // rows are exact, so their bytes equal the owner's (benign; no
-            // per-row ownership test: 0.679 -> 0.666 ms at c4)
-            if (PYR_STORE_ON && any_x) {
-              uint8_t* o = gdst + (uint32_t)(y * gp + gx0);  // a level is < 4 GB
-              // the whole group, also at the owned interval's edges: the
-              // planner computes every group holding an owned pixel whole, so
-              // the bytes this tile does not own carry the values their owner
-              // writes (or lie past the level's last column, in the row
-              // padding); no byte-store path (0.748 -> 0.66 ms at c4)
-              *reinterpret_cast<uint32_t*>(o) = packed[u];  // pyr offsets/pitches are 16-B multiples
-            }
-          }
+          // (v >> 2) of the four columns as bytes: two u16 pairs shifted as
+          // whole dwords (v < 1024: the pair's high value lands whole in
+          // bits 16..23), then one v_perm
+          uint32_t p01, p23;
+          asm("v_lshl_or_b32 %0, %1, 16, %2" : "=v"(p01) : "v"(v[1]), "v"(v[0]));
+          asm("v_lshl_or_b32 %0, %1, 16, %2" : "=v"(p23) : "v"(v[3]), "v"(v[2]));
+          p01 >>= 2;
+          p23 >>= 2;
+          const uint32_t packed = __builtin_amdgcn_perm(p23, p01, 0x06040200u);
+          *reinterpret_cast<uint32_t*>(plds + (lbase + __umul24(r, dpitch))) = packed;
+          // every computed row, also the ones another tile owns: computed
+          // rows are exact, so their bytes equal the owner's (benign); the
+          // whole group, also at the owned interval's edges: the planner
+          // computes every group holding an owned pixel whole, so the bytes
+          // this tile does not own carry the values their owner writes (or
+          // lie past the level's last column, in the row padding)
+          __builtin_amdgcn_raw_buffer_store_b32(packed, rs, gbase + __umul24(r, (uint32_t)gp), 0, 0);
         }
       }
     }
 #ifndef PYR_PROBE_NOSYNC  // profiling only: level passes without the block barrier (wrong pixels)
     __syncthreads();
 #endif
-    uint8_t* t = cur;
-    cur = nxt;
-    nxt = t;
-    cax = dax;
-    cay = Y.x;
-    cpitch = dpitch;
-    xo += dpitch;
+    xo += 4 * ncg;
     yo += nrows;
   }
 }

@@ -174,8 +174,9 @@ struct BriefArgs {
 #define ORBX_PYR_LDS_MAX 61440    /* + LUT blobs (below the 64 KiB default limit) */
 /* per tile column (row) a LUT blob of uint2 {src0 | src1 << 16, coef pair}
  * for every level s = 1..nl and every computed column c in [dax, dax+4*ncg)
- * (row in [clo, chi)), source positions relative to the LDS origin of level
- * s-1's region; blobs are padded to 16 B */
+ * (row in [clo, chi)); column sources relative to the LDS origin of level
+ * s-1's region, row sources as LDS byte offsets of the two source rows
+ * (ping-pong buffer + row * lpitch[s-1]); blobs are padded to 16 B */
 struct PyrSeg {
   int nl;
   int area;           /* 1: one exact-2x level by INTER_AREA (k_pyr_area2; nl = 1, no tiling) */
@@ -186,6 +187,7 @@ struct PyrSeg {
   int xbo_off, ybo_off; /* into the blob offset tables (ntx+1 / nty+1 entries) */
   int lev[ORBX_MAX_LEVELS], w[ORBX_MAX_LEVELS], h[ORBX_MAX_LEVELS], pitch[ORBX_MAX_LEVELS];
   int lut_x[ORBX_MAX_LEVELS], lut_y[ORBX_MAX_LEVELS];
+  int lpitch[ORBX_MAX_LEVELS];     /* LDS row pitch of level s's region, the same for every tile (max over tile columns) */
   long long off[ORBX_MAX_LEVELS]; /* pyr offset; -1 = the caller's frame (level 0) */
   int prio;                       /* 1: pyramid waves at ORBX_EX_PRIO (set at launch) */
 };

@@ -61,6 +61,8 @@ int main(int argc, char** argv) {
         int cax = X[0] & ~15, cay = Y[0], cpitch = ((X[1] + 15) & ~15) - cax;
         int cx0 = X[0], cx1 = X[1], cy0 = Y[0], cy1 = Y[1];
         if ((long long)cpitch * (cy1 - cy0) > g.lds_a) fail("lds_a", tx, ty);
+        if (cpitch > g.lpitch[0]) fail("lpitch 0", tx, cpitch);
+        if ((long long)g.lpitch[0] * (cy1 - cy0) > g.lds_a) fail("lds_a (uniform pitch)", tx, ty);
         std::vector<int> cur((size_t)cpitch * (cy1 - cy0), -1);
         for (int r = cy0; r < cy1; ++r)
           for (int c = cx0; c < cx1; ++c) {
@@ -73,13 +75,20 @@ int main(int argc, char** argv) {
           const int dax = X[0] & ~3, ncg = (X[1] - dax + 3) >> 2, nrows = Y[1] - Y[0];
           const int dpitch = 4 * ncg;
           if ((long long)dpitch * nrows > ((s & 1) ? g.lds_b : g.lds_a)) fail("lds", s, tx);
+          if (dpitch > g.lpitch[s] || (long long)g.lpitch[s] * nrows > ((s & 1) ? g.lds_b : g.lds_a))
+            fail("lds (uniform pitch)", s, tx);
           if (ncg > 256) fail("ncg", ncg, s);
           std::vector<int> nxt((size_t)std::max(dpitch * nrows, 1), -1);
           const LevelInfo& lv = P.levels[g.lev[s]];
           for (int r = 0; r < nrows; ++r) {
             const int y = Y[0] + r;
             const uint32_t* ye = &P.pyr_blob[2 * (yb + yo + r)];
-            const int ry0 = ye[0] & 0xFFFF, ry1 = ye[0] >> 16;
+            // row entries: LDS byte offsets of the two source rows in level
+            // s-1's buffer (k_pyramid's uniform pitch g.lpitch[s-1])
+            const int lbase = ((s - 1) & 1) ? g.lds_a : 0, lp = g.lpitch[s - 1];
+            const int o0 = (int)(ye[0] & 0xFFFF) - lbase, o1 = (int)(ye[0] >> 16) - lbase;
+            if (lp <= 0 || o0 < 0 || o1 < 0 || o0 % lp || o1 % lp) fail("yblob offset", s, y);
+            const int ry0 = o0 / lp, ry1 = o1 / lp;
             const int b0 = (int16_t)(ye[1] & 0xFFFF), b1 = (int16_t)(ye[1] >> 16);
             {  // blob vs the LUTs it packs
               const int sy = P.yofs[g.lut_y[s] + y], shm1 = g.h[s - 1] - 1;
