@@ -149,8 +149,9 @@ int orbx_extractor_level_host(orbx_extractor* e, int level, const uint8_t** data
                               int* width, int* height);
 
 /* Call statistics of an extractor since creation: calls of orbx_extract and
- * the calls whose keypoint count exceeded the speculative result copy (a
- * second D2H round trip). */
+ * the calls that needed a second D2H round trip for their results (always 0
+ * since round 6: one kernel writes exactly the frame's rows into the pinned
+ * staging; kept for ABI compatibility). */
 int orbx_extractor_stats(orbx_extractor* e, long long* calls, long long* refetches);
 
 /* ---------------------------------------------------------------------------

@@ -32,6 +32,8 @@ __global__ void k_quadtree(const LevelInfo*, const CellInfo*, const uint32_t*, s
 __global__ void k_quadtree_j6(const LevelInfo*, const CellInfo*, const uint32_t*, size_t,
                               const uint32_t*, int, uint32_t*, int32_t*, size_t, uint32_t*, size_t,
                               int*, int, int, int, int*, uint32_t*);
+__global__ void k_pack_results(const int*, const int*, const uint32_t*, const uint32_t*, int, uint32_t*, uint32_t);
+static_assert(sizeof(orbx_keypoint) == 28, "k_pack_results copies 7-dword keypoint rows");
 __global__ void k_quadtree_wide(const LevelInfo*, const CellInfo*, const uint32_t*, size_t,
                                 const uint32_t*, int, uint32_t*, int32_t*, size_t, uint32_t*, size_t,
                                 int*, int, int, int, int*, uint32_t*);
@@ -700,7 +702,7 @@ static void extractor_release_plan(orbx_extractor* e) {
   if (e->ev_pyr) hipEventDestroy(e->ev_pyr);
   if (e->s_copy) hipStreamDestroy(e->s_copy);
   e->plan = nullptr; e->d_img = nullptr; e->d_kps = nullptr; e->d_desc = nullptr;
-  e->d_count = nullptr; e->h_res = nullptr; e->W = e->H = 0; e->have_frame = false;
+  e->d_count = nullptr; e->h_res = nullptr; e->d_res = nullptr; e->W = e->H = 0; e->have_frame = false;
   e->h_img = nullptr; e->h_pyr = nullptr; e->ev_pyr = nullptr; e->s_copy = nullptr;
   e->pyr_bytes = 0; e->host_pyr = false;
 }
@@ -717,6 +719,7 @@ static int extractor_prepare(orbx_extractor* e, int W, int H) {
       dev_alloc((void**)&e->d_count, sizeof(int)) ||
       hipHostMalloc((void**)&e->h_res, 64 + (sizeof(orbx_keypoint) + 32) * kcap,
                     hipHostMallocDefault) != hipSuccess ||
+      hipHostGetDevicePointer((void**)&e->d_res, e->h_res, 0) != hipSuccess ||
       hipHostMalloc((void**)&e->h_img, (size_t)W * H, hipHostMallocDefault) != hipSuccess) {
     extractor_release_plan(e);
     return ORBX_ERR_HIP;
@@ -803,9 +806,28 @@ extern "C" int orbx_extract(orbx_extractor* e, const uint8_t* img, int W, int H,
       ORBX_TRY(hipMemcpyAsync(e->d_img + (size_t)r0 * W, h, (size_t)nr * W, hipMemcpyHostToDevice, s));
     }
   }
+  // one launch writes the count, the error word and exactly the frame's
+  // rows into the pinned staging (k_pack_results, over PCIe)
+  const int kcap = std::max(p->P.kcap, 1);
+  const int* h_hdr = reinterpret_cast<const int*>(e->h_res);  // {count, error word}
+  orbx_keypoint* h_kps = reinterpret_cast<orbx_keypoint*>(e->h_res + 64);
+  uint8_t* h_desc = e->h_res + 64 + sizeof(orbx_keypoint) * (size_t)kcap;
+  auto chain = [&]() -> int {
+    const int r = orbx_plan_extract(p, e->d_img, 1, (size_t)W * H, (size_t)W, e->d_kps, e->d_desc,
+                                    e->d_count, s);
+    if (r) return r;
+    hipLaunchKernelGGL(k_pack_results, dim3(std::min((kcap * 8 + 255) / 256, 64)), dim3(256), 0, s,
+                       p->d_err, e->d_count, reinterpret_cast<const uint32_t*>(e->d_kps),
+                       reinterpret_cast<const uint32_t*>(e->d_desc), kcap, reinterpret_cast<uint32_t*>(e->d_res),
+                       (uint32_t)((64 + sizeof(orbx_keypoint) * (size_t)kcap) / 4));
+    return hipGetLastError() == hipSuccess ? ORBX_OK : ORBX_ERR_HIP;
+  };
+  // (the chain captured once as a HIP graph and replayed was measured: no
+  // change in the call's latency, p50 174-176 us either way in the probe --
+  // the gap after the upload is the pageable copy's completion, not the
+  // host's launches; not kept)
   p->ev_after_pyr = to_host ? e->ev_pyr : nullptr;
-  rc = orbx_plan_extract(p, e->d_img, 1, (size_t)W * H, (size_t)W, e->d_kps, e->d_desc,
-                         e->d_count, s);
+  rc = chain();
   p->ev_after_pyr = nullptr;
   if (rc) return rc;
   if (to_host && e->pyr_bytes) {
@@ -814,19 +836,7 @@ extern "C" int orbx_extract(orbx_extractor* e, const uint8_t* img, int W, int H,
     ORBX_TRY(hipStreamWaitEvent(e->s_copy, e->ev_pyr, 0));
     ORBX_TRY(hipMemcpyAsync(e->h_pyr, p->d_pyr, e->pyr_bytes, hipMemcpyDeviceToHost, e->s_copy));
   }
-  // one round trip in the common case: the error word, the count and a
-  // speculative prefix of the rows (sized by the previous call) come back
-  // together into pinned staging; only a larger frame needs a second copy
-  const int kcap = std::max(p->P.kcap, 1);
-  const int guess = std::min(kcap, e->last_k + e->last_k / 4 + 64);
-  int* h_cnt = reinterpret_cast<int*>(e->h_res);
-  orbx_keypoint* h_kps = reinterpret_cast<orbx_keypoint*>(e->h_res + 64);
-  uint8_t* h_desc = e->h_res + 64 + sizeof(orbx_keypoint) * (size_t)kcap;
-  ORBX_TRY(hipMemcpyAsync(p->h_err, p->d_err, sizeof(int), hipMemcpyDeviceToHost, s));
-  ORBX_TRY(hipMemcpyAsync(h_cnt, e->d_count, sizeof(int), hipMemcpyDeviceToHost, s));
-  ORBX_TRY(hipMemcpyAsync(h_kps, e->d_kps, sizeof(orbx_keypoint) * (size_t)guess,
-                          hipMemcpyDeviceToHost, s));
-  ORBX_TRY(hipMemcpyAsync(h_desc, e->d_desc, 32 * (size_t)guess, hipMemcpyDeviceToHost, s));
+
   if (to_host && !(e->flags & ORBX_EXTRACTOR_PINNED_H2D)) {
     // level 0 (= level 1) of the host pyramid: a host copy of the caller's
     // rows made while the GPU works (the thread would only wait), instead of
@@ -839,25 +849,17 @@ extern "C" int orbx_extract(orbx_extractor* e, const uint8_t* img, int W, int H,
   }
   ORBX_TRY(stream_wait(s));
   if (to_host) ORBX_TRY(stream_wait(e->s_copy));
-  if (*p->h_err) {
+  if (h_hdr[1]) {
     rc = orbx_plan_check(p, s); /* resets the device error word */
     e->have_frame = false;
     return rc ? rc : ORBX_ERR_CAPACITY;
   }
   e->have_frame = true;
   e->host_pyr = to_host;
-  const int K = *h_cnt;
+  const int K = h_hdr[0];
   *n = K;
   if (K == 0) return ORBX_OK; /* keypoints untouched, descriptors released (:460-463) */
   if (K > cap || !kps || !desc) return ORBX_ERR_CAPACITY;
-  if (K > guess) {
-    ++e->n_refetch;
-    ORBX_TRY(hipMemcpyAsync(h_kps + guess, e->d_kps + guess,
-                            sizeof(orbx_keypoint) * (size_t)(K - guess), hipMemcpyDeviceToHost, s));
-    ORBX_TRY(hipMemcpyAsync(h_desc + 32 * (size_t)guess, e->d_desc + 32 * (size_t)guess,
-                            32 * (size_t)(K - guess), hipMemcpyDeviceToHost, s));
-    ORBX_TRY(stream_wait(s));
-  }
   e->last_k = K;
   memcpy(kps, h_kps, sizeof(orbx_keypoint) * (size_t)K);
   memcpy(desc, h_desc, 32 * (size_t)K);

@@ -72,9 +72,11 @@ struct orbx_extractor {
   orbx_keypoint* d_kps = nullptr;
   uint8_t* d_desc = nullptr;
   int* d_count = nullptr;
-  /* pinned result staging: [count | kps rows | desc rows] (kcap rows each) */
+  /* pinned result staging: [count, error word | kps rows | desc rows] (64-B
+   * header, kcap rows each), written by k_pack_results through d_res */
   uint8_t* h_res = nullptr;
-  int last_k = 0; /* keypoints of the previous call: sizes the speculative copy */
+  uint8_t* d_res = nullptr;  /* h_res's device address */
+  int last_k = 0; /* keypoints of the previous call */
   bool have_frame = false;
   int flags = 0;             /* ORBX_EXTRACTOR_* */
   uint8_t* h_img = nullptr;  /* pinned staging of the caller's image (= host level 0) */
@@ -83,7 +85,7 @@ struct orbx_extractor {
   hipStream_t s_copy = nullptr; /* pyramid D2H, overlapped with FAST .. BRIEF */
   hipEvent_t ev_pyr = nullptr;
   bool host_pyr = false;     /* the last call filled h_img / h_pyr */
-  long long n_calls = 0, n_refetch = 0;
+  long long n_calls = 0, n_refetch = 0; /* n_refetch: always 0 (k_pack_results writes exactly K rows) */
   void* stereo = nullptr; /* orbs_plan of orbx_stereo_match (api_stereo.hip) */
 };
 
