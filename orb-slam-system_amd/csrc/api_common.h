@@ -158,6 +158,10 @@ int set_max_dynamic_lds(const void* kernel, int device);
 // ORBM_STAGE_KERNEL, else a DMA copy.  bytes: a multiple of 16 (Carve's
 // 256-byte blocks)
 int stage_in(void* d, const void* h, size_t bytes, hipStream_t s);
+// its results [.., + bytes) from the device arena d back into the pinned
+// staging h (device-accessible host memory): the copy kernel writing host
+// memory when ORBM_STAGE_KERNEL, else a DMA copy.  bytes: a multiple of 16
+int stage_out(void* h, const void* d, size_t bytes, hipStream_t s);
 
 }  // namespace orbx
 

@@ -314,7 +314,8 @@ static int bow_search(const orbx_bow_frame* kf1, const orbx_bow_frame* kf2, floa
                reinterpret_cast<const int*>(d + o_loff), s, nullptr,
                upper_bytes_zero(kf1->desc, kf1->n) && upper_bytes_zero(kf2->desc, kf2->n));
   if (hipGetLastError() != hipSuccess) return ORBX_ERR_HIP;
-  ORBX_TRY(hipMemcpyAsync(h + in_end, d + in_end, out_end - in_end, hipMemcpyDeviceToHost, s));
+  rc2 = stage_out(h + in_end, d + in_end, out_end - in_end, s);
+  if (rc2) return rc2;
   ORBX_TRY(stream_wait(s));
   memcpy(match12, h + o_m12, n1 * 4);
   memcpy(nmatches, h + o_nm, sizeof(int));
@@ -396,7 +397,8 @@ extern "C" int orbm_descriptor_distance_batch(const uint8_t* a, int na, const ui
                      reinterpret_cast<const int32_t*>(d + o_ib), npairs,
                      reinterpret_cast<int32_t*>(d + o_d));
   if (hipGetLastError() != hipSuccess) return ORBX_ERR_HIP;
-  ORBX_TRY(hipMemcpyAsync(h + o_d, d + o_d, (size_t)npairs * 4, hipMemcpyDeviceToHost, s));
+  rc = stage_out(h + o_d, d + o_d, out_end - o_d, s);
+  if (rc) return rc;
   ORBX_TRY(stream_wait(s));
   memcpy(dist, h + o_d, (size_t)npairs * 4);
   return ORBX_OK;

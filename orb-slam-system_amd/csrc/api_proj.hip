@@ -126,7 +126,7 @@ extern "C" int orbm_search_by_projection(int mode, const orbx_proj_frame* F,
   if (stage_in(d, h, in_end, s)) return ORBX_ERR_HIP;
   launch_proj(dp, 1, n, nq, mode, nnratio, th_dist, check_ori, s);
   if (hipGetLastError() != hipSuccess) return ORBX_ERR_HIP;
-  ORBX_TRY(hipMemcpyAsync(h + in_end, d + in_end, out_end - in_end, hipMemcpyDeviceToHost, s));
+  if (stage_out(h + in_end, d + in_end, out_end - in_end, s)) return ORBX_ERR_HIP;
   ORBX_TRY(stream_wait(s));
   memcpy(match, h + o_match, (size_t)n * 4);
   memcpy(nmatches, h + o_nm, sizeof(int));

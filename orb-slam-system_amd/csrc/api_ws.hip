@@ -124,6 +124,20 @@ int stage_in(void* d, const void* h, size_t bytes, hipStream_t s) {
 #endif
 }
 
+int stage_out(void* h, const void* d, size_t bytes, hipStream_t s) {
+#if ORBM_STAGE_KERNEL
+  // the same copy kernel, the pinned buffer as the destination: the GPU
+  // writes the results over PCIe, no DMA copy and its completion handover
+  const size_t n16 = bytes / 16;
+  if (n16 == 0) return ORBX_OK;
+  hipLaunchKernelGGL(k_stage_in, dim3((unsigned)std::min<size_t>((n16 + 255) / 256, 1024)), dim3(256), 0, s,
+                     reinterpret_cast<uint4*>(h), reinterpret_cast<const uint4*>(d), n16);
+  return hipGetLastError() == hipSuccess ? ORBX_OK : ORBX_ERR_HIP;
+#else
+  return hipMemcpyAsync(h, d, bytes, hipMemcpyDeviceToHost, s) == hipSuccess ? ORBX_OK : ORBX_ERR_HIP;
+#endif
+}
+
 int set_max_dynamic_lds(const void* kernel, int device) {
   std::lock_guard<std::mutex> g(g_attr_mu);
   if (!g_attr) g_attr = new std::map<std::pair<const void*, int>, int>();
