@@ -27,6 +27,11 @@ EXTRACT_CASES = [
     (4096, 400, 2000, 8, "empty", "noise", 40),
     (5000, 720, 3000, 8, "empty", "rects", 41),
     (600, 4400, 2000, 8, "empty", "noise", 42),
+    # single frames with more than 1024 quadtree nodes at level 0: the wide
+    # single-frame quadtree (k_quadtree_wide) switches from its fast pass to
+    # the general pass mid-distribution
+    (1920, 1080, 12000, 8, "empty", "noise", 43),
+    (1920, 1080, 12000, 8, "empty", "rects", 44),
 ]
 
 
