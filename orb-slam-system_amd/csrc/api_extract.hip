@@ -249,6 +249,13 @@ extern "C" int orbx_plan_create(const orbx_params* prm, int width, int height, i
   for (StripInfo& si : p->P.strips) {
     si.pitch = si.level == 0 ? 0 : p->largs.pitch[si.level];
     si.off = si.level == 0 ? 0 : p->largs.pyr_off[si.level];
+    // the kernel's staging decisions for a 16-B-aligned base, made here
+    // once (fs_kernel's general branch makes the same test at run time)
+    si.lead16 = si.x & 15;
+    const int cg0 = (si.lead16 + 3) >> 2, cg1 = (si.lead16 + si.w) >> 2;
+    const int cgb = cg0 - (((si.lead16 + 3) & 3) != 3 ? 1 : 0);
+    si.cw16 = si.colwalk && si.h - 6 <= (FS_NT / 64) * FS_CW_RMAX && cg1 - cgb <= 63;
+    si.soff16 = si.level == 0 ? 0 : si.off + (long long)si.y * si.pitch + (si.x - si.lead16);
   }
   // plans with a pyramid run its waves and FAST's at a raised issue
   // priority (ORBX_EX_PRIO): measured in the pipelined step, c4 +1.4-2.3 %,
@@ -450,11 +457,15 @@ static int extract_pass(orbx_plan* p, const uint8_t* frames, int n, size_t fstri
   uint32_t* const d_qout = p->d_qout + f0 * p->qout_stride;
   int* const d_lcount = p->d_lcount + f0 * (size_t)L;
   // strips [strip0, strip1) of launch group g
+  // the call's level-0 alignment (k_fast_strips takes the planner's staging
+  // decisions when the frames are 16-B aligned)
+  LevelArgs la = p->largs;
+  la.l0al16 = ((reinterpret_cast<uintptr_t>(frames) | (uintptr_t)fstride | (uintptr_t)rstride) & 15) == 0;
   auto fast_launch = [&](int g, int strip0, int strip1, hipStream_t st) {
     if (strip1 <= strip0) return;
     const orbx_plan::FsGroup& G = p->fs_grp[g];
     hipLaunchKernelGGL(p->fs_tpitch == 288 ? k_fast_strips_p288 : k_fast_strips, dim3((unsigned)(strip1 - strip0), n), dim3(FS_NT), G.lds + p->pad_fast, st,
-                       frames, fstride, rstride, d_pyr, p->pyr_stride, p->largs, p->d_cells,
+                       frames, fstride, rstride, d_pyr, p->pyr_stride, la, p->d_cells,
                        p->d_strips, d_slots, p->slot_stride, d_ccount, P.ncells, P.ini_th,
                        P.min_th, p->fs_tpitch, G.tmaxh, G.mcells, G.ccap,
                        p->d_err + ORBX_ERRW_FAST_OVF, strip0, p->dbg);

@@ -502,7 +502,7 @@ __device__ __forceinline__ int wave_excl_scan(int n, int lane, int* total) {
 #define FS_L1CAP (FS_L1FLUSH + 256) /* per-wave cardinal survivors: < FS_L1FLUSH carried + <= 256 new */
 #define FS_L2CAP 128 /* per-wave even-test survivors: < 64 carried + <= 64 new */
 #ifndef FS_CW_RMAX
-#define FS_CW_RMAX 8 /* column walk: band rows per wave (registers hold FS_CW_RMAX + 6 rows) */
+/* FS_CW_RMAX: orbx_internal.h (the planner's column-walk test uses it too) */
 #endif
 
 
@@ -1074,27 +1074,41 @@ __device__ __forceinline__ void fs_kernel(
 #else
   const int fsrc = f;
 #endif
-  const uint8_t* base = st.level == 0 ? frames + (size_t)fsrc * fstride : pyr + (size_t)fsrc * pstride + st.off;
   const int slot_pref = tid < st.ncells ? cells[st.cell_begin + tid].slot_off : 0;  // in flight
-  const uintptr_t alb = reinterpret_cast<uintptr_t>(base) | (uintptr_t)pitch;
-  const bool aligned = (alb & 3) == 0;
-  const bool aligned16 = (alb & 15) == 0;
-  const int xal = aligned16 ? (st.x & ~15) : aligned ? (st.x & ~3) : st.x;
-  const int lead = st.x - xal;          // tile col of global st.x
-  const int tw = lead + st.w;           // columns in use
-  const uint8_t* s0 = base + (size_t)st.y * pitch + xal;
-  // column walk (fs_strip_body): dword-aligned rows, band rows <= 4 waves x
-  // FS_CW_RMAX, and the band's dword columns plus both halo dwords within
-  // the 64 lanes (every strip of the bench workloads but wCell-32 levels),
-  // on levels the planner marks (st.colwalk: wide levels, where it measured
-  // faster; block staging on the narrow ones)
+  bool aligned, aligned16, cw;
+  int xal, lead;
+  const uint8_t* s0;
+  if (st.level != 0 || LA.l0al16) {
+    // 16-B-aligned level base (the common case): the planner's lead, column
+    // walk decision and pyramid offset (StripInfo::lead16 / cw16 / soff16)
+    aligned = aligned16 = true;
+    lead = st.lead16;
+    xal = st.x - lead;
+    s0 = st.level == 0 ? frames + ((size_t)fsrc * fstride + (size_t)st.y * rstride + (size_t)xal)
+                       : pyr + ((size_t)fsrc * pstride + (size_t)st.soff16);
+    cw = FS_NW == 4 && st.cw16;
+  } else {
+    const uint8_t* base = frames + (size_t)fsrc * fstride;
+    const uintptr_t alb = reinterpret_cast<uintptr_t>(base) | (uintptr_t)pitch;
+    aligned = (alb & 3) == 0;
+    aligned16 = (alb & 15) == 0;
+    xal = aligned16 ? (st.x & ~15) : aligned ? (st.x & ~3) : st.x;
+    lead = st.x - xal;  // tile col of global st.x
+    s0 = base + (size_t)st.y * pitch + xal;
+    // column walk (fs_strip_body): dword-aligned rows, band rows <= 4 waves x
+    // FS_CW_RMAX, and the band's dword columns plus both halo dwords within
+    // the 64 lanes (every strip of the bench workloads but wCell-32 levels),
+    // on levels the planner marks (st.colwalk: wide levels, where it measured
+    // faster; block staging on the narrow ones); api_extract.hip makes the
+    // same test for StripInfo::cw16
+    const int cg0 = (lead + 3) >> 2, cg1 = (lead + st.w) >> 2;
+    const int cgb = cg0 - (((lead + 3) & 3) != 3 ? 1 : 0);
+    cw = FS_NW == 4 && st.colwalk && aligned && st.h - 6 <= FS_NW * FS_CW_RMAX && cg1 - cgb <= 63;
+  }
 #ifdef FS_NO_COLWALK  // profiling variant: block-wide staging for every strip
-  const bool cw = false;
-#else
-  const int cg0 = (lead + 3) >> 2, cg1 = (lead + st.w) >> 2;
-  const int cgb = cg0 - (((lead + 3) & 3) != 3 ? 1 : 0);
-  const bool cw = FS_NW == 4 && st.colwalk && aligned && st.h - 6 <= FS_NW * FS_CW_RMAX && cg1 - cgb <= 63;
+  cw = false;
 #endif
+  const int tw = lead + st.w;  // columns in use
   if (!cw) {
     if (aligned16) stage_region<v4u, 4, FS_NT>(tile, tpitch, s0, pitch, st.h, (tw + 15) >> 4, tid);
     else if (aligned) stage_region<uint32_t, 12, FS_NT>(tile, tpitch, s0, pitch, st.h, (tw + 3) >> 2, tid);

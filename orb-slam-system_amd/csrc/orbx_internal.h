@@ -80,6 +80,13 @@ struct StripInfo {
   int colwalk;    /* planner's choice of k_fast_strips' column walk (when it applies) */
   int pitch;      /* row pitch of the level's storage; 0 = level 0 (the call's row stride) */
   long long off;  /* byte offset of the level in the per-frame pyramid buffer (level > 0) */
+  /* k_fast_strips' staging for a 16-B-aligned level base (every pyramid
+   * level; level 0 when the call's frames are, LevelArgs::l0al16), set by
+   * the planner so the kernel skips its alignment and column-walk tests:
+   * the tile's lead columns (x & 15), the column-walk decision, and the
+   * tile's first byte in the per-frame pyramid buffer (level > 0) */
+  int lead16, cw16;
+  long long soff16;
 };
 
 /* per-level storage of the pyramid, passed by value to kernels that only
@@ -96,6 +103,7 @@ struct LevelArgs {
   int pitch[ORBX_MAX_LEVELS];
   int key_xs; /* orbx_pack_key shift */
   int prio;   /* 1: FAST waves at ORBX_EX_PRIO */
+  int l0al16; /* per launch: the call's frames, frame and row strides are 16-B aligned */
 };
 #define ORBX_STRIP_MAXCELLS 64 /* cells per FAST strip (>= 256 / min cell width) */
 
@@ -111,6 +119,9 @@ struct StereoArgs {
 };
 #ifndef FS_NT
 #define FS_NT 256 /* threads per k_fast_strips workgroup (one strip) */
+#endif
+#ifndef FS_CW_RMAX
+#define FS_CW_RMAX 8 /* column walk: band rows per wave (registers hold FS_CW_RMAX + 6 rows) */
 #endif
 #ifndef FS_CCAP
 #define FS_CCAP 1024 /* per-strip corner list (overflow falls back to a map scan); the plan may take
