@@ -57,6 +57,23 @@ def test_extract_matches_oracle(gpu, oracle, w, h, nf, L, guard, kind, idx):
         assert np.array_equal(ex.level(l), ref.level(l)), "pyramid level %d" % l
 
 
+def test_extract_calls_of_changing_size(gpu, oracle):
+    """Consecutive drop-in calls whose keypoint counts jump (none, dense,
+    sparse, dense again): k_pack_results writes exactly each call's rows
+    into the pinned staging, so no call sees a previous call's rows or
+    count, and the second-trip statistic stays 0."""
+    ref = oracle.Extractor(2000, 1.2, 8, 20, 7, cell_guard="empty")
+    ex = gpu.Extractor(2000, 1.2, 8, 20, 7, cell_guard="empty")
+    for i, kind in enumerate(("flat", "noise", "pan", "flat", "noise")):
+        img = synth.frame(1920, 1080, 120 + i, kind)
+        k, d = ex.extract(img)
+        rk, rd = ref.extract(img)
+        _cmp_kps(k, rk, "call %d (%s)" % (i, kind))
+        assert np.array_equal(d, rd), "call %d (%s): descriptors differ" % (i, kind)
+    st = ex.stats()
+    assert st["calls"] == 5 and st["refetches"] == 0
+
+
 @pytest.mark.parametrize("w,h,nf,guard", [(640, 480, 1000, "strict"), (1920, 1080, 2000, "empty"),
                                            (642, 361, 1000, "strict")])
 def test_extractor_options_match_oracle(gpu, oracle, w, h, nf, guard):
