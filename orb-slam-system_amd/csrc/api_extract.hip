@@ -32,7 +32,7 @@ __global__ void k_quadtree(const LevelInfo*, const CellInfo*, const uint32_t*, s
 __global__ void k_quadtree_j6(const LevelInfo*, const CellInfo*, const uint32_t*, size_t,
                               const uint32_t*, int, uint32_t*, int32_t*, size_t, uint32_t*, size_t,
                               int*, int, int, int, int*, uint32_t*);
-__global__ void k_pack_results(const int*, const int*, const uint32_t*, const uint32_t*, int, uint32_t*, uint32_t);
+__global__ void k_pack_results(const int*, const int*, const uint4*, const uint4*, int, uint4*, uint32_t);
 static_assert(sizeof(orbx_keypoint) == 28, "k_pack_results copies 7-dword keypoint rows");
 __global__ void k_quadtree_wide(const LevelInfo*, const CellInfo*, const uint32_t*, size_t,
                                 const uint32_t*, int, uint32_t*, int32_t*, size_t, uint32_t*, size_t,
@@ -725,10 +725,10 @@ static int extractor_prepare(orbx_extractor* e, int W, int H) {
   if (rc) return rc;
   const size_t kcap = (size_t)std::max(e->plan->P.kcap, 1);
   if (dev_alloc((void**)&e->d_img, (size_t)W * H) ||
-      dev_alloc((void**)&e->d_kps, sizeof(orbx_keypoint) * kcap) ||
+      dev_alloc((void**)&e->d_kps, sizeof(orbx_keypoint) * kcap + 16) ||  /* + k_pack_results' last 16-B chunk */
       dev_alloc((void**)&e->d_desc, 32 * kcap) ||
       dev_alloc((void**)&e->d_count, sizeof(int)) ||
-      hipHostMalloc((void**)&e->h_res, 64 + (sizeof(orbx_keypoint) + 32) * kcap,
+      hipHostMalloc((void**)&e->h_res, 64 + 16 + (sizeof(orbx_keypoint) + 32) * kcap,
                     hipHostMallocDefault) != hipSuccess ||
       hipHostGetDevicePointer((void**)&e->d_res, e->h_res, 0) != hipSuccess ||
       hipHostMalloc((void**)&e->h_img, (size_t)W * H, hipHostMallocDefault) != hipSuccess) {
@@ -823,15 +823,17 @@ extern "C" int orbx_extract(orbx_extractor* e, const uint8_t* img, int W, int H,
   const int kcap = std::max(p->P.kcap, 1);
   const int* h_hdr = reinterpret_cast<const int*>(e->h_res);  // {count, error word}
   orbx_keypoint* h_kps = reinterpret_cast<orbx_keypoint*>(e->h_res + 64);
-  uint8_t* h_desc = e->h_res + 64 + sizeof(orbx_keypoint) * (size_t)kcap;
+  // descriptor rows at a 16-B boundary (k_pack_results copies 16 B per lane)
+  const size_t desc_off = (64 + sizeof(orbx_keypoint) * (size_t)kcap + 15) & ~(size_t)15;
+  uint8_t* h_desc = e->h_res + desc_off;
   auto chain = [&]() -> int {
     const int r = orbx_plan_extract(p, e->d_img, 1, (size_t)W * H, (size_t)W, e->d_kps, e->d_desc,
                                     e->d_count, s);
     if (r) return r;
     hipLaunchKernelGGL(k_pack_results, dim3(std::min((kcap * 8 + 255) / 256, 64)), dim3(256), 0, s,
-                       p->d_err, e->d_count, reinterpret_cast<const uint32_t*>(e->d_kps),
-                       reinterpret_cast<const uint32_t*>(e->d_desc), kcap, reinterpret_cast<uint32_t*>(e->d_res),
-                       (uint32_t)((64 + sizeof(orbx_keypoint) * (size_t)kcap) / 4));
+                       p->d_err, e->d_count, reinterpret_cast<const uint4*>(e->d_kps),
+                       reinterpret_cast<const uint4*>(e->d_desc), kcap, reinterpret_cast<uint4*>(e->d_res),
+                       (uint32_t)(desc_off / 16));
     return hipGetLastError() == hipSuccess ? ORBX_OK : ORBX_ERR_HIP;
   };
   // (the chain captured once as a HIP graph and replayed was measured: no

@@ -129,23 +129,24 @@ __global__ __launch_bounds__(256) void k_boundary_copy(const uint8_t* __restrict
 // GPU over PCIe in one launch -- the exact K is known here, so no
 // speculative prefix and no second copy, and no chain of small D2H copies
 // (each a blit launch and a completion signal: 4 copies took ~37 us of a
-// 1080p call, round 6).  dword stores; K <= kcap; the rows are 28 / 32 B.
+// 1080p call, round 6).  16-B stores: the keypoint rows (28 B each) as one
+// contiguous run of K * 28 bytes (the device buffer is 16-B aligned and
+// sized for kcap rows, so the last 16-B chunk reads at most 12 bytes of
+// the next row, never past the buffer), the descriptor rows at the 16-B
+// aligned offset desc_q16 (in 16-B units).
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_pack_results(const int* __restrict__ d_err,
                                                       const int* __restrict__ d_count,
-                                                      const uint32_t* __restrict__ kps,
-                                                      const uint32_t* __restrict__ desc, int kcap,
-                                                      uint32_t* __restrict__ h_res, uint32_t desc_dw_off) {
+                                                      const uint4* __restrict__ kps,
+                                                      const uint4* __restrict__ desc, int kcap,
+                                                      uint4* __restrict__ h_res, uint32_t desc_q16) {
   const int err = *d_err, cnt = *d_count;
   const int K = err ? 0 : min(max(cnt, 0), kcap);
   const int tid = (int)(blockIdx.x * 256 + threadIdx.x), nt = (int)(gridDim.x * 256);
-  if (tid == 0) {
-    h_res[0] = (uint32_t)cnt;
-    h_res[1] = (uint32_t)err;
-  }
-  const int nk = K * 7, nd = K * 8;  // dwords: orbx_keypoint is 7 dwords, a descriptor 8
-  for (int i = tid; i < nk; i += nt) h_res[16 + i] = kps[i];
-  for (int i = tid; i < nd; i += nt) h_res[desc_dw_off + i] = desc[i];
+  if (tid == 0) h_res[0] = make_uint4((uint32_t)cnt, (uint32_t)err, 0u, 0u);
+  const int nk = (K * 28 + 15) >> 4, nd = K * 2;  // 16-B chunks: keypoint rows (7 dwords each), descriptors
+  for (int i = tid; i < nk; i += nt) h_res[4 + i] = kps[i];
+  for (int i = tid; i < nd; i += nt) h_res[desc_q16 + i] = desc[i];
 }
 
 }  // namespace orbx
