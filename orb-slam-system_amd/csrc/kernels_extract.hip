@@ -697,7 +697,10 @@ __device__ __forceinline__ void fs_strip_body(
       // each compare's ballot around its store and the list end advances by
       // one s_lshl1_add per append: 13 scalar instructions per group of 4
       // pixels instead of 28 (a store with no active lane writes nothing).
-      {
+      // The whole group's appends are skipped when no lane has a survivor
+      // (one compare and a branch; c4 FAST 1.08 -> 1.05 ms, c1 / c5 -2 %,
+      // c2 +2 %: its 640x480 frames leave few survivor-free wave groups).
+      if (__ballot((clo | chi) != 0u)) {
         const unsigned long long b0 = __ballot((uint16_t)clo != 0), b1 = __ballot((uint16_t)chi != 0),
                                  b2 = __ballot(clo > 0xFFFFu), b3 = __ballot(chi > 0xFFFFu);
         const uint32_t p0 = (uint32_t)lanes_below(b0), p1 = (uint32_t)lanes_below(b1),
