@@ -911,18 +911,23 @@ __device__ __forceinline__ void fs_strip_body(
   auto nms_pixel = [&](int r, int c, int a) {
     const int k = min((int)(((float)(c - c0) + 0.5f) * rwcell), st.ncells - 1);
     const int cb0 = c0 + k * wcell, cb1 = (k == st.ncells - 1) ? c1 : cb0 + wcell;
-    int nbm = 0, nbi = 0;  // max neighbour score at min / ini threshold (0 outside the band)
-#pragma unroll
-    for (int dy = -1; dy <= 1; ++dy)
-#pragma unroll
-      for (int dx = -1; dx <= 1; ++dx) {
-        if (!dx && !dy) continue;
-        const int rr = r + dy, cc = c + dx;
-        int aq = 0;
-        if (rr >= 3 && rr < 3 + bh && cc >= cb0 && cc < cb1) aq = amap[rr * tpitch + cc];
-        nbm = max(nbm, aq > min_th ? aq - 1 : 0);
-        nbi = max(nbi, aq > ini_th ? aq - 1 : 0);
-      }
+    // the neighbours' largest strength first: the per-threshold score
+    // a > th ? a - 1 : 0 is non-decreasing in a, so its maximum over the
+    // neighbours is the score of their maximum (one max per neighbour
+    // instead of two compares, two selects and two max; c1 / c2 FAST -1 %)
+    // branch-free: the 8 reads issued together at offsets clamped into the
+    // band / cell (an outside neighbour reads the centre row or column), the
+    // outside ones zeroed by selects.  The bounds-tested loop compiled to 8
+    // exec-masked reads, each waited for alone: FAST c4 1.064 -> 1.024 ms,
+    // c1 / c2 / c5 -2 to -3 %
+    const bool vu = r > 3, vd = r + 1 < 3 + bh, vl = c > cb0, vr = c + 1 < cb1;
+    const int ou = vu ? tpitch : 0, od = vd ? tpitch : 0, ol = vl ? 1 : 0, orr = vr ? 1 : 0;
+    const uint8_t* pc = amap + __mul24(r, tpitch) + c;
+    const int nu = pc[-ou], nd = pc[od], nl = pc[-ol], nr = pc[orr];
+    const int nul = pc[-ou - ol], nur = pc[orr - ou], ndl = pc[od - ol], ndr = pc[od + orr];
+    int mx = max(max(vu ? nu : 0, vd ? nd : 0), max(vl ? nl : 0, vr ? nr : 0));
+    mx = max(mx, max(max(vu && vl ? nul : 0, vu && vr ? nur : 0), max(vd && vl ? ndl : 0, vd && vr ? ndr : 0)));
+    const int nbm = max(0, mx > min_th ? mx - 1 : 0), nbi = max(0, mx > ini_th ? mx - 1 : 0);
     const unsigned long long bit = 1ull << (c - cb0);
     if (a > ini_th && a - 1 > nbi) {
       atomicOr(&mask[k * bh + (r - 3)], bit);
